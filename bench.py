@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""Benchmark of the LD-score hot path (BASELINE.json metric: SNP-pairs/s, chr1 N=315 599, 1 cM window).
+
+One step = one full `calculate` pass (repack + statistics + window schedule + band correlation kernel
++ finalize + results to host) over a chromosome-sized synthetic .bed image already resident in HBM
+(BASELINE.json configs[2]: N = 315 599, M = 80 000 over 280 cM, additive + dominance, --ld-wind-cm 1).
+With N GPUs (torchrun, one process per GPU, RCCL) every rank processes its own chromosome unit
+(weak scaling: position sharding across chromosomes has no hot-path exchange) and the per-SNP score
+tables are gathered to rank 0 over RCCL at the end of every step.
+
+Prints ONE JSON line on rank 0.  `roofline` is for the band correlation kernel (HIP events on the
+engine's stream, averaged over the timed steps); `cpu_baseline` times the C port of the reference's
+CPU path (oracle/, fp32 sdot per pair, OpenMP over window neighbours) on the first SNPs of the same
+chromosome (rank 0, N = 1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "SNP-pairs/sec + wall-clock, chr1 N=315k 1cM window, 1/2/4/8 MI355X"
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(bed_host: bytes, n_snp, n_org, w, maf, std_thr, rsq, pos, target_s=15.0):
+    """Time the C port of the reference CPU path on the first K SNPs (K sized for ~target_s)."""
+    from oracle import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    k0 = min(n_snp, 24)
+    t = time.perf_counter()
+    r0 = O.run_c(bed_host, n_snp, n_org, w, maf, std_thr, rsq, pos, end=k0, threads=threads)
+    t0 = time.perf_counter() - t
+    k = k0
+    if t0 < target_s:
+        k = int(min(n_snp, max(k0, k0 * target_s / max(t0, 1e-3))))
+    if k > k0:
+        t = time.perf_counter()
+        r0 = O.run_c(bed_host, n_snp, n_org, w, maf, std_thr, rsq, pos, end=k, threads=threads)
+        t0 = time.perf_counter() - t
+    ws = r0["l2_ws"][:k]
+    pairs = float(ws[ws > 0].sum())
+    return dict(value=pairs / t0, unit="SNP-pairs/s", cores=threads, kind="port",
+                sample=f"first {k} SNPs of the same chromosome (full sliding window from SNP 0), "
+                       f"{pairs:.0f} pairs in {t0:.2f} s, C port of the reference path (oracle/ldscore_oracle.c: "
+                       f"fp32 sdot + per-pair vector copies, OpenMP over neighbours)")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n-org", type=int, default=315_599)
+    ap.add_argument("--n-snp", type=int, default=80_000)
+    ap.add_argument("--length-cm", type=float, default=280.0)
+    ap.add_argument("--window-cm", type=float, default=1.0)
+    ap.add_argument("--maf", type=float, default=1e-4)
+    ap.add_argument("--std-thr", type=float, default=1e-5)
+    ap.add_argument("--additive-only", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+
+    from nldsc_amd import _lib, synth
+    from nldsc_amd.engine import Engine
+
+    N, M = args.n_org, args.n_snp
+    flags = _lib.FLAG_ADDITIVE_ONLY if args.additive_only else 0
+    t = time.perf_counter()
+    buf, pos = synth.device_bed(M, N, seed=7 + rank, length_cm=args.length_cm, device=local)
+    eng = Engine(local)
+    eng.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
+    bed_host = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        bed_host = buf.cpu().numpy().tobytes()
+    del buf
+    torch.cuda.empty_cache()
+    log(f"[rank {rank}] data ready ({(3 + M * ((N + 3) // 4)) / 1e9:.2f} GB .bed image) in "
+        f"{time.perf_counter() - t:.1f} s")
+    w, rsq = args.window_cm, 1.0 / M
+    out = None
+
+    def step():
+        nonlocal out
+        out = eng.run(w, args.maf, args.std_thr, rsq, pos, flags=flags, out=out)
+        if world > 1:  # assemble the score tables on rank 0 (RCCL over xGMI)
+            tab = torch.from_numpy(np.stack([out["l2"], out["l2d"], out["maf"], out["residuals_std"],
+                                             out["l2_ws"].astype(np.float64), out["l2d_ws"].astype(np.float64),
+                                             out["l2d_wse"].astype(np.float64)])).cuda()
+            gathered = torch.empty((world,) + tab.shape, dtype=tab.dtype, device=tab.device)
+            dist.all_gather_into_tensor(gathered, tab)
+        return eng.timings()
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tims = [step() for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    pairs_step = torch.tensor([tims[-1]["pairs"]], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(pairs_step, op=dist.ReduceOp.SUM)
+    t_max = float(el.item())
+    total_pairs = float(pairs_step.item()) * args.steps
+
+    res = None
+    if rank == 0:
+        band_ms = float(np.mean([x["band_ms"] for x in tims]))
+        flop = tims[-1]["flop_alg"]
+        achieved = flop / (band_ms * 1e-3) / 1e12
+        stages = {k: round(float(np.mean([x[k] for x in tims])), 3)
+                  for k in ("repack_ms", "stats_ms", "schedule_ms", "band_ms", "finalize_ms", "total_ms")}
+        ws = out["l2_ws"]
+        res = {
+            "metric": METRIC,
+            "value": total_pairs / t_max,
+            "unit": "SNP-pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * t_max / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (GPU-generated PLINK .bed, AR(1) haplotypes, 1% missing; one chromosome per GPU)",
+            "config": {
+                "workload": ("C3 (BASELINE.json configs[2]): chr1-like N=315599 individuals, M=%d SNPs over %.0f cM, "
+                             "%s, --ld-wind-cm %g, maf %g, std-thr %g, rsq 1/M" %
+                             (M, args.length_cm, "additive only" if args.additive_only else "additive+dominance",
+                              w, args.maf, args.std_thr)),
+                "n_org": N, "n_snp": M, "mean_window": float(ws[ws > 0].mean()),
+                "pairs_per_step_per_gpu": tims[-1]["pairs"],
+                "parallelism": f"position sharding, one chromosome unit per GPU x {world}",
+            },
+            "roofline": {
+                "bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                "kernel": "band_kernel<true> (v_mfma_f32_32x32x2_f32)",
+                "flop_alg_per_launch": flop, "avg_launch_ms": band_ms,
+            },
+            "stages_ms": stages,
+            "cpu_baseline": None,
+        }
+    if bed_host is not None:
+        log("[rank 0] timing the CPU baseline ...")
+        res["cpu_baseline"] = cpu_baseline(bed_host, M, N, w, args.maf, args.std_thr, rsq, pos,
+                                           target_s=args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

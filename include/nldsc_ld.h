@@ -1,0 +1,115 @@
+/*
+ * nldsc_ld.h — C ABI of the MI355X-native LD-score engine (libnldsc_amd.so).
+ *
+ * Drop-in boundary for bayarpark/nldsc's `_ldscore` extension:
+ *   - nldsc_ld_params  replaces  struct LDScoreParams   nldsc/ldscore/_ldscore/data.h:33-65
+ *   - nldsc_ld_result  replaces  struct LDScoreResult   nldsc/ldscore/_ldscore/data.h:21-31
+ *   - nldsc_ld_calculate replaces LDScoreResult calculate(LDScoreParams&)
+ *                                                       nldsc/ldscore/_ldscore/ldscalc.h:8
+ *     as bound by m.def("calculate", &calculate)        nldsc/ldscore/_ldscore/ldscore.cpp:53
+ * The pybind11 module `_ldscore` (nldsc_amd/csrc/ldscore_py.cpp) wraps exactly
+ * these entry points with the reference's Python signatures.
+ *
+ * The engine entry points below are the lower-level API used for device-resident
+ * inputs, repeated runs (benchmarks) and position sharding across GPUs.
+ *
+ * Plain C types only: pointers, sizes, ints and doubles.  All output arrays are
+ * caller-allocated with n_snp elements.  Every function returns NLDSC_OK (0) or
+ * a negative NLDSC_E_* code; when `err` is non-NULL a NUL-terminated message is
+ * written into it (at most errlen bytes).
+ */
+#ifndef NLDSC_LD_H
+#define NLDSC_LD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NLDSC_OK 0
+#define NLDSC_E_BAD_MAGIC (-1) /* "Invalid PLINK magic number..." (stream.h:88-102) -> ValueError */
+#define NLDSC_E_IO (-2)        /* cannot open / read the .bed file */
+#define NLDSC_E_SIZE (-3)      /* .bed shorter than 3 + n_snp * ceil(n_org / 4) bytes */
+#define NLDSC_E_ARG (-4)       /* invalid argument (sizes, NULL pointers, ranges) */
+#define NLDSC_E_HIP (-5)       /* HIP runtime error */
+#define NLDSC_E_OOM (-6)       /* device or host allocation failed */
+#define NLDSC_E_NODEV (-7)     /* no HIP device visible: there is no CPU fallback */
+
+/* flags */
+#define NLDSC_FLAG_STRICT_PLINK_ORDER 1u /* use PLINK sample order in the last .bed byte (reference
+                                            keeps the high n_org%4 bit pairs, stream.h:55-66) */
+#define NLDSC_FLAG_ADDITIVE_ONLY 2u      /* skip the dominance terms: l2d = NaN, l2d_ws = l2d_wse = -1 */
+
+typedef struct nldsc_ld_params {
+    const char* bedfile;      /* LDScoreParams::bedfile   (data.h:34) */
+    int32_t n_snp;            /* LDScoreParams::n_snp     (data.h:36) */
+    int32_t n_org;            /* LDScoreParams::n_org     (data.h:37) */
+    double ld_wind;           /* LDScoreParams::ld_wind   (data.h:39), same unit as positions */
+    const double* positions;  /* LDScoreParams::positions (data.h:40), n_snp values; < 0 = unused */
+    double maf;               /* LDScoreParams::maf       (data.h:42) */
+    double std_thr;           /* LDScoreParams::std_thr   (data.h:43) */
+    double rsq_thr;           /* LDScoreParams::rsq_thr   (data.h:44) */
+    uint32_t flags;           /* NLDSC_FLAG_* */
+    int32_t device;           /* HIP device ordinal; -1 = the calling thread's current device */
+} nldsc_ld_params;
+
+typedef struct nldsc_ld_result { /* LDScoreResult (data.h:21-31); n_snp elements each */
+    double* l2;              /* additive LD score; NaN for unused / MAF-failed SNPs */
+    double* l2d;             /* dominance LD score; NaN likewise */
+    double* maf;             /* MAF of every decoded SNP; NaN for unused SNPs */
+    double* residuals_std;   /* std of the dominance residual; NaN unless the SNP passed MAF */
+    int32_t* l2_ws;          /* window size (additive), -1 when not computed */
+    int32_t* l2d_ws;         /* neighbours with residual std > std_thr, -1 when not computed */
+    int32_t* l2d_wse;        /* ... of which r2adj > rsq_thr, -1 when not computed */
+} nldsc_ld_result;
+
+/* One-shot call: read `p->bedfile`, compute on the GPU, fill `r`. */
+int nldsc_ld_calculate(const nldsc_ld_params* p, nldsc_ld_result* r, char* err, size_t errlen);
+
+/* Library / device information. */
+const char* nldsc_version(void);
+int nldsc_device_count(void);
+
+/* ---- engine API ------------------------------------------------------------------------ */
+typedef struct nldsc_engine nldsc_engine;
+
+int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t errlen);
+void nldsc_engine_destroy(nldsc_engine* e);
+
+/* Make a .bed image resident on the engine's device.  `bed` is the complete file content
+ * (3 magic bytes + n_snp rows of ceil(n_org/4) bytes), in host memory (_host) or in device
+ * memory of the engine's device (_device, e.g. a torch tensor's data pointer; copied). */
+int nldsc_engine_load_bed_file(nldsc_engine* e, const char* path, int32_t n_snp, int32_t n_org,
+                               char* err, size_t errlen);
+int nldsc_engine_load_bed_host(nldsc_engine* e, const uint8_t* bed, size_t len, int32_t n_snp,
+                               int32_t n_org, char* err, size_t errlen);
+int nldsc_engine_load_bed_device(nldsc_engine* e, const void* bed, size_t len, int32_t n_snp,
+                                 int32_t n_org, char* err, size_t errlen);
+
+/* Compute LD scores for the SNPs with index in [own_begin, own_end) (position sharding:
+ * each GPU owns a contiguous SNP range and recomputes the pairs it shares with its
+ * neighbours' ranges, so no partial sums cross GPUs).  Entries of `r` outside the owned
+ * range are left untouched.  p->bedfile is ignored (the loaded image is used). */
+int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32_t own_end,
+                     nldsc_ld_result* r, char* err, size_t errlen);
+
+/* Per-stage device timings (milliseconds, HIP events on the engine stream) of the last run:
+ * [0] repack+count, [1] per-SNP statistics, [2] window replay + schedule (host, incl. sync),
+ * [3] band correlation kernel (all launches), [4] finalize, [5] total.
+ * Also: algorithmic FLOPs and SNP pairs of the last run, and kernel launch count. */
+int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, double* pairs,
+                         int32_t* n_band_launches);
+
+/* Deterministic synthetic PLINK .bed on the device (benchmarks / full-size tests):
+ * writes the complete file image (magic + rows) to `bed_dev` (len >= 3 + n_snp*ceil(n_org/4)).
+ * Model as nldsc_amd/synth.py: latent AR(1) haplotypes, thr[j] = Phi^-1(p_j), `missing` rate. */
+int nldsc_synth_bed_device(int32_t device, void* bed_dev, int32_t n_snp, int32_t n_org,
+                           const float* thr_host, float rho, float missing, uint64_t seed,
+                           char* err, size_t errlen);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NLDSC_LD_H */

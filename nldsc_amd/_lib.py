@@ -1,0 +1,119 @@
+"""ctypes binding of libnldsc_amd.so (C ABI: include/nldsc_ld.h).
+
+This is the product path's only route to the GPU engine besides the pybind11 `_ldscore`
+module.  There is no CPU fallback: if the library is missing, or no HIP device is visible,
+calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libnldsc_amd.so")
+
+OK = 0
+E_BAD_MAGIC, E_IO, E_SIZE, E_ARG, E_HIP, E_OOM, E_NODEV = -1, -2, -3, -4, -5, -6, -7
+FLAG_STRICT_PLINK_ORDER = 1
+FLAG_ADDITIVE_ONLY = 2
+
+# every symbol include/nldsc_ld.h declares (tests check the library exports all of them)
+EXPORTED = (
+    "nldsc_ld_calculate", "nldsc_version", "nldsc_device_count", "nldsc_engine_create",
+    "nldsc_engine_destroy", "nldsc_engine_load_bed_file", "nldsc_engine_load_bed_host",
+    "nldsc_engine_load_bed_device", "nldsc_engine_run", "nldsc_engine_timings",
+    "nldsc_synth_bed_device",
+)
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("bedfile", ctypes.c_char_p), ("n_snp", ctypes.c_int32), ("n_org", ctypes.c_int32),
+                ("ld_wind", ctypes.c_double), ("positions", ctypes.POINTER(ctypes.c_double)),
+                ("maf", ctypes.c_double), ("std_thr", ctypes.c_double), ("rsq_thr", ctypes.c_double),
+                ("flags", ctypes.c_uint32), ("device", ctypes.c_int32)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("l2", ctypes.POINTER(ctypes.c_double)), ("l2d", ctypes.POINTER(ctypes.c_double)),
+                ("maf", ctypes.POINTER(ctypes.c_double)), ("residuals_std", ctypes.POINTER(ctypes.c_double)),
+                ("l2_ws", ctypes.POINTER(ctypes.c_int32)), ("l2d_ws", ctypes.POINTER(ctypes.c_int32)),
+                ("l2d_wse", ctypes.POINTER(ctypes.c_int32))]
+
+
+class NLDSCError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                              f"g.build()'` (make -C nldsc_amd/csrc). nldsc_amd has no CPU fallback.")
+        L = ctypes.CDLL(LIB_PATH)
+        c_err = [ctypes.c_char_p, ctypes.c_size_t]
+        vp = ctypes.c_void_p
+        L.nldsc_version.restype = ctypes.c_char_p
+        L.nldsc_version.argtypes = []
+        L.nldsc_device_count.restype = ctypes.c_int
+        L.nldsc_device_count.argtypes = []
+        L.nldsc_ld_calculate.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(Result)] + c_err
+        L.nldsc_engine_create.argtypes = [ctypes.c_int32, ctypes.POINTER(vp)] + c_err
+        L.nldsc_engine_destroy.argtypes = [vp]
+        L.nldsc_engine_destroy.restype = None
+        L.nldsc_engine_load_bed_file.argtypes = [vp, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32] + c_err
+        L.nldsc_engine_load_bed_host.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int32, ctypes.c_int32] + c_err
+        L.nldsc_engine_load_bed_device.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int32, ctypes.c_int32] + c_err
+        L.nldsc_engine_run.argtypes = [vp, ctypes.POINTER(Params), ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.POINTER(Result)] + c_err
+        L.nldsc_engine_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)]
+        L.nldsc_synth_bed_device.argtypes = [ctypes.c_int32, vp, ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.POINTER(ctypes.c_float), ctypes.c_float, ctypes.c_float,
+                                             ctypes.c_uint64] + c_err
+        for name in EXPORTED:
+            if name not in ("nldsc_version", "nldsc_device_count", "nldsc_engine_destroy"):
+                getattr(L, name).restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def check(rc: int, err) -> None:
+    if rc != OK:
+        msg = err.value.decode(errors="replace") if err is not None else f"error {rc}"
+        if rc == E_BAD_MAGIC:
+            raise ValueError(msg)
+        raise NLDSCError(rc, msg)
+
+
+def errbuf():
+    return ctypes.create_string_buffer(1024)
+
+
+def alloc_result(n: int):
+    """numpy arrays + the C struct pointing at them."""
+    arrs = dict(l2=np.full(n, np.nan), l2d=np.full(n, np.nan), maf=np.full(n, np.nan),
+                residuals_std=np.full(n, np.nan), l2_ws=np.full(n, -1, np.int32),
+                l2d_ws=np.full(n, -1, np.int32), l2d_wse=np.full(n, -1, np.int32))
+    d, i = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)
+    res = Result(arrs["l2"].ctypes.data_as(d), arrs["l2d"].ctypes.data_as(d), arrs["maf"].ctypes.data_as(d),
+                 arrs["residuals_std"].ctypes.data_as(d), arrs["l2_ws"].ctypes.data_as(i),
+                 arrs["l2d_ws"].ctypes.data_as(i), arrs["l2d_wse"].ctypes.data_as(i))
+    return arrs, res
+
+
+def make_params(n_snp, n_org, ld_wind, maf, std_thr, rsq_thr, positions, *, bedfile=None, flags=0, device=-1):
+    pos = np.ascontiguousarray(positions, dtype=np.float64)
+    if pos.shape != (n_snp,):
+        raise ValueError(f"positions must have n_snp={n_snp} elements, got {pos.shape}")
+    p = Params(bedfile.encode() if bedfile else None, int(n_snp), int(n_org), float(ld_wind),
+               pos.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), float(maf), float(std_thr), float(rsq_thr),
+               int(flags), int(device))
+    return p, pos  # keep `pos` alive while p is used

@@ -1,0 +1,511 @@
+// ld_engine.cpp — host side of libnldsc_amd.so: the C ABI declared in include/nldsc_ld.h.
+//
+// One engine = one HIP device + one stream + device buffers that persist across runs.
+// A run (nldsc_engine_run) is the whole hot path of bayarpark/nldsc's `calculate`
+// (nldsc/ldscore/_ldscore/ldscalc.h:8-65) over a .bed image already resident in HBM:
+//   repack+count -> per-SNP statistics -> window replay + tile schedule (host, O(M)) ->
+//   band correlation kernels -> finalize -> results to host.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/nldsc_ld.h"
+#include "ld_kernels.h"
+
+#define NLDSC_VERSION "0.1.0"
+
+namespace {
+
+constexpr int BLK = 32;             // SNPs per MFMA block
+constexpr int ROW_ALIGN_BYTES = 32; // one K-loop chunk of a 2-bit row (16 B per lane half)
+
+// Message of BedStreamReader::check_plink_magic_number (stream.h:88-102), verbatim.
+const char* kBadMagic =
+    "Invalid PLINK magic number in BED file.The file is incorrect, or it was created using an incompatible "
+    "version of PLINK.";
+
+int set_err(char* err, size_t errlen, int code, const char* fmt, ...) {
+    if (err && errlen) {
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(err, errlen, fmt, ap);
+        va_end(ap);
+    }
+    return code;
+}
+
+#define HIPCHK(expr)                                                                                  \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess)                                                                         \
+            return set_err(err, errlen, NLDSC_E_HIP, "HIP error %s at %s:%d (%s)", hipGetErrorString(e_), \
+                           __FILE__, __LINE__, #expr);                                                \
+    } while (0)
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= n && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T));
+        if (e == hipSuccess) n = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+}  // namespace
+
+struct nldsc_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[6] = {};
+    // resident .bed image
+    DevBuf<uint8_t> bed;
+    size_t bed_len = 0;
+    int32_t n_snp = 0, n_org = 0;
+    // work buffers
+    DevBuf<uint32_t> geno;
+    DevBuf<int> counts, Lw, Rw, ws_acc, ws3;
+    DevBuf<float2> lut;
+    DevBuf<uint8_t> sflags;
+    DevBuf<double> pos, maf, rstd, l2_acc, l2d_acc, l2, l2d;
+    DevBuf<int4> items;
+    // host scratch
+    std::vector<uint8_t> h_flags;
+    std::vector<int> h_L, h_R;
+    std::vector<int4> h_items;
+    // timings of the last run
+    double ms[6] = {0, 0, 0, 0, 0, 0};
+    double flop_alg = 0, pairs = 0;
+    int32_t n_band_launches = 0;
+
+    ~nldsc_engine() {
+        (void)hipSetDevice(device);
+        bed.release(); geno.release(); counts.release(); Lw.release(); Rw.release(); ws_acc.release();
+        ws3.release(); lut.release(); sflags.release(); pos.release(); maf.release(); rstd.release();
+        l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release();
+        for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+int check_dims(int32_t n_snp, int32_t n_org, char* err, size_t errlen) {
+    if (n_snp <= 0) return set_err(err, errlen, NLDSC_E_ARG, "n_snp must be positive (got %d)", n_snp);
+    if (n_org <= 0) return set_err(err, errlen, NLDSC_E_ARG, "n_org must be positive (got %d)", n_org);
+    return NLDSC_OK;
+}
+
+size_t bed_bytes_needed(int32_t n_snp, int32_t n_org) {
+    const size_t nb = (size_t)(n_org / 4 + (n_org % 4 > 0));
+    return 3 + nb * (size_t)n_snp;
+}
+
+int check_magic(const uint8_t* m, size_t len, int32_t n_snp, int32_t n_org, char* err, size_t errlen) {
+    if (len < 3 || m[0] != 0x6c || m[1] != 0x1b || m[2] != 0x01)
+        return set_err(err, errlen, NLDSC_E_BAD_MAGIC, "%s", kBadMagic);
+    if (len < bed_bytes_needed(n_snp, n_org))
+        return set_err(err, errlen, NLDSC_E_SIZE,
+                       "BED file too short: %zu bytes, expected at least %zu for %d SNPs x %d individuals", len,
+                       bed_bytes_needed(n_snp, n_org), n_snp, n_org);
+    return NLDSC_OK;
+}
+
+int use_device(int32_t device, int* resolved, char* err, size_t errlen) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return set_err(err, errlen, NLDSC_E_NODEV, "no HIP device visible (nldsc_amd has no CPU fallback)");
+    int d = device;
+    if (d < 0) HIPCHK(hipGetDevice(&d));
+    if (d >= n) return set_err(err, errlen, NLDSC_E_ARG, "device %d out of range (%d visible)", d, n);
+    HIPCHK(hipSetDevice(d));
+    *resolved = d;
+    return NLDSC_OK;
+}
+
+// Replay of ChunkwiseReader's pointers (stream.h:131-155,182-197) from positions and MAF-pass
+// flags.  For every SNP j the reference computes, N(j) = { i in [L_j, R_j] : pass_i,
+// |pos_i - pos_j| <= w, i != j }; L_j = -1 marks a SNP it does not compute (unused, MAF-failed).
+void replay_windows(const double* pos, const uint8_t* flags, int n, double w, int* L, int* R) {
+    auto used = [&](int i) { return 0 <= i && i < n && pos[i] >= 0; };
+    auto inwin = [&](int a, int b) { return used(a) && used(b) && std::fabs(pos[b] - pos[a]) <= w; };
+    int left = 0, right = -1;
+    for (int j = 0; j < n; ++j) {
+        L[j] = -1;
+        R[j] = -2;
+        if (!used(j)) continue;                       // pass_chunk
+        do {                                          // extend_cache
+            if (right + 1 >= n) break;
+            ++right;
+        } while (inwin(j, right));
+        if (!(j <= right && (flags[j] & 1))) continue;  // initialize_next_chunk() == false
+        // chunk_indices: evict failing SNPs at the left edge
+        while (left < j && !((flags[left] & 1) && inwin(j, left))) ++left;
+        L[j] = left;
+        R[j] = right;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* nldsc_version(void) { return NLDSC_VERSION; }
+
+int nldsc_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t errlen) {
+    if (!out) return set_err(err, errlen, NLDSC_E_ARG, "out is NULL");
+    *out = nullptr;
+    int d = 0;
+    int rc = use_device(device, &d, err, errlen);
+    if (rc) return rc;
+    nldsc_engine* e = new (std::nothrow) nldsc_engine();
+    if (!e) return set_err(err, errlen, NLDSC_E_OOM, "out of host memory");
+    e->device = d;
+    hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    for (auto& ev : e->ev)
+        if (he == hipSuccess) he = hipEventCreate(&ev);
+    if (he != hipSuccess) {
+        delete e;
+        return set_err(err, errlen, NLDSC_E_HIP, "HIP error %s creating stream/events", hipGetErrorString(he));
+    }
+    *out = e;
+    return NLDSC_OK;
+}
+
+void nldsc_engine_destroy(nldsc_engine* e) { delete e; }
+
+int nldsc_engine_load_bed_host(nldsc_engine* e, const uint8_t* bed, size_t len, int32_t n_snp, int32_t n_org,
+                               char* err, size_t errlen) {
+    if (!e || !bed) return set_err(err, errlen, NLDSC_E_ARG, "NULL engine or buffer");
+    int rc = check_dims(n_snp, n_org, err, errlen);
+    if (rc) return rc;
+    rc = check_magic(bed, len, n_snp, n_org, err, errlen);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(e->device));
+    const size_t need = bed_bytes_needed(n_snp, n_org);
+    HIPCHK(e->bed.ensure(need));
+    HIPCHK(hipMemcpyAsync(e->bed.p, bed, need, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->bed_len = need;
+    e->n_snp = n_snp;
+    e->n_org = n_org;
+    return NLDSC_OK;
+}
+
+int nldsc_engine_load_bed_device(nldsc_engine* e, const void* bed, size_t len, int32_t n_snp, int32_t n_org,
+                                 char* err, size_t errlen) {
+    if (!e || !bed) return set_err(err, errlen, NLDSC_E_ARG, "NULL engine or buffer");
+    int rc = check_dims(n_snp, n_org, err, errlen);
+    if (rc) return rc;
+    const size_t need = bed_bytes_needed(n_snp, n_org);
+    if (len < 3) return set_err(err, errlen, NLDSC_E_BAD_MAGIC, "%s", kBadMagic);
+    HIPCHK(hipSetDevice(e->device));
+    uint8_t magic[3];
+    HIPCHK(hipMemcpy(magic, bed, 3, hipMemcpyDeviceToHost));
+    if (magic[0] != 0x6c || magic[1] != 0x1b || magic[2] != 0x01)
+        return set_err(err, errlen, NLDSC_E_BAD_MAGIC, "%s", kBadMagic);
+    if (len < need)
+        return set_err(err, errlen, NLDSC_E_SIZE, "BED image too short: %zu bytes, expected at least %zu", len, need);
+    HIPCHK(e->bed.ensure(need));
+    HIPCHK(hipMemcpyAsync(e->bed.p, bed, need, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->bed_len = need;
+    e->n_snp = n_snp;
+    e->n_org = n_org;
+    return NLDSC_OK;
+}
+
+int nldsc_engine_load_bed_file(nldsc_engine* e, const char* path, int32_t n_snp, int32_t n_org, char* err,
+                               size_t errlen) {
+    if (!e || !path) return set_err(err, errlen, NLDSC_E_ARG, "NULL engine or path");
+    int rc = check_dims(n_snp, n_org, err, errlen);
+    if (rc) return rc;
+    FILE* f = std::fopen(path, "rb");
+    if (!f) {
+        // the reference's ifstream fails silently and then rejects the (unread) magic number
+        return set_err(err, errlen, NLDSC_E_BAD_MAGIC, "%s", kBadMagic);
+    }
+    const size_t need = bed_bytes_needed(n_snp, n_org);
+    uint8_t magic[3] = {0, 0, 0};
+    size_t got = std::fread(magic, 1, 3, f);
+    if (got < 3 || magic[0] != 0x6c || magic[1] != 0x1b || magic[2] != 0x01) {
+        std::fclose(f);
+        return set_err(err, errlen, NLDSC_E_BAD_MAGIC, "%s", kBadMagic);
+    }
+    HIPCHK(hipSetDevice(e->device));
+    // stream the rows through a pinned staging buffer (64 MiB double-buffered)
+    constexpr size_t CH = size_t(64) << 20;
+    uint8_t* stage = nullptr;
+    if (hipHostMalloc((void**)&stage, 2 * CH) != hipSuccess) {
+        std::fclose(f);
+        return set_err(err, errlen, NLDSC_E_OOM, "cannot allocate pinned staging buffer");
+    }
+    hipError_t he = e->bed.ensure(need);
+    size_t off = 3;
+    int slot = 0;
+    if (he == hipSuccess) he = hipMemcpyAsync(e->bed.p, magic, 3, hipMemcpyHostToDevice, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    while (he == hipSuccess && off < need) {
+        const size_t n = std::min(CH, need - off);
+        uint8_t* buf = stage + (size_t)slot * CH;
+        // the copy issued two chunks ago used this slot; wait for it before overwriting
+        he = hipStreamSynchronize(e->stream);
+        if (he != hipSuccess) break;
+        const size_t r = std::fread(buf, 1, n, f);
+        if (r != n) {
+            std::fclose(f);
+            (void)hipStreamSynchronize(e->stream);
+            (void)hipHostFree(stage);
+            return set_err(err, errlen, NLDSC_E_SIZE,
+                           "BED file too short: %zu bytes, expected at least %zu for %d SNPs x %d individuals",
+                           off + r, need, n_snp, n_org);
+        }
+        he = hipMemcpyAsync(e->bed.p + off, buf, n, hipMemcpyHostToDevice, e->stream);
+        off += n;
+        slot ^= 1;
+    }
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    std::fclose(f);
+    (void)hipHostFree(stage);
+    if (he != hipSuccess) return set_err(err, errlen, NLDSC_E_HIP, "HIP error %s loading BED", hipGetErrorString(he));
+    e->bed_len = need;
+    e->n_snp = n_snp;
+    e->n_org = n_org;
+    return NLDSC_OK;
+}
+
+int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32_t own_end,
+                     nldsc_ld_result* r, char* err, size_t errlen) {
+    if (!e || !p || !r) return set_err(err, errlen, NLDSC_E_ARG, "NULL argument");
+    if (!e->bed.p) return set_err(err, errlen, NLDSC_E_ARG, "no BED image loaded");
+    if (p->n_snp != e->n_snp || p->n_org != e->n_org)
+        return set_err(err, errlen, NLDSC_E_ARG, "params (%d SNPs x %d) do not match the loaded BED (%d x %d)",
+                       p->n_snp, p->n_org, e->n_snp, e->n_org);
+    if (!p->positions) return set_err(err, errlen, NLDSC_E_ARG, "positions is NULL");
+    if (!r->l2 || !r->l2d || !r->maf || !r->residuals_std || !r->l2_ws || !r->l2d_ws || !r->l2d_wse)
+        return set_err(err, errlen, NLDSC_E_ARG, "a result array is NULL");
+    const int M = p->n_snp, N = p->n_org;
+    if (own_begin < 0 || own_end > M || own_begin > own_end)
+        return set_err(err, errlen, NLDSC_E_ARG, "owned range [%d, %d) outside [0, %d)", own_begin, own_end, M);
+    const bool dom = !(p->flags & NLDSC_FLAG_ADDITIVE_ONLY);
+    const bool strict = (p->flags & NLDSC_FLAG_STRICT_PLINK_ORDER) != 0;
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t st = e->stream;
+
+    const int nb = N / 4 + (N % 4 > 0);
+    const int row_bytes = (nb + ROW_ALIGN_BYTES - 1) / ROW_ALIGN_BYTES * ROW_ALIGN_BYTES;
+    const int pitch_words = row_bytes / 4;
+    const int n_it = row_bytes / ROW_ALIGN_BYTES;
+    const int nblk = (M + BLK - 1) / BLK;
+    const int Mpad = nblk * BLK;
+    // last .bed byte: bit pairs that are individuals for the reference (high pairs first,
+    // stream.h:55-66) or for PLINK (low pairs first) — the rest are recoded as missing (-> 0)
+    const int rem = N % 4;
+    uint32_t tail_keep = 0xFFu;
+    if (rem) tail_keep = strict ? (uint32_t)((1u << (2 * rem)) - 1u) : (uint32_t)(0xFFu << (8 - 2 * rem)) & 0xFFu;
+
+    HIPCHK(e->geno.ensure((size_t)Mpad * pitch_words));
+    HIPCHK(e->counts.ensure((size_t)M * 4));
+    HIPCHK(e->lut.ensure((size_t)Mpad * 4));
+    HIPCHK(e->sflags.ensure((size_t)Mpad));
+    HIPCHK(e->pos.ensure((size_t)M));
+    HIPCHK(e->maf.ensure((size_t)M));
+    HIPCHK(e->rstd.ensure((size_t)M));
+    HIPCHK(e->Lw.ensure((size_t)M));
+    HIPCHK(e->Rw.ensure((size_t)M));
+    HIPCHK(e->l2_acc.ensure((size_t)M));
+    HIPCHK(e->l2d_acc.ensure((size_t)M));
+    HIPCHK(e->ws_acc.ensure((size_t)M * 3));
+    HIPCHK(e->l2.ensure((size_t)M));
+    HIPCHK(e->l2d.ensure((size_t)M));
+    HIPCHK(e->ws3.ensure((size_t)M * 3));
+
+    auto t_start = std::chrono::steady_clock::now();
+    HIPCHK(hipEventRecord(e->ev[0], st));
+    HIPCHK(hipMemcpyAsync(e->pos.p, p->positions, sizeof(double) * M, hipMemcpyHostToDevice, st));
+    if (Mpad > M) HIPCHK(hipMemsetAsync(e->geno.p + (size_t)M * pitch_words, 0x55, (size_t)(Mpad - M) * row_bytes, st));
+    HIPCHK(nldsc::launch_repack_count(e->bed.p + 3, e->geno.p, M, nb, pitch_words, tail_keep, e->counts.p, st));
+    HIPCHK(hipEventRecord(e->ev[1], st));
+    HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->sflags.p,
+                                   e->maf.p, e->rstd.p, st));
+    HIPCHK(hipEventRecord(e->ev[2], st));
+
+    // ---- window replay + schedule on the host (needs the MAF-pass flags) ----
+    auto t_host0 = std::chrono::steady_clock::now();
+    e->h_flags.resize(Mpad);
+    HIPCHK(hipMemcpyAsync(e->h_flags.data(), e->sflags.p, Mpad, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    e->h_L.resize(M);
+    e->h_R.resize(M);
+    replay_windows(p->positions, e->h_flags.data(), M, p->ld_wind, e->h_L.data(), e->h_R.data());
+
+    // Work items: row block I, column blocks [J0, J0 + nc).  A block pair (I <= J) is needed when
+    // it holds a pair (i < j) with j in N(i) or i in N(j) and one of i, j is owned.
+    std::vector<int> blk_pass(nblk, 0), blk_own(nblk, 0);
+    for (int j = 0; j < M; ++j) {
+        if (e->h_flags[j] & 1) blk_pass[j / BLK] = 1;
+        if (j >= own_begin && j < own_end) blk_own[j / BLK] = 1;
+    }
+    // colmax[x]: largest computed j with L_j <= x (L is non-decreasing over computed SNPs)
+    std::vector<int> comp;
+    comp.reserve(M);
+    for (int j = 0; j < M; ++j) if (e->h_L[j] >= 0) comp.push_back(j);
+    int lo_row = M;  // first row any owned SNP needs: min L_j over owned computed j
+    for (int j : comp) if (j >= own_begin && j < own_end) { lo_row = std::min(lo_row, e->h_L[j]); }
+    lo_row = std::min(lo_row, own_begin);
+    std::vector<int4> items2, items1;
+    size_t cp = 0;
+    int run_rmax = -1;
+    for (int I = std::max(0, lo_row / BLK); I < nblk && I * BLK < own_end + 0; ++I) {
+        const int i_end = std::min(M, (I + 1) * BLK) - 1;
+        int jmax = -1;
+        for (int i = I * BLK; i <= i_end; ++i) if (e->h_L[i] >= 0) jmax = std::max(jmax, e->h_R[i]);
+        while (cp < comp.size() && e->h_L[comp[cp]] <= i_end) { run_rmax = comp[cp]; ++cp; }
+        jmax = std::max(jmax, run_rmax);
+        if (!blk_pass[I] || jmax < I * BLK) continue;
+        const int Jmax = std::min(nblk - 1, jmax / BLK);
+        int J = I;
+        while (J <= Jmax) {
+            auto useful = [&](int JJ) { return blk_pass[JJ] && (blk_own[I] || blk_own[JJ]); };
+            if (!useful(J)) { ++J; continue; }
+            if (J + 1 <= Jmax && useful(J + 1)) {
+                items2.push_back(make_int4(I, J, 2, 0));
+                J += 2;
+            } else {
+                items1.push_back(make_int4(I, J, 1, 0));
+                J += 1;
+            }
+        }
+    }
+    e->h_items.clear();
+    e->h_items.insert(e->h_items.end(), items2.begin(), items2.end());
+    e->h_items.insert(e->h_items.end(), items1.begin(), items1.end());
+    // the band kernel reads rows [32 I, 32 (J0 + nc)) of geno / lut: check before launching
+    if (pitch_words % 8 != 0 || n_it * 8 != pitch_words)
+        return set_err(err, errlen, NLDSC_E_ARG, "internal: bad row pitch %d", pitch_words);
+    for (const int4& it : e->h_items)
+        if (it.x < 0 || it.y < it.x || (it.z != 1 && it.z != 2) || it.y + it.z > nblk)
+            return set_err(err, errlen, NLDSC_E_ARG, "internal: bad work item (%d, %d, %d) for %d blocks", it.x,
+                           it.y, it.z, nblk);
+    HIPCHK(e->items.ensure(std::max<size_t>(e->h_items.size(), 1)));
+    HIPCHK(hipMemcpyAsync(e->Lw.p, e->h_L.data(), sizeof(int) * M, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(e->Rw.p, e->h_R.data(), sizeof(int) * M, hipMemcpyHostToDevice, st));
+    if (!e->h_items.empty())
+        HIPCHK(hipMemcpyAsync(e->items.p, e->h_items.data(), sizeof(int4) * e->h_items.size(), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(e->l2_acc.p, 0, sizeof(double) * M, st));
+    HIPCHK(hipMemsetAsync(e->l2d_acc.p, 0, sizeof(double) * M, st));
+    HIPCHK(hipMemsetAsync(e->ws_acc.p, 0, sizeof(int) * 3 * (size_t)M, st));
+    auto t_host1 = std::chrono::steady_clock::now();
+
+    HIPCHK(hipEventRecord(e->ev[3], st));
+    e->n_band_launches = 0;
+    if (!e->h_items.empty()) {
+        HIPCHK(nldsc::launch_band(dom, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, e->lut.p, e->items.p,
+                                  e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr,
+                                  own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, st));
+        ++e->n_band_launches;
+    }
+    HIPCHK(hipEventRecord(e->ev[4], st));
+    HIPCHK(nldsc::launch_finalize(e->Lw.p, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, own_begin, own_end, dom,
+                                  e->l2.p, e->l2d.p, e->ws3.p, st));
+    HIPCHK(hipEventRecord(e->ev[5], st));
+    const int n_own = own_end - own_begin;
+    if (n_own > 0) {
+        const size_t o = own_begin;
+        HIPCHK(hipMemcpyAsync(r->l2 + o, e->l2.p + o, sizeof(double) * n_own, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(r->l2d + o, e->l2d.p + o, sizeof(double) * n_own, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(r->maf + o, e->maf.p + o, sizeof(double) * n_own, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(r->residuals_std + o, e->rstd.p + o, sizeof(double) * n_own, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(r->l2_ws + o, e->ws3.p + o, sizeof(int) * n_own, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(r->l2d_ws + o, e->ws3.p + M + o, sizeof(int) * n_own, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(r->l2d_wse + o, e->ws3.p + 2 * (size_t)M + o, sizeof(int) * n_own, hipMemcpyDeviceToHost,
+                              st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    auto t_end = std::chrono::steady_clock::now();
+
+    float f = 0;
+    HIPCHK(hipEventElapsedTime(&f, e->ev[0], e->ev[1])); e->ms[0] = f;
+    HIPCHK(hipEventElapsedTime(&f, e->ev[1], e->ev[2])); e->ms[1] = f;
+    e->ms[2] = std::chrono::duration<double, std::milli>(t_host1 - t_host0).count();
+    HIPCHK(hipEventElapsedTime(&f, e->ev[3], e->ev[4])); e->ms[3] = f;
+    HIPCHK(hipEventElapsedTime(&f, e->ev[4], e->ev[5])); e->ms[4] = f;
+    e->ms[5] = std::chrono::duration<double, std::milli>(t_end - t_start).count();
+    double sw = 0, sd = 0;
+    for (int j = own_begin; j < own_end; ++j) {
+        if (r->l2_ws[j] > 0) sw += r->l2_ws[j];
+        if (dom && r->l2d_ws[j] > 0) sd += r->l2d_ws[j];
+    }
+    e->pairs = sw;
+    // BASELINE.md metric: FLOP_alg = 2N(1/2 sum WSA + sum WSD); additive-only 2N * 1/2 sum WSA
+    e->flop_alg = 2.0 * (double)N * (0.5 * sw + sd);
+    return NLDSC_OK;
+}
+
+int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, double* pairs,
+                         int32_t* n_band_launches) {
+    if (!e) return NLDSC_E_ARG;
+    if (ms6) for (int k = 0; k < 6; ++k) ms6[k] = e->ms[k];
+    if (flop_alg) *flop_alg = e->flop_alg;
+    if (pairs) *pairs = e->pairs;
+    if (n_band_launches) *n_band_launches = e->n_band_launches;
+    return NLDSC_OK;
+}
+
+int nldsc_ld_calculate(const nldsc_ld_params* p, nldsc_ld_result* r, char* err, size_t errlen) {
+    if (!p || !r || !p->bedfile) return set_err(err, errlen, NLDSC_E_ARG, "NULL argument");
+    nldsc_engine* e = nullptr;
+    int rc = nldsc_engine_create(p->device, &e, err, errlen);
+    if (rc) return rc;
+    rc = nldsc_engine_load_bed_file(e, p->bedfile, p->n_snp, p->n_org, err, errlen);
+    if (!rc) rc = nldsc_engine_run(e, p, 0, p->n_snp, r, err, errlen);
+    nldsc_engine_destroy(e);
+    return rc;
+}
+
+int nldsc_synth_bed_device(int32_t device, void* bed_dev, int32_t n_snp, int32_t n_org, const float* thr_host,
+                           float rho, float missing, uint64_t seed, char* err, size_t errlen) {
+    if (!bed_dev || !thr_host) return set_err(err, errlen, NLDSC_E_ARG, "NULL argument");
+    int rc = check_dims(n_snp, n_org, err, errlen);
+    if (rc) return rc;
+    int d = 0;
+    rc = use_device(device, &d, err, errlen);
+    if (rc) return rc;
+    const int nb = n_org / 4 + (n_org % 4 > 0);
+    float* thr = nullptr;
+    HIPCHK(hipMalloc(&thr, sizeof(float) * n_snp));
+    hipError_t he = hipMemcpy(thr, thr_host, sizeof(float) * n_snp, hipMemcpyHostToDevice);
+    const uint8_t magic[3] = {0x6c, 0x1b, 0x01};
+    if (he == hipSuccess) he = hipMemcpy(bed_dev, magic, 3, hipMemcpyHostToDevice);
+    if (he == hipSuccess)
+        he = nldsc::launch_synth_bed((uint8_t*)bed_dev + 3, n_snp, n_org, nb, thr, rho, missing, seed, nullptr);
+    if (he == hipSuccess) he = hipDeviceSynchronize();
+    (void)hipFree(thr);
+    if (he != hipSuccess) return set_err(err, errlen, NLDSC_E_HIP, "HIP error %s in synth", hipGetErrorString(he));
+    return NLDSC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,22 @@
+// Internal launcher declarations for ld_kernels.hip (not part of the public C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nldsc {
+
+hipError_t launch_repack_count(const uint8_t* rows, uint32_t* geno, int n_snp, int nb, int pitch_words,
+                               uint32_t tail_keep, int* counts, hipStream_t st);
+hipError_t launch_snp_stats(const int* counts, const double* pos, int n_snp, int n_snp_pad, int n_org, double maf_thr,
+                            double std_thr, float2* lut, uint8_t* sflags, double* maf_out, double* rstd_out,
+                            hipStream_t st);
+hipError_t launch_band(bool dom, int n_items, const uint32_t* geno, int pitch_words, int n_it,
+                       const float2* lut, const int4* items, const double* pos, const int* Lw, const int* Rw,
+                       const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
+                       int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, hipStream_t st);
+hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2d_acc, const int* ws_acc, int n_snp,
+                           int own_lo, int own_hi, bool dom, double* l2, double* l2d, int* ws3, hipStream_t st);
+hipError_t launch_synth_bed(uint8_t* rows, int n_snp, int n_org, int nb, const float* thr, float rho, float missing,
+                            uint64_t seed, hipStream_t st);
+
+}  // namespace nldsc

@@ -1,0 +1,490 @@
+// ld_kernels.hip — gfx950 (MI355X, CDNA4) kernels of the LD-score engine.
+//
+// Pipeline for one `calculate` (reference: nldsc/ldscore/_ldscore/ldscalc.h:8-65):
+//   1. repack_count_kernel  .bed rows (unaligned, ceil(N/4) B) -> aligned 2-bit genotype rows in HBM,
+//                           the reference's last-byte rule applied (stream.h:55-66), plus per-SNP
+//                           genotype-code counts.  HBM-bound byte work.
+//   2. snp_stats_kernel     per-SNP MAF / filters / residual std and two 4-entry fp32 lookup tables
+//                           (standardised additive value and standardised dominance residual per
+//                           2-bit code), in closed form from the counts (encoder.h:91-133,
+//                           tools.h:54-85).
+//   3. band_kernel<NC,DOM>  the windowed correlation block: for a 32-SNP row block I and NC 32-SNP
+//                           column blocks, X_I^T X_J, X_I^T R_J and R_I^T X_J over all samples with
+//                           v_mfma_f32_32x32x2_f32.  Operands are decoded straight from the 2-bit
+//                           rows into VGPRs through a per-wave LDS table [code][snp] -> (a, r); a
+//                           fused epilogue applies r2adj (tools.h:87-92), the window / MAF / residual
+//                           masks and reduces per-SNP sums (ldscalc.h:34-54).
+//   4. finalize_kernel      L2 = 1 + sum, NaN / -1 for SNPs that are not computed (ldscalc.h:16-21).
+//   (+) synth_bed_kernel    deterministic synthetic .bed image for benchmarks.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ld_kernels.h"
+
+namespace nldsc {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ------------------------------------------------------------------------------------------
+// 1. repack + count
+// ------------------------------------------------------------------------------------------
+// Output row j: pitch_words little-endian words.  Byte p of the row keeps the .bed byte
+// (4 samples, first sample in bits 7:6 per the reference's unpack order — any fixed slot order
+// is fine for dot products as long as every SNP uses the same one).  Bytes past the row and
+// the last byte's invalid bit pairs become 01 ("missing"), whose standardised value is exactly
+// 0 in both lookup tables, so they contribute nothing to any dot product.
+__global__ void __launch_bounds__(256) repack_count_kernel(const uint8_t* __restrict__ rows, uint32_t* __restrict__ geno,
+                                                           int n_snp, int nb, int pitch_words, uint32_t tail_keep,
+                                                           int* __restrict__ counts) {
+    const int j = blockIdx.x;
+    if (j >= n_snp) return;
+    const uint8_t* src = rows + (size_t)j * (size_t)nb;
+    uint32_t* dst = geno + (size_t)j * (size_t)pitch_words;
+    int c0 = 0, c1 = 0, c2 = 0;
+    for (int w = threadIdx.x; w < pitch_words; w += blockDim.x) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int p = 4 * w + k;
+            uint32_t b = p < nb ? (uint32_t)src[p] : 0x55u;
+            if (p == nb - 1) b = (b & tail_keep) | (0x55u & ~tail_keep);
+            word |= b << (8 * k);
+        }
+        dst[w] = word;
+        const uint32_t hi = (word >> 1) & 0x55555555u, lo = word & 0x55555555u;
+        c0 += __popc(~hi & ~lo & 0x55555555u);  // 00 hom A1
+        c1 += __popc(hi & ~lo);                 // 10 het
+        c2 += __popc(hi & lo);                  // 11 hom A2
+    }
+    // block reduction (4 waves of 64)
+    for (int o = 32; o > 0; o >>= 1) {
+        c0 += __shfl_down(c0, o, 64);
+        c1 += __shfl_down(c1, o, 64);
+        c2 += __shfl_down(c2, o, 64);
+    }
+    __shared__ int red[3][4];
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][wv] = c0; red[1][wv] = c1; red[2][wv] = c2; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        int s = 0;
+        for (int q = 0; q < (int)(blockDim.x >> 6); ++q) s += red[threadIdx.x][q];
+        counts[(size_t)j * 4 + threadIdx.x] = s;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// 2. per-SNP statistics -> lookup tables
+// ------------------------------------------------------------------------------------------
+// Closed form of SNPInMemory::decode + standardise (encoder.h:91-133, tools.h:54-85) from the
+// genotype counts c0 (hom A1), c1 (het), c2 (hom A2) over the n_org individuals the reference
+// reads.  Missing calls are mean-imputed by the reference, so their centred value is exactly 0.
+__global__ void snp_stats_kernel(const int* __restrict__ counts, const double* __restrict__ pos, int n_snp,
+                                 int n_snp_pad, int n_org, double maf_thr, double std_thr,
+                                 float2* __restrict__ lut, uint8_t* __restrict__ sflags,
+                                 double* __restrict__ maf_out, double* __restrict__ rstd_out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_snp_pad) return;
+    float2 L[4] = {make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
+    uint8_t fl = 0;
+    if (j < n_snp) {
+        const double qnan = __builtin_nan("");
+        double maf_d = qnan, rstd_d = qnan;
+        if (pos[j] >= 0.0) {  // SNPFilter::is_used (tools.h:15-23)
+            const double c0 = counts[4 * (size_t)j], c1 = counts[4 * (size_t)j + 1], c2 = counts[4 * (size_t)j + 2];
+            const double n_obs = c0 + c1 + c2;
+            const double N = (double)n_org;
+            // MAF exactly as encoder.h:114-118 (fp64 mean of integers cast to fp32)
+            const float add_mean = (float)((c1 + 2.0 * c2) / n_obs);
+            const float f2 = add_mean / 2;
+            const float maf = f2 < 0.5f ? f2 : 1 - f2;
+            maf_d = (double)maf;
+            if (!((double)maf <= maf_thr)) {  // encoder.h:120
+                fl |= 1;  // MAF pass
+                if (n_obs == 0.0) {
+                    // every call missing: the reference's vectors are all NaN (MAF NaN passes the
+                    // filter); they poison every window containing this SNP.
+                    for (int c = 0; c < 4; ++c) L[c] = make_float2(qnan, 0.f);
+                } else {
+                    const double abar = (c1 + 2.0 * c2) / n_obs, dbar = 2.0 * (c1 + c2) / n_obs;
+                    const double da0 = -abar, da1 = 1.0 - abar, da2 = 2.0 - abar;
+                    const double dd0 = -dbar, dd1 = 2.0 - dbar, dd2 = 2.0 - dbar;
+                    const double var_a = (c0 * da0 * da0 + c1 * da1 * da1 + c2 * da2 * da2) / N;
+                    const double cov = (c0 * da0 * dd0 + c1 * da1 * dd1 + c2 * da2 * dd2) / N;
+                    const double beta = cov / var_a;  // Math::regression_residuals slope
+                    const double r0 = dd0 - beta * da0, r1 = dd1 - beta * da1, r2 = dd2 - beta * da2;
+                    const int distinct = (c0 > 0) + (c1 > 0) + (c2 > 0);
+                    // <= 2 observed genotypes: the dominance coding is affine in the additive one,
+                    // the residual is exactly constant, its std exactly 0.
+                    const double var_r = distinct <= 2 ? 0.0 : (c0 * r0 * r0 + c1 * r1 * r1 + c2 * r2 * r2) / N;
+                    const double sd_a = sqrt(var_a);
+                    rstd_d = sqrt(var_r);
+                    const bool rpass = rstd_d > std_thr;  // SNPFilter::residuals_std (tools.h:40-43)
+                    if (rpass) fl |= 2;
+                    const float ia = (float)(da0 / sd_a), ib = (float)(da1 / sd_a), ic = (float)(da2 / sd_a);
+                    float ra = 0.f, rb = 0.f, rc = 0.f;
+                    if (rpass) { ra = (float)(r0 / rstd_d); rb = (float)(r1 / rstd_d); rc = (float)(r2 / rstd_d); }
+                    L[0] = make_float2(ia, ra);   // code 00 hom A1
+                    L[1] = make_float2(0.f, 0.f); // code 01 missing (imputed -> centred 0)
+                    L[2] = make_float2(ib, rb);   // code 10 het
+                    L[3] = make_float2(ic, rc);   // code 11 hom A2
+                }
+            }
+        }
+        maf_out[j] = maf_d;
+        rstd_out[j] = (fl & 1) ? rstd_d : qnan;
+    }
+    for (int c = 0; c < 4; ++c) lut[(size_t)j * 4 + c] = L[c];
+    sflags[j] = fl;
+}
+
+// ------------------------------------------------------------------------------------------
+// 3. band correlation kernel
+// ------------------------------------------------------------------------------------------
+// One wave per work item (I, J0, NC): row SNPs 32*I..+31, column SNPs 32*(J0+b)..+31.
+// Lane l: i = l & 31 (its row SNP for the A operand and its column SNP for the B operand),
+// h = l >> 5 (which half of each 32-byte chunk of the 2-bit rows it decodes).  At every MFMA
+// step lane (i, h) supplies A[i][h] and B[h][j=i] for the same sample slot, so D accumulates
+// sum_k A[i][k] B[k][j] over all sample slots.  fp32 partial sums are flushed into a second
+// fp32 accumulator every FLUSH_IT chunks (2048 samples) to keep the K = N fp32 chain short.
+constexpr int FLUSH_IT = 16;
+
+struct SnpSlot {
+    double pos;
+    int L, R, fl, g;
+};
+
+__device__ __forceinline__ double r2_adjusted(double dot, double n) {
+    // Math::r2_adjusted (tools.h:87-92)
+    const double corr = dot * (1. / n);
+    const double r2 = corr * corr;
+    return 1. - (1. - r2) * (n - 1) / (n - 2);
+}
+
+constexpr int NC_MAX = 2;
+constexpr int NS_MAX = 32 * (1 + NC_MAX);
+
+struct BandLds {
+    float2 tab[4 * NS_MAX];  // [code][slot], slot stride NS = 32 * (1 + NC) of the body
+    SnpSlot info[NS_MAX];
+    double l2[NS_MAX], l2d[NS_MAX];
+    int wsa[NS_MAX], wsd[NS_MAX], wse[NS_MAX];
+};
+
+template <int NC, bool DOM>
+__device__ __forceinline__ void band_body(BandLds& sh, const int4 it, const uint32_t* __restrict__ geno,
+                                          int pitch_words, int n_it, const float2* __restrict__ lut,
+                                          const double* __restrict__ pos, const int* __restrict__ Lw,
+                                          const int* __restrict__ Rw, const uint8_t* __restrict__ sflags, int n_snp,
+                                          double ld_wind, double n_org, double rsq_thr, int own_lo, int own_hi,
+                                          double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
+                                          int* __restrict__ ws_acc) {
+    constexpr int NS = 32 * (1 + NC);  // SNP slots: 32 rows, then NC x 32 columns
+    float2 (*tab)[NS] = reinterpret_cast<float2 (*)[NS]>(sh.tab);
+    SnpSlot* info = sh.info;
+    double* s_l2 = sh.l2;
+    double* s_l2d = sh.l2d;
+    int* s_wsa = sh.wsa;
+    int* s_wsd = sh.wsd;
+    int* s_wse = sh.wse;
+
+    const int lane = threadIdx.x;
+    const int i = lane & 31, h = lane >> 5;
+    const int I = it.x, J0 = it.y;
+
+    for (int s = lane; s < NS; s += 64) {
+        const int g = s < 32 ? I * 32 + s : (J0 + (s - 32) / 32) * 32 + (s & 31);
+        const float4 l01 = *reinterpret_cast<const float4*>(lut + (size_t)g * 4);
+        const float4 l23 = *reinterpret_cast<const float4*>(lut + (size_t)g * 4 + 2);
+        tab[0][s] = make_float2(l01.x, l01.y);
+        tab[1][s] = make_float2(l01.z, l01.w);
+        tab[2][s] = make_float2(l23.x, l23.y);
+        tab[3][s] = make_float2(l23.z, l23.w);
+        SnpSlot si;
+        si.g = g;
+        if (g < n_snp) {
+            si.pos = pos[g]; si.L = Lw[g]; si.R = Rw[g]; si.fl = sflags[g];
+        } else {
+            si.pos = 0.0; si.L = -1; si.R = -2; si.fl = 0;
+        }
+        info[s] = si;
+        s_l2[s] = 0.0; s_l2d[s] = 0.0;
+        s_wsa[s] = 0; s_wsd[s] = 0; s_wse[s] = 0;
+    }
+    __syncthreads();
+
+    f32x16 aa[NC], ar[NC], ra[NC], haa[NC], har[NC], hra[NC];
+#pragma unroll
+    for (int b = 0; b < NC; ++b) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            aa[b][r] = 0.f; haa[b][r] = 0.f;
+            if (DOM) { ar[b][r] = 0.f; ra[b][r] = 0.f; har[b][r] = 0.f; hra[b][r] = 0.f; }
+        }
+    }
+
+    const uint4* rowp = reinterpret_cast<const uint4*>(geno + (size_t)(I * 32 + i) * (size_t)pitch_words) + h;
+    const uint4* colp[NC];
+#pragma unroll
+    for (int b = 0; b < NC; ++b)
+        colp[b] = reinterpret_cast<const uint4*>(geno + (size_t)((J0 + b) * 32 + i) * (size_t)pitch_words) + h;
+
+    const char* tabc = reinterpret_cast<const char*>(&tab[0][0]);
+    const uint32_t rbase = (uint32_t)i * 8u;
+
+    uint4 nr = rowp[0];
+    uint4 nc[NC];
+#pragma unroll
+    for (int b = 0; b < NC; ++b) nc[b] = colp[b][0];
+
+    for (int t0 = 0; t0 < n_it; t0 += FLUSH_IT) {
+      const int t1 = min(t0 + FLUSH_IT, n_it);
+      for (int t = t0; t < t1; ++t) {
+        const uint4 wr4 = nr;
+        uint4 wc4[NC];
+#pragma unroll
+        for (int b = 0; b < NC; ++b) wc4[b] = nc[b];
+        if (t + 1 < n_it) {  // prefetch the next 32-byte chunk of every row
+            nr = rowp[2 * (t + 1)];
+#pragma unroll
+            for (int b = 0; b < NC; ++b) nc[b] = colp[b][2 * (t + 1)];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t wr = q == 0 ? wr4.x : q == 1 ? wr4.y : q == 2 ? wr4.z : wr4.w;
+            uint32_t wc[NC];
+#pragma unroll
+            for (int b = 0; b < NC; ++b) wc[b] = q == 0 ? wc4[b].x : q == 1 ? wc4[b].y : q == 2 ? wc4[b].z : wc4[b].w;
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                const uint32_t cr = (wr >> (2 * s)) & 3u;
+                const float2 vr = *reinterpret_cast<const float2*>(tabc + cr * (uint32_t)(NS * 8) + rbase);
+#pragma unroll
+                for (int b = 0; b < NC; ++b) {
+                    const uint32_t cc = (wc[b] >> (2 * s)) & 3u;
+                    const float2 vc = *reinterpret_cast<const float2*>(tabc + cc * (uint32_t)(NS * 8) +
+                                                                       (uint32_t)(32 + 32 * b) * 8u + rbase);
+                    aa[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(vr.x, vc.x, aa[b], 0, 0, 0);
+                    if (DOM) {
+                        ar[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(vr.x, vc.y, ar[b], 0, 0, 0);
+                        ra[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(vr.y, vc.x, ra[b], 0, 0, 0);
+                    }
+                }
+            }
+        }
+      }
+      // flush the fp32 chain of the last <= 2048 samples into the second-level sum
+#pragma unroll
+      for (int b = 0; b < NC; ++b) {
+          haa[b] += aa[b];
+          aa[b] = 0.f;
+          if (DOM) { har[b] += ar[b]; hra[b] += ra[b]; ar[b] = 0.f; ra[b] = 0.f; }
+      }
+    }
+
+    // ---- fused epilogue: r2adj, window / MAF / residual masks, per-SNP sums ------------------
+#pragma unroll
+    for (int b = 0; b < NC; ++b) {
+        const int sj = 32 + 32 * b + i;
+        const SnpSlot cj = info[sj];
+        const bool diag = (J0 + b) == I;
+        const bool pj = cj.fl & 1, rpj = (cj.fl & 2) != 0;
+        const bool compj = cj.L >= 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int si = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const SnpSlot ci = info[si];
+            const bool pi = ci.fl & 1, rpi = (ci.fl & 2) != 0;
+            const bool inwin = fabs(cj.pos - ci.pos) <= ld_wind && ci.g != cj.g;
+            // j in N(i): SNP i's window scan (stream.h:142-155) covers j
+            const bool nij = inwin && ci.L >= 0 && cj.g >= ci.L && cj.g <= ci.R && pj;
+            // i in N(j): only for off-diagonal blocks (a diagonal block holds both orders)
+            const bool nji = !diag && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
+            if (nij || nji) {
+                const double r2 = r2_adjusted((double)haa[b][r], n_org);
+                if (nij) { atomicAdd(&s_l2[si], r2); atomicAdd(&s_wsa[si], 1); }
+                if (nji) { atomicAdd(&s_l2[sj], r2); atomicAdd(&s_wsa[sj], 1); }
+                if (DOM) {
+                    if (nij && rpj) {  // a_i . r_j -> L2D_i (ldscalc.h:40-46)
+                        const double rd = r2_adjusted((double)har[b][r], n_org);
+                        atomicAdd(&s_l2d[si], rd); atomicAdd(&s_wsd[si], 1);
+                        if (rd > rsq_thr) atomicAdd(&s_wse[si], 1);
+                    }
+                    if (nji && rpi) {  // r_i . a_j -> L2D_j
+                        const double rd = r2_adjusted((double)hra[b][r], n_org);
+                        atomicAdd(&s_l2d[sj], rd); atomicAdd(&s_wsd[sj], 1);
+                        if (rd > rsq_thr) atomicAdd(&s_wse[sj], 1);
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int s = lane; s < NS; s += 64) {
+        const int g = info[s].g;
+        if (g < own_lo || g >= own_hi || g >= n_snp) continue;
+        if (s_wsa[s]) {
+            unsafeAtomicAdd(&l2_acc[g], s_l2[s]);
+            atomicAdd(&ws_acc[g], s_wsa[s]);
+        }
+        if (DOM && s_wsd[s]) {
+            unsafeAtomicAdd(&l2d_acc[g], s_l2d[s]);
+            atomicAdd(&ws_acc[(size_t)n_snp + g], s_wsd[s]);
+            if (s_wse[s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + g], s_wse[s]);
+        }
+    }
+}
+
+// One launch for all work items; `nc` (1 or 2 column blocks) is wave-uniform per item.
+template <bool DOM>
+__global__ void __launch_bounds__(64) band_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
+                                                  const float2* __restrict__ lut, const int4* __restrict__ items,
+                                                  const double* __restrict__ pos, const int* __restrict__ Lw,
+                                                  const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
+                                                  int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
+                                                  int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
+                                                  int* __restrict__ ws_acc) {
+    __shared__ BandLds sh;
+    const int4 it = items[blockIdx.x];
+    if (it.z == 2)
+        band_body<2, DOM>(sh, it, geno, pitch_words, n_it, lut, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr,
+                          own_lo, own_hi, l2_acc, l2d_acc, ws_acc);
+    else
+        band_body<1, DOM>(sh, it, geno, pitch_words, n_it, lut, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr,
+                          own_lo, own_hi, l2_acc, l2d_acc, ws_acc);
+}
+
+// ------------------------------------------------------------------------------------------
+// 4. finalize
+// ------------------------------------------------------------------------------------------
+__global__ void finalize_kernel(const int* __restrict__ Lw, const double* __restrict__ l2_acc,
+                                const double* __restrict__ l2d_acc, const int* __restrict__ ws_acc, int n_snp,
+                                int own_lo, int own_hi, int dom, double* __restrict__ l2, double* __restrict__ l2d,
+                                int* __restrict__ ws3) {
+    const int g = own_lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= own_hi) return;
+    const double qnan = __builtin_nan("");
+    if (Lw[g] >= 0) {  // computed SNP (ldscalc.h:49-54)
+        l2[g] = 1.0 + l2_acc[g];
+        l2d[g] = dom ? l2d_acc[g] : qnan;
+        ws3[g] = ws_acc[g];
+        ws3[(size_t)n_snp + g] = dom ? ws_acc[(size_t)n_snp + g] : -1;
+        ws3[2 * (size_t)n_snp + g] = dom ? ws_acc[2 * (size_t)n_snp + g] : -1;
+    } else {  // not computed: initial values of ldscalc.h:16-21
+        l2[g] = qnan; l2d[g] = qnan;
+        ws3[g] = -1; ws3[(size_t)n_snp + g] = -1; ws3[2 * (size_t)n_snp + g] = -1;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// synthetic .bed generator (benchmarks / full-size tests)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+__device__ __forceinline__ float u01(uint32_t v) { return ((v >> 8) + 0.5f) * (1.0f / 16777216.0f); }
+__device__ __forceinline__ float2 normal2(uint64_t key) {
+    const uint64_t r = splitmix64(key);
+    const float u1 = u01((uint32_t)r), u2 = u01((uint32_t)(r >> 32));
+    const float rad = sqrtf(-2.0f * __logf(u1));
+    float s, c;
+    __sincosf(6.283185307f * u2, &s, &c);
+    return make_float2(rad * c, rad * s);
+}
+
+// Thread = one byte column (4 samples, 8 haplotypes); loops over SNPs carrying the AR(1) latent
+// state.  PLINK-correct packing: sample 4b+k in bits 2k..2k+1; padding bits zero.
+__global__ void __launch_bounds__(256) synth_bed_kernel(uint8_t* __restrict__ rows, int n_snp, int n_org, int nb,
+                                                        const float* __restrict__ thr, float rho, float missing,
+                                                        uint64_t seed) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const float sq = sqrtf(1.0f - rho * rho);
+    float z[8];
+    const uint64_t base = splitmix64(seed) ^ ((uint64_t)b << 20);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float2 n = normal2(base + 0xFFFFFull * 4 + k);
+        z[2 * k] = n.x; z[2 * k + 1] = n.y;
+    }
+    for (int j = 0; j < n_snp; ++j) {
+        const uint64_t key = splitmix64(base ^ ((uint64_t)j * 0x9E3779B97F4A7C15ull));
+        if (j > 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float2 n = normal2(key + k);
+                z[2 * k] = rho * z[2 * k] + sq * n.x;
+                z[2 * k + 1] = rho * z[2 * k + 1] + sq * n.y;
+            }
+        }
+        const float tj = thr[j];
+        const uint64_t mk = splitmix64(key + 17);
+        uint32_t byte = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (4 * b + k >= n_org) break;
+            const int g = (z[2 * k] < tj) + (z[2 * k + 1] < tj);
+            const bool miss = ((mk >> (16 * k)) & 0xFFFF) < (uint32_t)(missing * 65536.0f);
+            const uint32_t code = miss ? 1u : (g == 0 ? 0u : g == 1 ? 2u : 3u);
+            byte |= code << (2 * k);
+        }
+        rows[(size_t)j * nb + b] = (uint8_t)byte;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------
+hipError_t launch_repack_count(const uint8_t* rows, uint32_t* geno, int n_snp, int nb, int pitch_words,
+                               uint32_t tail_keep, int* counts, hipStream_t st) {
+    if (n_snp <= 0) return hipSuccess;
+    hipLaunchKernelGGL(repack_count_kernel, dim3(n_snp), dim3(256), 0, st, rows, geno, n_snp, nb, pitch_words,
+                       tail_keep, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_snp_stats(const int* counts, const double* pos, int n_snp, int n_snp_pad, int n_org, double maf_thr,
+                            double std_thr, float2* lut, uint8_t* sflags, double* maf_out, double* rstd_out,
+                            hipStream_t st) {
+    const int blocks = (n_snp_pad + 255) / 256;
+    hipLaunchKernelGGL(snp_stats_kernel, dim3(blocks), dim3(256), 0, st, counts, pos, n_snp, n_snp_pad, n_org, maf_thr,
+                       std_thr, lut, sflags, maf_out, rstd_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_band(bool dom, int n_items, const uint32_t* geno, int pitch_words, int n_it, const float2* lut,
+                       const int4* items, const double* pos, const int* Lw, const int* Rw, const uint8_t* sflags,
+                       int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo, int own_hi,
+                       double* l2_acc, double* l2d_acc, int* ws_acc, hipStream_t st) {
+    if (n_items <= 0) return hipSuccess;
+    if (dom)
+        hipLaunchKernelGGL((band_kernel<true>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, lut, items,
+                           pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc,
+                           ws_acc);
+    else
+        hipLaunchKernelGGL((band_kernel<false>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, lut, items,
+                           pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc,
+                           ws_acc);
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2d_acc, const int* ws_acc, int n_snp,
+                           int own_lo, int own_hi, bool dom, double* l2, double* l2d, int* ws3, hipStream_t st) {
+    const int n = own_hi - own_lo;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, st, Lw, l2_acc, l2d_acc, ws_acc, n_snp,
+                       own_lo, own_hi, dom ? 1 : 0, l2, l2d, ws3);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_bed(uint8_t* rows, int n_snp, int n_org, int nb, const float* thr, float rho, float missing,
+                            uint64_t seed, hipStream_t st) {
+    hipLaunchKernelGGL(synth_bed_kernel, dim3((nb + 255) / 256), dim3(256), 0, st, rows, n_snp, n_org, nb, thr, rho,
+                       missing, seed);
+    return hipGetLastError();
+}
+
+}  // namespace nldsc

@@ -1,0 +1,114 @@
+"""Python handle on the GPU engine (C ABI `nldsc_engine_*`, include/nldsc_ld.h).
+
+`Engine` keeps a .bed image resident in HBM and runs the LD-score hot path over it; it is
+what the benchmark, the GPU parity tests and the multi-GPU driver use.  `calculate` is the
+one-shot equivalent of the reference's `_ldscore.calculate(params)`
+(nldsc/ldscore/_ldscore/ldscalc.h:8-65).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+
+class Engine:
+    def __init__(self, device: int = -1):
+        L = _lib.lib()
+        self._h = ctypes.c_void_p()
+        err = _lib.errbuf()
+        _lib.check(L.nldsc_engine_create(int(device), ctypes.byref(self._h), err, len(err)), err)
+        self.n_snp = 0
+        self.n_org = 0
+
+    def close(self):
+        if self._h:
+            _lib.lib().nldsc_engine_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- loading ------------------------------------------------------------------------
+    def load_bed_file(self, path: str, n_snp: int, n_org: int):
+        err = _lib.errbuf()
+        _lib.check(_lib.lib().nldsc_engine_load_bed_file(self._h, path.encode(), n_snp, n_org, err, len(err)), err)
+        self.n_snp, self.n_org = n_snp, n_org
+
+    def load_bed_bytes(self, bed, n_snp: int, n_org: int):
+        """`bed`: the whole .bed content (bytes / uint8 numpy array), magic included."""
+        buf = np.frombuffer(bed, dtype=np.uint8) if isinstance(bed, (bytes, bytearray)) else np.ascontiguousarray(bed, np.uint8)
+        err = _lib.errbuf()
+        _lib.check(_lib.lib().nldsc_engine_load_bed_host(self._h, buf.ctypes.data, buf.nbytes, n_snp, n_org, err,
+                                                         len(err)), err)
+        self.n_snp, self.n_org = n_snp, n_org
+
+    def load_bed_device(self, ptr: int, nbytes: int, n_snp: int, n_org: int):
+        """Copy a .bed image that already lives in this device's memory (e.g. a torch tensor)."""
+        err = _lib.errbuf()
+        _lib.check(_lib.lib().nldsc_engine_load_bed_device(self._h, ctypes.c_void_p(ptr), nbytes, n_snp, n_org, err,
+                                                           len(err)), err)
+        self.n_snp, self.n_org = n_snp, n_org
+
+    # ---- compute ------------------------------------------------------------------------
+    def run(self, ld_wind, maf, std_thr, rsq_thr, positions, *, own=None, flags=0, out=None):
+        """LD scores for owned SNPs [own[0], own[1]) (default all).  Returns dict of numpy arrays
+        (entries outside the owned range are NaN / -1, or whatever `out` held)."""
+        n = self.n_snp
+        own = (0, n) if own is None else own
+        p, _keep = _lib.make_params(n, self.n_org, ld_wind, maf, std_thr, rsq_thr, positions, flags=flags)
+        if out is None:
+            arrs, res = _lib.alloc_result(n)
+        else:
+            arrs = out
+            d, i = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)
+            res = _lib.Result(*(arrs[k].ctypes.data_as(d if arrs[k].dtype == np.float64 else i)
+                                for k in ("l2", "l2d", "maf", "residuals_std", "l2_ws", "l2d_ws", "l2d_wse")))
+        err = _lib.errbuf()
+        _lib.check(_lib.lib().nldsc_engine_run(self._h, ctypes.byref(p), int(own[0]), int(own[1]),
+                                               ctypes.byref(res), err, len(err)), err)
+        return arrs
+
+    def timings(self) -> dict:
+        ms = (ctypes.c_double * 6)()
+        flop, pairs = ctypes.c_double(), ctypes.c_double()
+        nl = ctypes.c_int32()
+        _lib.lib().nldsc_engine_timings(self._h, ms, ctypes.byref(flop), ctypes.byref(pairs), ctypes.byref(nl))
+        keys = ("repack_ms", "stats_ms", "schedule_ms", "band_ms", "finalize_ms", "total_ms")
+        d = {k: ms[i] for i, k in enumerate(keys)}
+        d.update(flop_alg=flop.value, pairs=pairs.value, band_launches=nl.value)
+        return d
+
+
+def calculate(bedfile: str, n_snp, n_org, ld_wind, maf, std_thr, rsq_thr, positions, *, flags=0, device=-1) -> dict:
+    """One-shot C-ABI call `nldsc_ld_calculate` (file -> GPU -> results)."""
+    p, _keep = _lib.make_params(n_snp, n_org, ld_wind, maf, std_thr, rsq_thr, positions, bedfile=bedfile,
+                                flags=flags, device=device)
+    arrs, res = _lib.alloc_result(n_snp)
+    err = _lib.errbuf()
+    _lib.check(_lib.lib().nldsc_ld_calculate(ctypes.byref(p), ctypes.byref(res), err, len(err)), err)
+    return arrs
+
+
+def device_count() -> int:
+    return int(_lib.lib().nldsc_device_count())
+
+
+def synth_bed_device(device: int, ptr: int, n_snp: int, n_org: int, thr: np.ndarray, rho: float = 0.9,
+                     missing: float = 0.01, seed: int = 7):
+    t = np.ascontiguousarray(thr, dtype=np.float32)
+    err = _lib.errbuf()
+    _lib.check(_lib.lib().nldsc_synth_bed_device(int(device), ctypes.c_void_p(ptr), n_snp, n_org,
+                                                 t.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), float(rho),
+                                                 float(missing), int(seed), err, len(err)), err)

@@ -1,0 +1,95 @@
+"""`estimate_lds` — the caller of the hot path (behaviour of nldsc/ldscore/routine.py:15-102).
+
+Parses .bed/.bim/.fam, validates parameters, builds `_ldscore.LDScoreParams`, runs
+`_ldscore.calculate` on the GPU, optionally prints the summary, and writes the TSV
+`CHR SNP BP L2 L2D [MAF WSA WSD WSDE RSTD]` (tab-separated, `%.5f`, NaN as empty field)
+to `out`.  Additions: `write_m` writes the `M`/`MD` file the h2 reader looks for
+(nldsc/h2/common.py:115-132,142-144) with exactly the values its fallback would compute.
+"""
+from __future__ import annotations
+
+from pathlib import Path
+
+import numpy as np
+import pandas as pd
+
+from ..core.common import elapsed_time
+from ..core.logger import log
+from . import _ldscore as lds
+from .common import BIMFile, LDWindow, MAF, PLINKFile, ResidualsSTDThreshold, RSQThreshold
+
+__all__ = ["estimate_lds", "make_output", "show_summary", "m_values", "write_m_file"]
+
+
+def show_summary(ld) -> None:
+    import click
+    pd.set_option("display.precision", 3)
+    data = pd.DataFrame({"L2": list(ld.l2), "L2D": list(ld.l2d), "MAF": list(ld.maf)})
+    click.echo("=" * 62)
+    click.echo("L2/L2D/MAF Correlation matrix\n" + str(data.corr()))
+    description = data.describe().drop("count")
+    click.echo(f"\nShort summary:\n"
+               f"- Number of additive non-null LD: {data['L2'].count()}\n"
+               f"- Number of non-additive non-null LD: {data['L2D'].count()}\n"
+               + str(description))
+    click.echo("=" * 62)
+
+
+def make_output(bim: BIMFile, ld, *, extra: bool = False) -> pd.DataFrame:
+    cols = {"CHR": bim.chr.reset_index(drop=True), "SNP": bim.snp.reset_index(drop=True),
+            "BP": bim.bp.reset_index(drop=True), "L2": pd.Series(list(ld.l2)), "L2D": pd.Series(list(ld.l2d))}
+    if extra:
+        cols.update(MAF=pd.Series(list(ld.maf)), WSA=pd.Series(list(ld.l2_ws)), WSD=pd.Series(list(ld.l2d_ws)),
+                    WSDE=pd.Series(list(ld.l2d_wse)), RSTD=pd.Series(list(ld.residuals_std)))
+    return pd.DataFrame(cols)
+
+
+def m_values(bim: BIMFile, ld) -> tuple[int, int]:
+    """M, MD as LDScoreReader derives them without an .M file (h2/common.py:128-130): rows
+    surviving dropna + SNP de-duplication, and M * mean(WSDE / WSA)."""
+    df = make_output(bim, ld, extra=True).sort_values(by=["CHR", "BP"]).dropna().drop_duplicates(subset="SNP")
+    m = len(df["L2"])
+    md = m * (df["WSDE"] / df["WSA"]).mean()
+    return int(m), int(md)
+
+
+def write_m_file(path: str, m: int, md: int) -> None:
+    pd.DataFrame({"M": [m], "MD": [md]}).to_csv(path, sep="\t", index=False)
+
+
+@elapsed_time
+def estimate_lds(bfile: str, ld_wind: float, wind_metric: str, maf_thr: float = 1e-5, std_thr: float = 1e-5,
+                 rsq_thr: float | None = None, *, out: str | None = None, extra: bool = False, summary: bool = False,
+                 verbose: int = 0, write_m: bool = False, flags: int = 0, device: int | None = None):
+    bed_, bim_, fam_ = PLINKFile.parse(bfile)
+    ld_wind_ = LDWindow(ld_wind, metric=wind_metric)
+    maf_thr_ = MAF(maf_thr)
+    std_thr_ = ResidualsSTDThreshold(std_thr)
+    if rsq_thr is None:
+        rsq_thr = 1.0 / bim_.n_snp
+    rsq_thr_ = RSQThreshold(rsq_thr)
+    log.info(f"Input: {bed_.data}, size: (M={bim_.n_snp}, N={fam_.n_org})")
+
+    params = lds.LDScoreParams(
+        bfile=bed_.data, n_snp=bim_.n_snp, n_org=fam_.n_org, ld_wind=ld_wind_.data, maf=maf_thr_.data,
+        std_thr=std_thr_.data, rsq_thr=rsq_thr_.data,
+        positions=np.asarray(getattr(bim_, ld_wind_.metric), dtype=np.float64).tolist())
+    params.flags = int(flags)
+    if device is not None:
+        params.device = int(device)
+    log.info("Running the estimator. It may take a long time.")
+    ld = lds.calculate(params)
+    log.info("Estimation completed")
+
+    if summary:
+        show_summary(ld)
+    out_df = make_output(bim_, ld, extra=extra)
+    if out:
+        log.info("Writing data to disk...")
+        out_df.to_csv(out, sep="\t", index=False, float_format="%.5f")
+        if write_m:
+            m, md = m_values(bim_, ld)
+            write_m_file(str(Path(out).with_suffix(".M")), m, md)
+        log.info(f"Completed. File: {out}")
+        return None
+    return out_df

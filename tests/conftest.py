@@ -1,0 +1,60 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+GOLDEN = os.path.join(REPO, "tests", "golden")
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); run with -m gpu")
+
+
+def golden_sets():
+    with open(os.path.join(GOLDEN, "sets.json")) as fh:
+        return json.load(fh)
+
+
+def load_set(name):
+    """(bed bytes, positions, meta, oracle result, f64 result) of a committed fixture."""
+    import pandas as pd
+    meta = golden_sets()[name]
+    bed = open(os.path.join(GOLDEN, name + ".bed"), "rb").read()
+    bim = pd.read_csv(os.path.join(GOLDEN, name + ".bim"), sep="\t", header=None)
+    pos = (bim[2] if meta["metric"] == "cm" else bim[3]).to_numpy(dtype=np.float64)
+    orc = dict(np.load(os.path.join(GOLDEN, name + ".oracle.npz")))
+    f64 = dict(np.load(os.path.join(GOLDEN, name + ".f64.npz")))
+    return bed, pos, meta, orc, f64
+
+
+# Tolerances: integer window counts exact; MAF exact;
+# residual std relative 1e-5; L2 |d| <= 1e-3 + 1e-4 |L2|; L2D |d| <= 1e-5 + 1e-4 |L2D|;
+# WSDE exact except pairs whose r2adj lies within 1e-6 of rsq_thr (budget: 0.1 % of SNPs, +-1).
+TOL = dict(l2=(1e-3, 1e-4), l2d=(1e-5, 1e-4), residuals_std=(0.0, 1e-5), maf=(0.0, 0.0))
+
+
+def assert_ld_close(got: dict, exp: dict, *, tol=TOL, wse_budget=0.001, label="", skip=None):
+    skip = np.zeros(len(exp["l2"]), bool) if skip is None else skip
+    keep = ~skip
+    for k in ("l2_ws", "l2d_ws"):
+        bad = np.flatnonzero((got[k] != exp[k]) & keep)
+        assert bad.size == 0, f"{label} {k} differs at {bad[:10]}: got {got[k][bad[:10]]} exp {exp[k][bad[:10]]}"
+    d = np.abs(got["l2d_wse"].astype(np.int64) - exp["l2d_wse"]) * keep
+    assert d.max(initial=0) <= 1 and (d > 0).sum() <= max(1, int(wse_budget * len(d))), \
+        f"{label} l2d_wse differs at {np.flatnonzero(d)[:10]}"
+    for k, (atol, rtol) in tol.items():
+        g, e = got[k][keep], exp[k][keep]
+        nan_g, nan_e = np.isnan(g), np.isnan(e)
+        bad = np.flatnonzero(nan_g != nan_e)
+        assert bad.size == 0, f"{label} {k} NaN pattern differs at {np.flatnonzero(keep)[bad[:10]]}"
+        m = ~nan_e
+        err = np.abs(g[m] - e[m])
+        lim = atol + rtol * np.abs(e[m])
+        bad = np.flatnonzero(err > lim)
+        assert bad.size == 0, (f"{label} {k}: {bad.size} out of tolerance, worst |d|={err.max():.3g} "
+                               f"at {np.flatnonzero(keep)[np.flatnonzero(m)[bad[:5]]]}")

@@ -1,0 +1,179 @@
+"""GPU parity: the HIP path (through the C ABI / the pybind11 drop-in) against the oracle.
+
+Tolerances are those of conftest.TOL.  Integer outputs (window sizes) and
+MAF are exact; NaN patterns are exact.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, REPO, assert_ld_close, golden_sets, load_set
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+SETS = sorted(golden_sets())
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from nldsc_amd.engine import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def run_set(engine, name, flags=0, own=None):
+    bed, pos, meta, orc, f64 = load_set(name)
+    engine.load_bed_bytes(bed, meta["n_snp"], meta["n_org"])
+    got = engine.run(meta["ld_wind"], meta["maf"], meta["std_thr"], meta["rsq_thr"], pos, flags=flags, own=own)
+    return got, meta, orc, f64, pos, bed
+
+
+@pytest.mark.parametrize("name", SETS)
+def test_golden_sets_vs_oracle_and_f64(engine, name):
+    got, meta, orc, f64, _, _ = run_set(engine, name)
+    # MAF: the same fp32 formula from integer counts -> bit-exact
+    np.testing.assert_array_equal(got["maf"], f64["maf"])
+    np.testing.assert_array_equal(got["maf"], orc["maf"])
+    assert_ld_close(got, f64, label=f"{name} vs f64")
+    assert_ld_close(got, orc, label=f"{name} vs oracle")
+    # tighter against the fp64 restatement: the GPU path differs only by fp32 lookup values and
+    # 2048-sample fp32 MFMA chains
+    m = ~np.isnan(f64["l2"])
+    assert np.max(np.abs(got["l2"][m] - f64["l2"][m]), initial=0) < 5e-5
+    m = ~np.isnan(f64["l2d"])
+    assert np.max(np.abs(got["l2d"][m] - f64["l2d"][m]), initial=0) < 5e-6
+    m = ~np.isnan(f64["residuals_std"])
+    np.testing.assert_allclose(got["residuals_std"][m], f64["residuals_std"][m], rtol=1e-12)
+
+
+@pytest.mark.parametrize("name", ["n1001", "n1003"])
+def test_sharded_runs_assemble_to_full(engine, name):
+    full, meta, _, _, pos, _ = run_set(engine, name)
+    M = meta["n_snp"]
+    cuts = [0, 17, 400, 401, 777, M]
+    parts = {k: np.full_like(v, np.nan if v.dtype.kind == "f" else -7) for k, v in full.items()}
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        engine.run(meta["ld_wind"], meta["maf"], meta["std_thr"], meta["rsq_thr"], pos, own=(a, b), out=parts)
+    for k in full:
+        if full[k].dtype.kind == "i":
+            np.testing.assert_array_equal(parts[k], full[k], err_msg=k)
+        else:
+            np.testing.assert_allclose(parts[k], full[k], rtol=1e-12, atol=1e-13, err_msg=k)
+
+
+def test_strict_plink_order(engine):
+    from nldsc_amd import _lib
+    name = "n1003"
+    got, meta, _, _, pos, bed = run_set(engine, name, flags=_lib.FLAG_STRICT_PLINK_ORDER)
+    rows = np.frombuffer(bed, np.uint8, offset=3).reshape(meta["n_snp"], -1)
+    exp = O.run_f64(rows, meta["n_org"], meta["ld_wind"], meta["maf"], meta["std_thr"], meta["rsq_thr"], pos,
+                    strict=True)
+    assert_ld_close(got, exp, label="strict")
+    ref, *_ = run_set(engine, name)
+    assert not np.allclose(np.nan_to_num(ref["l2"]), np.nan_to_num(got["l2"]))  # N%4=3: the order matters
+
+
+def test_additive_only(engine):
+    from nldsc_amd import _lib
+    full, *_ = run_set(engine, "n1002")
+    got, *_ = run_set(engine, "n1002", flags=_lib.FLAG_ADDITIVE_ONLY)
+    np.testing.assert_allclose(got["l2"], full["l2"], rtol=1e-12, atol=1e-13)
+    np.testing.assert_array_equal(got["l2_ws"], full["l2_ws"])
+    assert np.isnan(got["l2d"]).all()
+    assert (got["l2d_ws"] == -1).all() and (got["l2d_wse"] == -1).all()
+
+
+def test_pybind_calculate_on_files():
+    from nldsc_amd.ldscore import _ldscore as lds
+    for name in ("n1000", "allmiss"):
+        _, pos, meta, orc, f64 = load_set(name)
+        p = lds.LDScoreParams(os.path.join(GOLDEN, name + ".bed"), n_snp=meta["n_snp"], n_org=meta["n_org"],
+                              ld_wind=meta["ld_wind"], maf=meta["maf"], std_thr=meta["std_thr"],
+                              rsq_thr=meta["rsq_thr"], positions=pos.tolist())
+        r = lds.calculate(p)
+        got = {k: np.asarray(getattr(r, k), dtype=orc[k].dtype) for k in orc}
+        assert_ld_close(got, orc, label=name)
+
+
+def test_pybind_errors(tmp_path):
+    from nldsc_amd.ldscore import _ldscore as lds
+    bad = tmp_path / "bad.bed"
+    bad.write_bytes(b"\x6c\x1b\x00" + b"\x00" * 100)
+    p = lds.LDScoreParams(str(bad), n_snp=4, n_org=100, ld_wind=1.0, maf=0.01, std_thr=1e-5, rsq_thr=0.01,
+                          positions=[0.0, 0.1, 0.2, 0.3])
+    with pytest.raises(ValueError, match="Invalid PLINK magic number"):
+        lds.calculate(p)
+    short = tmp_path / "short.bed"
+    short.write_bytes(b"\x6c\x1b\x01" + b"\x00" * 50)  # 4 SNPs x 25 B needed
+    p.bedfile = str(short)
+    with pytest.raises(RuntimeError, match="too short"):
+        lds.calculate(p)
+
+
+def test_cli_end_to_end(tmp_path):
+    out = tmp_path / "n1000.L2"
+    cmd = [sys.executable, "-m", "nldsc_amd", "ld", "--bfile", os.path.join(GOLDEN, "n1000"), "--ld-wind-cm", "1",
+           "-maf", "0.01", "--std-thr", "1e-5", "--extra", "--write-m", "--out", str(out)]
+    subprocess.run(cmd, check=True, cwd=REPO, capture_output=True, timeout=300)
+    import pandas as pd
+    got = pd.read_csv(out, sep="\t")
+    ref = pd.read_csv(os.path.join(GOLDEN, "n1000.ref.L2"), sep="\t")  # reference formatting of the oracle
+    assert list(got.columns) == list(ref.columns)
+    for c in ("CHR", "SNP", "BP", "WSA", "WSD", "WSDE", "MAF"):
+        assert got[c].equals(ref[c]) or np.allclose(got[c], ref[c], equal_nan=True), c
+    for c, tol in (("L2", 2e-5), ("L2D", 2e-5), ("RSTD", 2e-5)):
+        assert np.allclose(got[c], ref[c], atol=tol, equal_nan=True), c
+    mfile = tmp_path / "n1000.M"
+    m = pd.read_csv(mfile, sep="\t")
+    sc = ref.sort_values(by=["CHR", "BP"]).dropna().drop_duplicates(subset="SNP")
+    assert int(m["M"][0]) == len(sc)
+    assert int(m["MD"][0]) == int(len(sc) * (sc["WSDE"] / sc["WSA"]).mean())
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_small_configs_vs_f64(engine, seed):
+    """Ragged sizes: N from 3 (tiny K) to 700, M from 1 to 260, windows from a few SNPs to all."""
+    from nldsc_amd import synth
+    rng = np.random.default_rng(1000 + seed)
+    N = int(rng.choice([3, 4, 5, 7, 33, 64, 127, 255, 256, 511, 700]))
+    M = int(rng.integers(1, 260))
+    spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=float(rng.uniform(0.5, 20)), seed=seed,
+                           missing=float(rng.choice([0.0, 0.01, 0.2])))
+    if M > 10:
+        spec.negative_pos = [int(rng.integers(0, M))]
+    g = synth.genotypes(spec)
+    rows = synth.pack_bed_rows(g)
+    pos = synth.positions_cm(spec)
+    w = float(rng.choice([0.05, 0.5, 1.0, 100.0]))
+    maf, std_thr, rsq = float(rng.choice([0.0, 0.01, 0.05])), float(rng.choice([0.0, 1e-5])), 0.5 / max(M, 11)
+    engine.load_bed_bytes(synth.bed_bytes(rows), M, N)
+    got = engine.run(w, maf, std_thr, rsq, pos)
+    exp = O.run_f64(rows, N, w, maf, std_thr, rsq, pos)
+    tol = dict(l2=(1e-4, 1e-5), l2d=(1e-5, 1e-5), residuals_std=(1e-12, 1e-10), maf=(0.0, 0.0))
+    assert_ld_close(got, exp, tol=tol, wse_budget=0.02, label=f"seed{seed} N{N} M{M}")
+
+
+def test_full_size_spot_check_vs_oracle(engine):
+    """N = 315 599 (N % 4 = 3, BASELINE.json configs[2]) on a 2 000-SNP chromosome slice generated on the
+    GPU: 12 SNPs against the oracle's targets mode, the rest by invariants."""
+    from nldsc_amd import synth
+    N, M = 315_599, 2000
+    buf, pos = synth.device_bed(M, N, seed=3, length_cm=7.0)
+    engine.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
+    w, maf, std_thr, rsq = 1.0, 1e-4, 1e-5, 1.0 / M
+    got = engine.run(w, maf, std_thr, rsq, pos)
+    bed = buf.cpu().numpy().tobytes()
+    t = np.linspace(0, M - 1, 12).astype(np.int32)
+    exp = O.run_c(bed, M, N, w, maf, std_thr, rsq, pos, targets=t)
+    sub = {k: v[t] for k, v in got.items()}
+    assert_ld_close(sub, exp, label="N=315599")
+    assert (got["l2_ws"] > 100).all() and np.isfinite(got["l2"]).all()
+    # determinism of the integer outputs and closeness of a second run
+    again = engine.run(w, maf, std_thr, rsq, pos)
+    np.testing.assert_array_equal(again["l2_ws"], got["l2_ws"])
+    np.testing.assert_array_equal(again["l2d_wse"], got["l2d_wse"])
+    np.testing.assert_allclose(again["l2"], got["l2"], rtol=1e-13)

@@ -1,0 +1,92 @@
+"""The oracle against the committed golden vectors, the fp64 restatement and the reference's
+documented quirks (CPU only)."""
+import numpy as np
+import pytest
+
+from conftest import assert_ld_close, golden_sets, load_set
+from oracle import oracle as O
+
+SETS = sorted(golden_sets())
+
+
+@pytest.mark.parametrize("name", SETS)
+def test_c_oracle_reproduces_golden(name):
+    bed, pos, meta, orc, _ = load_set(name)
+    got = O.run_c(bed, meta["n_snp"], meta["n_org"], meta["ld_wind"], meta["maf"], meta["std_thr"],
+                  meta["rsq_thr"], pos, threads=1)
+    for k in orc:
+        np.testing.assert_array_equal(got[k], orc[k], err_msg=f"{name}:{k}")
+
+
+@pytest.mark.parametrize("name", SETS)
+def test_f64_restatement_reproduces_golden(name):
+    bed, pos, meta, _, f64 = load_set(name)
+    rows = np.frombuffer(bed, np.uint8, offset=3).reshape(meta["n_snp"], -1)
+    got = O.run_f64(rows, meta["n_org"], meta["ld_wind"], meta["maf"], meta["std_thr"], meta["rsq_thr"], pos)
+    for k in f64:
+        np.testing.assert_allclose(got[k], f64[k], rtol=1e-12, atol=1e-12, err_msg=f"{name}:{k}")
+
+
+@pytest.mark.parametrize("name", SETS)
+def test_c_oracle_matches_f64_restatement(name):
+    """Two independent formulations of the reference's algorithm agree within fp32 noise."""
+    _, _, _, orc, f64 = load_set(name)
+    assert_ld_close(orc, f64, label=name)
+
+
+@pytest.mark.parametrize("name", ["n1001", "n1003"])
+def test_targets_mode_equals_full_mode(name):
+    bed, pos, meta, orc, _ = load_set(name)
+    t = np.arange(0, meta["n_snp"], 13, dtype=np.int32)
+    got = O.run_c(bed, meta["n_snp"], meta["n_org"], meta["ld_wind"], meta["maf"], meta["std_thr"],
+                  meta["rsq_thr"], pos, targets=t, threads=1)
+    for k in orc:
+        np.testing.assert_array_equal(got[k], orc[k][t], err_msg=k)
+
+
+def test_unpack_order_reference_vs_plink():
+    """stream.h:55-66: high bit pair first; the last byte keeps its high N%4 pairs."""
+    row = np.array([[0b11_10_01_00, 0b00_00_10_11]], np.uint8)  # byte 0 codes (PLINK low->high) 0,1,2,3
+    ref = O.unpack_codes(row, 7)
+    assert ref.tolist() == [[3, 2, 1, 0, 0, 0, 2]]  # reference: high pairs first, then 3 high pairs of byte 1
+    strict = O.unpack_codes(row, 7, strict=True)
+    assert strict.tolist() == [[0, 1, 2, 3, 3, 2, 0]]  # PLINK order
+
+
+def test_all_missing_snp_poisons_windows():
+    _, _, _, orc, _ = load_set("allmiss")
+    j = 50
+    assert np.isnan(orc["maf"][j]) and np.isnan(orc["l2"][j])
+    in_win = np.flatnonzero(np.isnan(orc["l2"]))
+    assert j in in_win and len(in_win) > 100  # every window containing SNP 50
+    # L2D is NaN only for the SNP itself (its residual std is NaN, so it is never a dominance neighbour)
+    assert np.flatnonzero(np.isnan(orc["l2d"])).tolist() == [j]
+
+
+def test_all_missing_with_padding_pair_fails_maf():
+    _, _, _, orc, _ = load_set("allmiss_pad")
+    assert orc["maf"][50] == 0.0 and np.isnan(orc["l2"][50]) and orc["l2_ws"][50] == -1
+
+
+def test_unused_and_maf_failed_snps():
+    _, pos, meta, orc, _ = load_set("n1003")
+    for j in (103, 1199):  # position -1
+        assert pos[j] < 0 and np.isnan(orc["maf"][j]) and np.isnan(orc["l2"][j]) and orc["l2_ws"][j] == -1
+    j = 8  # monomorphic: MAF reported, no scores
+    assert orc["maf"][j] == 0.0 and np.isnan(orc["l2"][j]) and np.isnan(orc["residuals_std"][j])
+    j = 20  # hom-A1/het only: residual std exactly 0 -> never a dominance neighbour
+    assert orc["residuals_std"][j] == 0.0 and orc["l2d_ws"][j] >= 0
+
+
+def test_window_tie_is_inclusive():
+    bed, pos, meta, orc, _ = load_set("n1000")
+    a = 200
+    b = int(np.flatnonzero(pos == pos[a] + meta["ld_wind"])[0])
+    nb = O.replay_windows(pos, np.ones(len(pos), bool), meta["ld_wind"])
+    assert nb[0][b] <= a  # a is inside b's window: |pos_b - pos_a| == w counts (tools.h:41-49)
+
+
+def test_bad_magic_raises_value_error():
+    bed, pos, meta, _, _ = load_set("n1001")
+    with pytest.raises(ValueError):
+        O.run_c(b"\x00" + bed[1:], meta["n_snp"], meta["n_org"], 1.0, 0.01, 1e-5, 0.001, pos)
