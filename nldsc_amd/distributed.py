@@ -1,0 +1,105 @@
+"""Position sharding of the LD-score computation over GPUs (one process per GPU, torch.distributed).
+
+SURVEY.md §8(e): windows are local (1 cM), so a chromosome splits into contiguous SNP ranges with
+no exchange on the hot path.  Rank g owns SNPs [lo_g, hi_g) and computes every pair that touches an
+owned SNP (the engine recomputes the pairs it shares with the neighbouring ranges — a halo of about
+one window — instead of exchanging partial sums).  The per-SNP score tables are then gathered to
+rank 0 in one collective (RCCL over xGMI with the "nccl" backend, gloo on CPU).
+
+Whole-genome runs (several chromosome files) assign chromosome units to ranks by longest-processing-
+time-first on the estimated pair count (`assign_units`).
+"""
+from __future__ import annotations
+
+from typing import Callable, Sequence
+
+import numpy as np
+
+RESULT_KEYS = ("l2", "l2d", "maf", "residuals_std", "l2_ws", "l2d_ws", "l2d_wse")
+
+
+def window_work(positions: np.ndarray, ld_wind: float) -> np.ndarray:
+    """Estimated in-window neighbours per SNP (two-pointer sweep over sorted used positions)."""
+    pos = np.asarray(positions, dtype=np.float64)
+    used = pos >= 0
+    p = pos[used]
+    lo = np.searchsorted(p, p - ld_wind, side="left")
+    hi = np.searchsorted(p, p + ld_wind, side="right")
+    w = np.zeros(len(pos))
+    w[used] = (hi - lo - 1).clip(min=0) + 1.0  # + per-SNP fixed cost
+    return w
+
+
+def shard_ranges(positions: np.ndarray, ld_wind: float, world: int) -> list[tuple[int, int]]:
+    """Contiguous SNP ranges with about equal estimated pair work."""
+    n = len(positions)
+    if world <= 1 or n == 0:
+        return [(0, n)]
+    c = np.concatenate([[0.0], np.cumsum(window_work(positions, ld_wind))])
+    cuts = [0] + [int(np.searchsorted(c, c[-1] * g / world, side="left")) for g in range(1, world)] + [n]
+    cuts = np.maximum.accumulate(np.clip(cuts, 0, n))
+    return [(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:])]
+
+
+def assign_units(work: Sequence[float], world: int) -> list[list[int]]:
+    """LPT: unit indices per rank, heaviest units first onto the least loaded rank."""
+    load = np.zeros(world)
+    out: list[list[int]] = [[] for _ in range(world)]
+    for u in sorted(range(len(work)), key=lambda k: -work[k]):
+        g = int(np.argmin(load))
+        out[g].append(u)
+        load[g] += work[u]
+    return out
+
+
+def gather_ranges(local: dict, own: tuple[int, int], n_snp: int, *, device=None) -> dict | None:
+    """Gather every rank's owned slice of the result table; the full table on rank 0, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    lo, hi = own
+    n_own = hi - lo
+    span = torch.tensor([lo, hi], dtype=torch.int64, device=device)
+    spans = [torch.empty_like(span) for _ in range(world)]
+    dist.all_gather(spans, span)
+    width = max(int(s[1] - s[0]) for s in spans)
+    tab = np.full((len(RESULT_KEYS), max(width, 1)), np.nan)
+    for k, key in enumerate(RESULT_KEYS):
+        tab[k, :n_own] = np.asarray(local[key][lo:hi], dtype=np.float64)
+    t = torch.from_numpy(tab)
+    if device is not None:
+        t = t.to(device)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    if rank != 0:
+        return None
+    full = {k: (np.full(n_snp, np.nan) if k in RESULT_KEYS[:4] else np.full(n_snp, -1, np.int32))
+            for k in RESULT_KEYS}
+    for s, part in zip(spans, parts):
+        a, b = int(s[0]), int(s[1])
+        arr = part.cpu().numpy()
+        for k, key in enumerate(RESULT_KEYS):
+            v = arr[k, : b - a]
+            full[key][a:b] = v if full[key].dtype.kind == "f" else v.astype(np.int32)
+    return full
+
+
+def calculate_sharded(load_and_run: Callable[[tuple[int, int]], dict], positions: np.ndarray, ld_wind: float,
+                      n_snp: int, *, device=None) -> dict | None:
+    """Run `load_and_run(own_range) -> result dict` on this rank's range and gather to rank 0."""
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    own = shard_ranges(positions, ld_wind, world)[rank]
+    local = load_and_run(own)
+    return gather_ranges(local, own, n_snp, device=device)
+
+
+def engine_runner(bed_path: str, n_snp: int, n_org: int, ld_wind: float, maf: float, std_thr: float,
+                  rsq_thr: float, positions: np.ndarray, *, flags: int = 0, device: int = 0):
+    """`load_and_run` for calculate_sharded backed by this rank's GPU engine."""
+    def run(own):
+        from .engine import Engine
+        with Engine(device) as e:
+            e.load_bed_file(bed_path, n_snp, n_org)
+            return e.run(ld_wind, maf, std_thr, rsq_thr, positions, own=own, flags=flags)
+    return run

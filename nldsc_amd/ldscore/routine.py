@@ -57,6 +57,42 @@ def write_m_file(path: str, m: int, md: int) -> None:
     pd.DataFrame({"M": [m], "MD": [md]}).to_csv(path, sep="\t", index=False)
 
 
+class _Result:
+    """LDScoreResult-shaped holder for tables assembled from several ranks."""
+
+    def __init__(self, d: dict):
+        for k, v in d.items():
+            setattr(self, k, v.tolist())
+
+
+def _process_group():
+    """The torch.distributed module when launched by torchrun with WORLD_SIZE > 1, else None."""
+    import os
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return None
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    return dist
+
+
+def _calculate_sharded(dist, params):
+    import os
+
+    import torch
+
+    from .. import distributed as D
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pos = np.asarray(params.positions, dtype=np.float64)
+    run = D.engine_runner(params.bedfile, params.n_snp, params.n_org, params.ld_wind, params.maf, params.std_thr,
+                          params.rsq_thr, pos, flags=params.flags, device=local)
+    full = D.calculate_sharded(run, pos, params.ld_wind, params.n_snp, device=torch.device(f"cuda:{local}"))
+    return None if full is None else _Result(full)
+
+
 @elapsed_time
 def estimate_lds(bfile: str, ld_wind: float, wind_metric: str, maf_thr: float = 1e-5, std_thr: float = 1e-5,
                  rsq_thr: float | None = None, *, out: str | None = None, extra: bool = False, summary: bool = False,
@@ -78,7 +114,13 @@ def estimate_lds(bfile: str, ld_wind: float, wind_metric: str, maf_thr: float = 
     if device is not None:
         params.device = int(device)
     log.info("Running the estimator. It may take a long time.")
-    ld = lds.calculate(params)
+    dist = _process_group()
+    if dist is None:
+        ld = lds.calculate(params)
+    else:  # torchrun: position-sharded over the ranks' GPUs, tables gathered on rank 0
+        ld = _calculate_sharded(dist, params)
+        if ld is None:
+            return None
     log.info("Estimation completed")
 
     if summary:

@@ -1,0 +1,105 @@
+"""The host layer (nldsc_amd.ldscore.common / routine, CLI) against vectors produced by the
+reference's own Python (tests/golden/reference_python.json, tests/golden/make_golden.py): the
+LDScoreParams it hands to `calculate`, the TSV it writes, and its validation errors."""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import types
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, REPO
+
+REF = json.load(open(os.path.join(GOLDEN, "reference_python.json")))
+
+
+class _Recorder:
+    def __init__(self, result):
+        from nldsc_amd.ldscore import _ldscore
+        self.real = _ldscore
+        self.result = result
+        self.params = None
+        self.LDScoreParams = _ldscore.LDScoreParams
+        self.LDScoreResult = _ldscore.LDScoreResult
+
+    def calculate(self, params):
+        self.params = params
+        r = self.real.LDScoreResult()
+        for k, v in self.result.items():
+            setattr(r, k, v.tolist())
+        return r
+
+
+@pytest.mark.parametrize("sc", REF["scenarios"], ids=[s["set"] for s in REF["scenarios"]])
+def test_estimate_lds_matches_reference_python(sc, tmp_path, monkeypatch):
+    from nldsc_amd.ldscore import routine
+    name = sc["set"]
+    orc = dict(np.load(os.path.join(GOLDEN, name + ".oracle.npz")))
+    rec = _Recorder(orc)
+    monkeypatch.setattr(routine, "lds", rec)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    out = tmp_path / (name + ".L2")
+    a = sc["args"]
+    routine.estimate_lds(os.path.join(GOLDEN, name), ld_wind=a["ld_wind"], wind_metric=a["wind_metric"],
+                         maf_thr=a["maf_thr"], std_thr=a["std_thr"], rsq_thr=a["rsq_thr"], out=str(out),
+                         extra=a["extra"], summary=False)
+    p, e = rec.params, sc["params"]
+    assert os.path.basename(p.bedfile) == e["bfile_basename"]
+    assert (p.n_snp, p.n_org) == (e["n_snp"], e["n_org"])
+    assert (p.ld_wind, p.maf, p.std_thr, p.rsq_thr) == (e["ld_wind"], e["maf"], e["std_thr"], e["rsq_thr"])
+    pos = np.asarray(p.positions, dtype=np.float64)
+    assert len(pos) == e["positions_len"]
+    assert hashlib.sha256(pos.tobytes()).hexdigest() == e["positions_sha256"]
+    text = out.read_text()
+    assert text == open(os.path.join(GOLDEN, sc["tsv_file"])).read()
+    assert hashlib.sha256(text.encode()).hexdigest() == sc["tsv_sha256"]
+
+
+@pytest.mark.parametrize("case", REF["errors"], ids=[f"{c['cls']}{c['args']}" for c in REF["errors"]])
+def test_validation_errors_match_reference(case):
+    from nldsc_amd.ldscore import common
+    cls = getattr(common, case["cls"])
+    if case["error"] is None:
+        cls(*case["args"])
+        return
+    with pytest.raises(Exception) as ei:
+        cls(*case["args"])
+    assert type(ei.value).__name__ == case["error"]
+    assert str(ei.value) == case["message"]
+
+
+def test_bim_single_chromosome(tmp_path):
+    from nldsc_amd.ldscore.common import BIMFile, NLDSCParameterError
+    f = tmp_path / "x.bim"
+    f.write_text("1\trs1\t0.1\t100\tA\tG\n2\trs2\t0.2\t200\tA\tG\n")
+    with pytest.raises(NLDSCParameterError, match="one chromosome"):
+        BIMFile(str(f))
+
+
+def test_parse_accepts_any_of_the_three_files():
+    from nldsc_amd.ldscore.common import PLINKFile
+    for ext in ("", ".bed", ".bim", ".fam"):
+        bed, bim, fam = PLINKFile.parse(os.path.join(GOLDEN, "n1000" + ext))
+        assert bed.data.endswith("n1000.bed") and bim.n_snp == 1200 and fam.n_org == 1000
+
+
+def test_m_file_values(tmp_path):
+    from nldsc_amd.ldscore import routine
+    from nldsc_amd.ldscore.common import BIMFile
+    orc = dict(np.load(os.path.join(GOLDEN, "n1000.oracle.npz")))
+    ld = types.SimpleNamespace(**{k: v.tolist() for k, v in orc.items()})
+    m, md = routine.m_values(BIMFile(os.path.join(GOLDEN, "n1000.bim")), ld)
+    import pandas as pd
+    ref = pd.read_csv(os.path.join(GOLDEN, "n1000.ref.L2"), sep="\t")
+    sc = ref.sort_values(by=["CHR", "BP"]).dropna().drop_duplicates(subset="SNP")
+    assert m == len(sc) and md == int(len(sc) * (sc["WSDE"] / sc["WSA"]).mean())
+
+
+def test_cli_requires_exactly_one_window():
+    r = subprocess.run([sys.executable, "-m", "nldsc_amd", "ld", "--bfile", os.path.join(GOLDEN, "n1000"),
+                        "-maf", "0.01"], cwd=REPO, capture_output=True, text=True, timeout=120)
+    assert "Please, specify exactly one --ld-wind option" in r.stderr
+    assert "The program crashed with RuntimeError" in r.stderr
