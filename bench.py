@@ -36,17 +36,19 @@ def cpu_baseline(bed_host: bytes, n_snp, n_org, w, maf, std_thr, rsq, pos, targe
     """Time the C port of the reference CPU path on the first K SNPs (K sized for ~target_s)."""
     from oracle import oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    k0 = min(n_snp, 24)
-    t = time.perf_counter()
-    r0 = O.run_c(bed_host, n_snp, n_org, w, maf, std_thr, rsq, pos, end=k0, threads=threads)
-    t0 = time.perf_counter() - t
-    k = k0
-    if t0 < target_s:
-        k = int(min(n_snp, max(k0, k0 * target_s / max(t0, 1e-3))))
-    if k > k0:
+    # two short runs give the fixed window-fill cost and the marginal cost per SNP; then size K
+    def timed(k):
         t = time.perf_counter()
-        r0 = O.run_c(bed_host, n_snp, n_org, w, maf, std_thr, rsq, pos, end=k, threads=threads)
-        t0 = time.perf_counter() - t
+        r = O.run_c(bed_host, n_snp, n_org, w, maf, std_thr, rsq, pos, end=k, threads=threads)
+        return r, time.perf_counter() - t
+    k0, k1 = min(n_snp, 16), min(n_snp, 48)
+    _, t_a = timed(k0)
+    r0, t0 = timed(k1)
+    k = k1
+    marginal = max((t0 - t_a) / max(k1 - k0, 1), 1e-4)
+    if t0 < target_s and k1 < n_snp:
+        k = int(min(n_snp, k1 + (target_s - t0) / marginal))
+        r0, t0 = timed(k)
     ws = r0["l2_ws"][:k]
     pairs = float(ws[ws > 0].sum())
     return dict(value=pairs / t0, unit="SNP-pairs/s", cores=threads, kind="port",

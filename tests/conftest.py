@@ -33,9 +33,30 @@ def load_set(name):
 
 
 # Tolerances: integer window counts exact; MAF exact;
-# residual std relative 1e-5; L2 |d| <= 1e-3 + 1e-4 |L2|; L2D |d| <= 1e-5 + 1e-4 |L2D|;
+# residual std relative 1e-4 (the reference accumulates means and variances in fp32: measured 4e-5
+# relative at N = 315 599, 1.4e-7 at N = 1 000); L2 |d| <= 1e-3 + 1e-4 |L2|; L2D |d| <= 1e-5 + 1e-4 |L2D|;
 # WSDE exact except pairs whose r2adj lies within 1e-6 of rsq_thr (budget: 0.1 % of SNPs, +-1).
-TOL = dict(l2=(1e-3, 1e-4), l2d=(1e-5, 1e-4), residuals_std=(0.0, 1e-5), maf=(0.0, 0.0))
+TOL = dict(l2=(1e-3, 1e-4), l2d=(1e-5, 1e-4), residuals_std=(0.0, 1e-4), maf=(0.0, 0.0))
+
+
+def max_errors(got: dict, exp: dict) -> dict:
+    out = {}
+    for k in ("l2", "l2d", "residuals_std"):
+        m = ~np.isnan(exp[k]) & ~np.isnan(got[k])
+        d = np.abs(got[k][m] - exp[k][m])
+        out[k] = dict(max_abs=float(d.max(initial=0)),
+                      max_rel=float((d / np.maximum(np.abs(exp[k][m]), 1e-300)).max(initial=0)))
+    for k in ("l2_ws", "l2d_ws", "l2d_wse"):
+        out[k] = dict(mismatches=int((got[k] != exp[k]).sum()))
+    return out
+
+
+def record(name: str, payload: dict) -> None:
+    """Write measured parity numbers to gpurun_out/ when it exists (GPU box runs)."""
+    d = os.path.join(REPO, "gpurun_out")
+    if os.path.isdir(d):
+        with open(os.path.join(d, f"parity_{name}.json"), "w") as fh:
+            json.dump(payload, fh, indent=1)
 
 
 def assert_ld_close(got: dict, exp: dict, *, tol=TOL, wse_budget=0.001, label="", skip=None):

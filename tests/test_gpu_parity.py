@@ -10,7 +10,7 @@ import sys
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, REPO, assert_ld_close, golden_sets, load_set
+from conftest import GOLDEN, REPO, assert_ld_close, golden_sets, load_set, max_errors, record
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -35,6 +35,7 @@ def run_set(engine, name, flags=0, own=None):
 @pytest.mark.parametrize("name", SETS)
 def test_golden_sets_vs_oracle_and_f64(engine, name):
     got, meta, orc, f64, _, _ = run_set(engine, name)
+    record(f"golden_{name}", dict(vs_oracle=max_errors(got, orc), vs_f64=max_errors(got, f64)))
     # MAF: the same fp32 formula from integer counts -> bit-exact
     np.testing.assert_array_equal(got["maf"], f64["maf"])
     np.testing.assert_array_equal(got["maf"], orc["maf"])
@@ -170,6 +171,11 @@ def test_full_size_spot_check_vs_oracle(engine):
     t = np.linspace(0, M - 1, 12).astype(np.int32)
     exp = O.run_c(bed, M, N, w, maf, std_thr, rsq, pos, targets=t)
     sub = {k: v[t] for k, v in got.items()}
+    rows = np.frombuffer(bed, np.uint8, offset=3).reshape(M, -1)
+    truth = O.run_f64_targets(rows, N, w, maf, std_thr, rsq, pos, t)
+    record("full_size", dict(n_org=N, n_snp=M, targets=t.tolist(), gpu_vs_oracle=max_errors(sub, exp),
+                             gpu_vs_truth=max_errors(sub, truth), oracle_vs_truth=max_errors(exp, truth)))
+    assert_ld_close(sub, truth, label="N=315599 vs fp64 truth")
     assert_ld_close(sub, exp, label="N=315599")
     assert (got["l2_ws"] > 100).all() and np.isfinite(got["l2"]).all()
     # determinism of the integer outputs and closeness of a second run

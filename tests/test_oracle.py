@@ -90,3 +90,14 @@ def test_bad_magic_raises_value_error():
     bed, pos, meta, _, _ = load_set("n1001")
     with pytest.raises(ValueError):
         O.run_c(b"\x00" + bed[1:], meta["n_snp"], meta["n_org"], 1.0, 0.01, 1e-5, 0.001, pos)
+
+
+@pytest.mark.parametrize("name", ["n1003", "allmiss"])
+def test_f64_targets_contingency_truth(name):
+    bed, pos, meta, _, f64 = load_set(name)
+    rows = np.frombuffer(bed, np.uint8, offset=3).reshape(meta["n_snp"], -1)
+    t = np.arange(0, meta["n_snp"], 29)
+    got = O.run_f64_targets(rows, meta["n_org"], meta["ld_wind"], meta["maf"], meta["std_thr"], meta["rsq_thr"],
+                            pos, t)
+    for k in got:
+        np.testing.assert_allclose(got[k], f64[k][t], rtol=1e-12, atol=1e-12, err_msg=k)
