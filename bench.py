@@ -167,6 +167,8 @@ def main():
                 "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
                 "kernel": "band_kernel<true> (v_mfma_f32_32x32x2_f32)",
                 "flop_alg_per_launch": flop, "avg_launch_ms": band_ms,
+                "flop_issued_per_launch": tims[-1]["flop_issued"], "work_items": tims[-1]["band_items"],
+                "mfma_pipe_frac": tims[-1]["flop_issued"] / (band_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
             },
             "stages_ms": stages,
             "cpu_baseline": None,

@@ -98,9 +98,11 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
 /* Per-stage device timings (milliseconds, HIP events on the engine stream) of the last run:
  * [0] repack+count, [1] per-SNP statistics, [2] window replay + schedule (host, incl. sync),
  * [3] band correlation kernel (all launches), [4] finalize, [5] total.
- * Also: algorithmic FLOPs and SNP pairs of the last run, and kernel launch count. */
-int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, double* pairs,
-                         int32_t* n_band_launches);
+ * Also: algorithmic FLOPs (2N(1/2 sum WSA + sum WSD)), FLOPs issued to the matrix cores by the
+ * band kernel (all 32x32 blocks of the schedule, padded sample slots included), SNP pairs
+ * (sum WSA) of the last run, and the band kernel's work-item count. */
+int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, double* flop_issued,
+                         double* pairs, int32_t* n_band_items);
 
 /* Deterministic synthetic PLINK .bed on the device (benchmarks / full-size tests):
  * writes the complete file image (magic + rows) to `bed_dev` (len >= 3 + n_snp*ceil(n_org/4)).

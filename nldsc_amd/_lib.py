@@ -74,7 +74,8 @@ def lib() -> ctypes.CDLL:
         L.nldsc_engine_run.argtypes = [vp, ctypes.POINTER(Params), ctypes.c_int32, ctypes.c_int32,
                                        ctypes.POINTER(Result)] + c_err
         L.nldsc_engine_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
-                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)]
+                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_int32)]
         L.nldsc_synth_bed_device.argtypes = [ctypes.c_int32, vp, ctypes.c_int32, ctypes.c_int32,
                                              ctypes.POINTER(ctypes.c_float), ctypes.c_float, ctypes.c_float,
                                              ctypes.c_uint64] + c_err

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -92,8 +93,10 @@ struct nldsc_engine {
     std::vector<int4> h_items;
     // timings of the last run
     double ms[6] = {0, 0, 0, 0, 0, 0};
-    double flop_alg = 0, pairs = 0;
-    int32_t n_band_launches = 0;
+    double flop_alg = 0, flop_issued = 0, pairs = 0;
+    int32_t n_band_items = 0;
+    // tuning knobs (environment, read at engine creation): band kernel waves/SIMD, max column blocks
+    int band_wps = 2, band_nc = 2;
 
     ~nldsc_engine() {
         (void)hipSetDevice(device);
@@ -184,6 +187,8 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     nldsc_engine* e = new (std::nothrow) nldsc_engine();
     if (!e) return set_err(err, errlen, NLDSC_E_OOM, "out of host memory");
     e->device = d;
+    if (const char* v = std::getenv("NLDSC_BAND_WPS")) e->band_wps = std::atoi(v) == 1 ? 1 : 2;
+    if (const char* v = std::getenv("NLDSC_BAND_NC")) e->band_nc = std::atoi(v) == 1 ? 1 : 2;
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     for (auto& ev : e->ev)
         if (he == hipSuccess) he = hipEventCreate(&ev);
@@ -391,7 +396,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         while (J <= Jmax) {
             auto useful = [&](int JJ) { return blk_pass[JJ] && (blk_own[I] || blk_own[JJ]); };
             if (!useful(J)) { ++J; continue; }
-            if (J + 1 <= Jmax && useful(J + 1)) {
+            if (e->band_nc == 2 && J + 1 <= Jmax && useful(J + 1)) {
                 items2.push_back(make_int4(I, J, 2, 0));
                 J += 2;
             } else {
@@ -421,12 +426,16 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     auto t_host1 = std::chrono::steady_clock::now();
 
     HIPCHK(hipEventRecord(e->ev[3], st));
-    e->n_band_launches = 0;
+    e->n_band_items = (int32_t)e->h_items.size();
+    {
+        double blocks = 0;
+        for (const int4& it : e->h_items) blocks += it.z;
+        e->flop_issued = blocks * (dom ? 3.0 : 1.0) * 2.0 * BLK * BLK * (double)row_bytes * 4.0;
+    }
     if (!e->h_items.empty()) {
-        HIPCHK(nldsc::launch_band(dom, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, e->lut.p, e->items.p,
+        HIPCHK(nldsc::launch_band(dom, e->band_wps, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, e->lut.p, e->items.p,
                                   e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr,
                                   own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, st));
-        ++e->n_band_launches;
     }
     HIPCHK(hipEventRecord(e->ev[4], st));
     HIPCHK(nldsc::launch_finalize(e->Lw.p, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, own_begin, own_end, dom,
@@ -465,13 +474,14 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     return NLDSC_OK;
 }
 
-int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, double* pairs,
-                         int32_t* n_band_launches) {
+int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, double* flop_issued,
+                         double* pairs, int32_t* n_band_items) {
     if (!e) return NLDSC_E_ARG;
     if (ms6) for (int k = 0; k < 6; ++k) ms6[k] = e->ms[k];
     if (flop_alg) *flop_alg = e->flop_alg;
+    if (flop_issued) *flop_issued = e->flop_issued;
     if (pairs) *pairs = e->pairs;
-    if (n_band_launches) *n_band_launches = e->n_band_launches;
+    if (n_band_items) *n_band_items = e->n_band_items;
     return NLDSC_OK;
 }
 

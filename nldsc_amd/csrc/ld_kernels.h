@@ -10,7 +10,7 @@ hipError_t launch_repack_count(const uint8_t* rows, uint32_t* geno, int n_snp, i
 hipError_t launch_snp_stats(const int* counts, const double* pos, int n_snp, int n_snp_pad, int n_org, double maf_thr,
                             double std_thr, float2* lut, uint8_t* sflags, double* maf_out, double* rstd_out,
                             hipStream_t st);
-hipError_t launch_band(bool dom, int n_items, const uint32_t* geno, int pitch_words, int n_it,
+hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                        const float2* lut, const int4* items, const double* pos, const int* Lw, const int* Rw,
                        const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                        int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, hipStream_t st);

@@ -336,8 +336,10 @@ __device__ __forceinline__ void band_body(BandLds& sh, const int4 it, const uint
 }
 
 // One launch for all work items; `nc` (1 or 2 column blocks) is wave-uniform per item.
-template <bool DOM>
-__global__ void __launch_bounds__(64) band_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
+// WPS = minimum waves per SIMD the register allocation must allow (1: up to 512 VGPR+AGPR,
+// 2: <= 256).
+template <bool DOM, int WPS>
+__global__ void __launch_bounds__(64, WPS) band_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
                                                   const float2* __restrict__ lut, const int4* __restrict__ items,
                                                   const double* __restrict__ pos, const int* __restrict__ Lw,
                                                   const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
@@ -455,19 +457,17 @@ hipError_t launch_snp_stats(const int* counts, const double* pos, int n_snp, int
     return hipGetLastError();
 }
 
-hipError_t launch_band(bool dom, int n_items, const uint32_t* geno, int pitch_words, int n_it, const float2* lut,
-                       const int4* items, const double* pos, const int* Lw, const int* Rw, const uint8_t* sflags,
-                       int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo, int own_hi,
-                       double* l2_acc, double* l2d_acc, int* ws_acc, hipStream_t st) {
+hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int pitch_words, int n_it,
+                       const float2* lut, const int4* items, const double* pos, const int* Lw, const int* Rw,
+                       const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
+                       int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, hipStream_t st) {
     if (n_items <= 0) return hipSuccess;
-    if (dom)
-        hipLaunchKernelGGL((band_kernel<true>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, lut, items,
-                           pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc,
-                           ws_acc);
-    else
-        hipLaunchKernelGGL((band_kernel<false>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, lut, items,
-                           pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc,
-                           ws_acc);
+#define NLDSC_BAND(DOM_, WPS_)                                                                                       \
+    hipLaunchKernelGGL((band_kernel<DOM_, WPS_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, lut, items, \
+                       pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc)
+    if (dom) { if (wps == 2) NLDSC_BAND(true, 2); else NLDSC_BAND(true, 1); }
+    else { if (wps == 2) NLDSC_BAND(false, 2); else NLDSC_BAND(false, 1); }
+#undef NLDSC_BAND
     return hipGetLastError();
 }
 

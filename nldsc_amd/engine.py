@@ -82,12 +82,13 @@ class Engine:
 
     def timings(self) -> dict:
         ms = (ctypes.c_double * 6)()
-        flop, pairs = ctypes.c_double(), ctypes.c_double()
+        flop, issued, pairs = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
         nl = ctypes.c_int32()
-        _lib.lib().nldsc_engine_timings(self._h, ms, ctypes.byref(flop), ctypes.byref(pairs), ctypes.byref(nl))
+        _lib.lib().nldsc_engine_timings(self._h, ms, ctypes.byref(flop), ctypes.byref(issued), ctypes.byref(pairs),
+                                        ctypes.byref(nl))
         keys = ("repack_ms", "stats_ms", "schedule_ms", "band_ms", "finalize_ms", "total_ms")
         d = {k: ms[i] for i, k in enumerate(keys)}
-        d.update(flop_alg=flop.value, pairs=pairs.value, band_launches=nl.value)
+        d.update(flop_alg=flop.value, flop_issued=issued.value, pairs=pairs.value, band_items=nl.value)
         return d
 
 

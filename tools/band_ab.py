@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of band-kernel variants in ONE process on the C3 workload (cdna_hip_programming.md
+§5.4 rule 24).  Variants are engine knobs read at engine creation (NLDSC_BAND_WPS, NLDSC_BAND_NC).
+
+    python tools/band_ab.py [--rounds 3] [--n-snp 20000] [--variants wps1:nc2,wps2:nc2,wps2:nc1]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--n-org", type=int, default=315_599)
+    ap.add_argument("--n-snp", type=int, default=20_000)
+    ap.add_argument("--length-cm", type=float, default=70.0)
+    ap.add_argument("--variants", default="wps1:nc2,wps2:nc2,wps2:nc1,wps1:nc1")
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    import torch
+
+    from nldsc_amd import synth
+    from nldsc_amd.engine import Engine
+    N, M = args.n_org, args.n_snp
+    buf, pos = synth.device_bed(M, N, seed=7, length_cm=args.length_cm)
+    engines = {}
+    for v in args.variants.split(","):
+        wps = v.split(":")[0][3:]
+        nc = v.split(":")[1][2:]
+        os.environ["NLDSC_BAND_WPS"] = wps
+        os.environ["NLDSC_BAND_NC"] = nc
+        e = Engine(0)
+        e.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
+        engines[v] = e
+    del buf
+    torch.cuda.empty_cache()
+    res = {v: [] for v in engines}
+    outs = {}
+    for r in range(args.rounds + 1):
+        for v, e in engines.items():
+            o = e.run(1.0, 1e-4, 1e-5, 1.0 / M, pos)
+            t = e.timings()
+            if r > 0:
+                res[v].append(t)
+            outs[v] = o
+    ref = next(iter(outs.values()))
+    summary = {}
+    for v, ts in res.items():
+        band = [t["band_ms"] for t in ts]
+        fa, fi = ts[-1]["flop_alg"], ts[-1]["flop_issued"]
+        med = float(np.median(band))
+        summary[v] = dict(band_ms_median=med, band_ms_min=float(min(band)), alg_tflops=fa / med / 1e9,
+                          issued_tflops=fi / med / 1e9, items=ts[-1]["band_items"],
+                          alg_over_issued=fa / fi,
+                          max_abs_l2_vs_first=float(np.nanmax(np.abs(outs[v]["l2"] - ref["l2"]))),
+                          ws_equal=bool(np.array_equal(outs[v]["l2_ws"], ref["l2_ws"])))
+    print(json.dumps(summary, indent=1))
+    if args.out:
+        with open(args.out, "w") as fh:
+            json.dump(dict(config=vars(args), summary=summary), fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
