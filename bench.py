@@ -26,6 +26,7 @@ sys.path.insert(0, REPO)
 
 METRIC = "SNP-pairs/sec + wall-clock, chr1 N=315k 1cM window, 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+I8_MFMA_PEAK_TOPS = 5000.0     # MI355X_MICROARCH.md: int8 MFMA = 2x the 2.5 PF dense bf16 rate
 
 
 def log(*a):
@@ -69,6 +70,8 @@ def main():
     ap.add_argument("--maf", type=float, default=1e-4)
     ap.add_argument("--std-thr", type=float, default=1e-5)
     ap.add_argument("--additive-only", action="store_true")
+    ap.add_argument("--path", choices=("i8", "f32"), default="i8",
+                    help="correlation path: exact int8 Gram (default) or fp32 standardised values")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -87,7 +90,8 @@ def main():
     from nldsc_amd.engine import Engine
 
     N, M = args.n_org, args.n_snp
-    flags = _lib.FLAG_ADDITIVE_ONLY if args.additive_only else 0
+    flags = (_lib.FLAG_ADDITIVE_ONLY if args.additive_only else 0) | \
+        (_lib.FLAG_EXACT_I8 if args.path == "i8" else _lib.FLAG_FP32)
     t = time.perf_counter()
     buf, pos = synth.device_bed(M, N, seed=7 + rank, length_cm=args.length_cm, device=local)
     eng = Engine(local)
@@ -136,7 +140,26 @@ def main():
     if rank == 0:
         band_ms = float(np.mean([x["band_ms"] for x in tims]))
         flop = tims[-1]["flop_alg"]
-        achieved = flop / (band_ms * 1e-3) / 1e12
+        fp32_equiv = flop / (band_ms * 1e-3) / 1e12
+        exact = tims[-1]["exact_i8"]
+        if exact:
+            ops = tims[-1]["ops_alg_i8"]
+            roof = {"bound": "mfma", "achieved": ops / (band_ms * 1e-3) / 1e12, "peak": I8_MFMA_PEAK_TOPS,
+                    "unit": "TOP/s", "kernel": "band_i8_kernel<true> (v_mfma_i32_32x32x32_i8, exact int32 Gram)",
+                    "ops_alg_per_launch": ops,
+                    "ops_alg_definition": "2N(4*(1/2)sumWSA + 2*sumWSD): 4 integer dots per unordered additive "
+                                          "pair (xx,xo,ox,oo), 2 per ordered dominance pair (xh,oh)"}
+            peak = I8_MFMA_PEAK_TOPS
+        else:
+            roof = {"bound": "mfma", "achieved": fp32_equiv, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "kernel": "band_kernel<true> (v_mfma_f32_32x32x2_f32)", "flop_alg_per_launch": flop}
+            peak = FP32_MFMA_PEAK_TFLOPS
+        roof.update(frac=roof["achieved"] / peak, traffic=None, avg_launch_ms=band_ms,
+                    issued_per_launch=tims[-1]["flop_issued"], work_items=tims[-1]["band_items"],
+                    mfma_pipe_frac=tims[-1]["flop_issued"] / (band_ms * 1e-3) / 1e12 / peak,
+                    fp32_formulation_flop_per_launch=flop, fp32_equivalent_tflops=fp32_equiv,
+                    fp32_equivalent_frac_of_fp32_peak=fp32_equiv / FP32_MFMA_PEAK_TFLOPS)
+        achieved = roof["achieved"]
         stages = {k: round(float(np.mean([x[k] for x in tims])), 3)
                   for k in ("repack_ms", "stats_ms", "schedule_ms", "band_ms", "finalize_ms", "total_ms")}
         ws = out["l2_ws"]
@@ -151,7 +174,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "i8" if exact else "f32",
             "data": "synthetic (GPU-generated PLINK .bed, AR(1) haplotypes, 1% missing; one chromosome per GPU)",
             "config": {
                 "workload": ("C3 (BASELINE.json configs[2]): chr1-like N=315599 individuals, M=%d SNPs over %.0f cM, "
@@ -162,14 +185,7 @@ def main():
                 "pairs_per_step_per_gpu": tims[-1]["pairs"],
                 "parallelism": f"position sharding, one chromosome unit per GPU x {world}",
             },
-            "roofline": {
-                "bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
-                "kernel": "band_kernel<true> (v_mfma_f32_32x32x2_f32)",
-                "flop_alg_per_launch": flop, "avg_launch_ms": band_ms,
-                "flop_issued_per_launch": tims[-1]["flop_issued"], "work_items": tims[-1]["band_items"],
-                "mfma_pipe_frac": tims[-1]["flop_issued"] / (band_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
-            },
+            "roofline": roof,
             "stages_ms": stages,
             "cpu_baseline": None,
         }

@@ -41,6 +41,9 @@ extern "C" {
 #define NLDSC_FLAG_STRICT_PLINK_ORDER 1u /* use PLINK sample order in the last .bed byte (reference
                                             keeps the high n_org%4 bit pairs, stream.h:55-66) */
 #define NLDSC_FLAG_ADDITIVE_ONLY 2u      /* skip the dominance terms: l2d = NaN, l2d_ws = l2d_wse = -1 */
+#define NLDSC_FLAG_EXACT_I8 4u           /* correlations from exact integer Gram products (int8 MFMA) */
+#define NLDSC_FLAG_FP32 8u               /* correlations from fp32 standardised values (fp32 MFMA) */
+/* Neither EXACT_I8 nor FP32: the engine default, EXACT_I8 ($NLDSC_BAND_MODE = i8 | f32 overrides it). */
 
 typedef struct nldsc_ld_params {
     const char* bedfile;      /* LDScoreParams::bedfile   (data.h:34) */
@@ -103,6 +106,9 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
  * (sum WSA) of the last run, and the band kernel's work-item count. */
 int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, double* flop_issued,
                          double* pairs, int32_t* n_band_items);
+/* Path of the last run: 1 = exact int8 Gram, 0 = fp32; *ops_alg_i8 = algorithmic int8 ops of the exact
+ * formulation, 2N (2 sum WSA + 2 sum WSD). */
+int nldsc_engine_path(const nldsc_engine* e, int32_t* exact_i8, double* ops_alg_i8);
 
 /* Deterministic synthetic PLINK .bed on the device (benchmarks / full-size tests):
  * writes the complete file image (magic + rows) to `bed_dev` (len >= 3 + n_snp*ceil(n_org/4)).

@@ -18,13 +18,15 @@ OK = 0
 E_BAD_MAGIC, E_IO, E_SIZE, E_ARG, E_HIP, E_OOM, E_NODEV = -1, -2, -3, -4, -5, -6, -7
 FLAG_STRICT_PLINK_ORDER = 1
 FLAG_ADDITIVE_ONLY = 2
+FLAG_EXACT_I8 = 4
+FLAG_FP32 = 8
 
 # every symbol include/nldsc_ld.h declares (tests check the library exports all of them)
 EXPORTED = (
     "nldsc_ld_calculate", "nldsc_version", "nldsc_device_count", "nldsc_engine_create",
     "nldsc_engine_destroy", "nldsc_engine_load_bed_file", "nldsc_engine_load_bed_host",
     "nldsc_engine_load_bed_device", "nldsc_engine_run", "nldsc_engine_timings",
-    "nldsc_synth_bed_device",
+    "nldsc_synth_bed_device", "nldsc_engine_path",
 )
 
 
@@ -48,16 +50,18 @@ class NLDSCError(RuntimeError):
         self.code = code
 
 
-_lib = None
+_libs: dict = {}
 
 
-def lib() -> ctypes.CDLL:
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+def lib(path: str | None = None) -> ctypes.CDLL:
+    """The engine library (default: the in-tree build; `path` loads another build of the same ABI,
+    e.g. for interleaved A/B timing of kernel variants in one process)."""
+    path = path or LIB_PATH
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise ImportError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; "
                               f"g.build()'` (make -C nldsc_amd/csrc). nldsc_amd has no CPU fallback.")
-        L = ctypes.CDLL(LIB_PATH)
+        L = ctypes.CDLL(path)
         c_err = [ctypes.c_char_p, ctypes.c_size_t]
         vp = ctypes.c_void_p
         L.nldsc_version.restype = ctypes.c_char_p
@@ -76,14 +80,15 @@ def lib() -> ctypes.CDLL:
         L.nldsc_engine_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_int32)]
+        L.nldsc_engine_path.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)]
         L.nldsc_synth_bed_device.argtypes = [ctypes.c_int32, vp, ctypes.c_int32, ctypes.c_int32,
                                              ctypes.POINTER(ctypes.c_float), ctypes.c_float, ctypes.c_float,
                                              ctypes.c_uint64] + c_err
         for name in EXPORTED:
             if name not in ("nldsc_version", "nldsc_device_count", "nldsc_engine_destroy"):
                 getattr(L, name).restype = ctypes.c_int
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
 def check(rc: int, err) -> None:

@@ -84,6 +84,7 @@ struct nldsc_engine {
     DevBuf<uint32_t> geno;
     DevBuf<int> counts, Lw, Rw, ws_acc, ws3;
     DevBuf<float2> lut;
+    DevBuf<nldsc::SnpConst> cst;
     DevBuf<uint8_t> sflags;
     DevBuf<double> pos, maf, rstd, l2_acc, l2d_acc, l2, l2d;
     DevBuf<int4> items;
@@ -93,15 +94,17 @@ struct nldsc_engine {
     std::vector<int4> h_items;
     // timings of the last run
     double ms[6] = {0, 0, 0, 0, 0, 0};
-    double flop_alg = 0, flop_issued = 0, pairs = 0;
+    double flop_alg = 0, flop_issued = 0, pairs = 0, ops_alg_i8 = 0;
     int32_t n_band_items = 0;
     // tuning knobs (environment, read at engine creation): band kernel waves/SIMD, max column blocks
     int band_wps = 2, band_nc = 2;
+    bool last_i8 = false;  // path of the last run
+    bool band_i8 = true;   // default correlation path: exact int8 Gram (NLDSC_BAND_MODE=i8|f32)
 
     ~nldsc_engine() {
         (void)hipSetDevice(device);
         bed.release(); geno.release(); counts.release(); Lw.release(); Rw.release(); ws_acc.release();
-        ws3.release(); lut.release(); sflags.release(); pos.release(); maf.release(); rstd.release();
+        ws3.release(); lut.release(); cst.release(); sflags.release(); pos.release(); maf.release(); rstd.release();
         l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
@@ -189,6 +192,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     e->device = d;
     if (const char* v = std::getenv("NLDSC_BAND_WPS")) e->band_wps = std::atoi(v) == 1 ? 1 : 2;
     if (const char* v = std::getenv("NLDSC_BAND_NC")) e->band_nc = std::atoi(v) == 1 ? 1 : 2;
+    if (const char* v = std::getenv("NLDSC_BAND_MODE")) e->band_i8 = std::strcmp(v, "f32") != 0;
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     for (auto& ev : e->ev)
         if (he == hipSuccess) he = hipEventCreate(&ev);
@@ -317,6 +321,8 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         return set_err(err, errlen, NLDSC_E_ARG, "owned range [%d, %d) outside [0, %d)", own_begin, own_end, M);
     const bool dom = !(p->flags & NLDSC_FLAG_ADDITIVE_ONLY);
     const bool strict = (p->flags & NLDSC_FLAG_STRICT_PLINK_ORDER) != 0;
+    const bool use_i8 = (p->flags & NLDSC_FLAG_EXACT_I8) ? true : (p->flags & NLDSC_FLAG_FP32) ? false : e->band_i8;
+    const int max_nc = use_i8 ? 1 : e->band_nc;
     HIPCHK(hipSetDevice(e->device));
     hipStream_t st = e->stream;
 
@@ -335,6 +341,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     HIPCHK(e->geno.ensure((size_t)Mpad * pitch_words));
     HIPCHK(e->counts.ensure((size_t)M * 4));
     HIPCHK(e->lut.ensure((size_t)Mpad * 4));
+    HIPCHK(e->cst.ensure((size_t)Mpad));
     HIPCHK(e->sflags.ensure((size_t)Mpad));
     HIPCHK(e->pos.ensure((size_t)M));
     HIPCHK(e->maf.ensure((size_t)M));
@@ -354,8 +361,8 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     if (Mpad > M) HIPCHK(hipMemsetAsync(e->geno.p + (size_t)M * pitch_words, 0x55, (size_t)(Mpad - M) * row_bytes, st));
     HIPCHK(nldsc::launch_repack_count(e->bed.p + 3, e->geno.p, M, nb, pitch_words, tail_keep, e->counts.p, st));
     HIPCHK(hipEventRecord(e->ev[1], st));
-    HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->sflags.p,
-                                   e->maf.p, e->rstd.p, st));
+    HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->cst.p,
+                                   e->sflags.p, e->maf.p, e->rstd.p, st));
     HIPCHK(hipEventRecord(e->ev[2], st));
 
     // ---- window replay + schedule on the host (needs the MAF-pass flags) ----
@@ -396,7 +403,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         while (J <= Jmax) {
             auto useful = [&](int JJ) { return blk_pass[JJ] && (blk_own[I] || blk_own[JJ]); };
             if (!useful(J)) { ++J; continue; }
-            if (e->band_nc == 2 && J + 1 <= Jmax && useful(J + 1)) {
+            if (max_nc == 2 && J + 1 <= Jmax && useful(J + 1)) {
                 items2.push_back(make_int4(I, J, 2, 0));
                 J += 2;
             } else {
@@ -428,15 +435,29 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     HIPCHK(hipEventRecord(e->ev[3], st));
     e->n_band_items = (int32_t)e->h_items.size();
     {
-        double blocks = 0;
-        for (const int4& it : e->h_items) blocks += it.z;
-        e->flop_issued = blocks * (dom ? 3.0 : 1.0) * 2.0 * BLK * BLK * (double)row_bytes * 4.0;
+        double products = 0;  // 32x32 block products issued per sample slot
+        for (const int4& it : e->h_items) {
+            const bool dg = it.x == it.y;
+            if (use_i8)  // int8 Gram: xx, xo, ox, oo (+ xh, oh, and hx, ho off the diagonal)
+                products += dom ? (dg ? 6.0 : 8.0) : 4.0;
+            else         // fp32: AA (+ AR, and RA off the diagonal)
+                products += it.z * (dom ? 3.0 : 1.0) - ((dom && dg) ? 1.0 : 0.0);
+        }
+        e->flop_issued = products * 2.0 * BLK * BLK * (double)row_bytes * 4.0;
     }
     if (!e->h_items.empty()) {
-        HIPCHK(nldsc::launch_band(dom, e->band_wps, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, e->lut.p, e->items.p,
-                                  e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr,
-                                  own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, st));
+        if (use_i8)
+            HIPCHK(nldsc::launch_band_i8(dom, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, e->cst.p,
+                                         e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
+                                         (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
+                                         e->ws_acc.p, st));
+        else
+            HIPCHK(nldsc::launch_band(dom, e->band_wps, (int)e->h_items.size(), e->geno.p, pitch_words, n_it,
+                                      e->lut.p, e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
+                                      (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
+                                      e->ws_acc.p, st));
     }
+    e->last_i8 = use_i8;
     HIPCHK(hipEventRecord(e->ev[4], st));
     HIPCHK(nldsc::launch_finalize(e->Lw.p, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, own_begin, own_end, dom,
                                   e->l2.p, e->l2d.p, e->ws3.p, st));
@@ -471,6 +492,9 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     e->pairs = sw;
     // BASELINE.md metric: FLOP_alg = 2N(1/2 sum WSA + sum WSD); additive-only 2N * 1/2 sum WSA
     e->flop_alg = 2.0 * (double)N * (0.5 * sw + sd);
+    // exact formulation: 4 integer dot products per unordered additive pair (xx, xo, ox, oo) and
+    // 2 per ordered dominance pair (xh, oh): 2N (4 * 1/2 sum WSA + 2 sum WSD) int8 ops
+    e->ops_alg_i8 = 2.0 * (double)N * (2.0 * sw + 2.0 * sd);
     return NLDSC_OK;
 }
 
@@ -482,6 +506,13 @@ int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, d
     if (flop_issued) *flop_issued = e->flop_issued;
     if (pairs) *pairs = e->pairs;
     if (n_band_items) *n_band_items = e->n_band_items;
+    return NLDSC_OK;
+}
+
+int nldsc_engine_path(const nldsc_engine* e, int32_t* exact_i8, double* ops_alg_i8) {
+    if (!e) return NLDSC_E_ARG;
+    if (exact_i8) *exact_i8 = e->last_i8 ? 1 : 0;
+    if (ops_alg_i8) *ops_alg_i8 = e->ops_alg_i8;
     return NLDSC_OK;
 }
 

@@ -5,15 +5,26 @@
 
 namespace nldsc {
 
+// Per-SNP constants of the exact-integer path: with x = additive count, h = [genotype >= 1],
+// o = [observed] (all 0 for missing calls and padding), the reference's standardised vectors are
+// A = (x - mu o) / sa and R = (2h - beta x - c o) / s.
+struct SnpConst {
+    double mu, sa, c, beta, s;
+};
+
 hipError_t launch_repack_count(const uint8_t* rows, uint32_t* geno, int n_snp, int nb, int pitch_words,
                                uint32_t tail_keep, int* counts, hipStream_t st);
 hipError_t launch_snp_stats(const int* counts, const double* pos, int n_snp, int n_snp_pad, int n_org, double maf_thr,
-                            double std_thr, float2* lut, uint8_t* sflags, double* maf_out, double* rstd_out,
-                            hipStream_t st);
+                            double std_thr, float2* lut, SnpConst* cst, uint8_t* sflags, double* maf_out,
+                            double* rstd_out, hipStream_t st);
 hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                        const float2* lut, const int4* items, const double* pos, const int* Lw, const int* Rw,
                        const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                        int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, hipStream_t st);
+hipError_t launch_band_i8(bool dom, int n_items, const uint32_t* geno, int pitch_words, int n_it,
+                          const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
+                          const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
+                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, hipStream_t st);
 hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2d_acc, const int* ws_acc, int n_snp,
                            int own_lo, int own_hi, bool dom, double* l2, double* l2d, int* ws3, hipStream_t st);
 hipError_t launch_synth_bed(uint8_t* rows, int n_snp, int n_org, int nb, const float* thr, float rho, float missing,

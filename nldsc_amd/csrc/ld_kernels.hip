@@ -81,11 +81,12 @@ __global__ void __launch_bounds__(256) repack_count_kernel(const uint8_t* __rest
 // reads.  Missing calls are mean-imputed by the reference, so their centred value is exactly 0.
 __global__ void snp_stats_kernel(const int* __restrict__ counts, const double* __restrict__ pos, int n_snp,
                                  int n_snp_pad, int n_org, double maf_thr, double std_thr,
-                                 float2* __restrict__ lut, uint8_t* __restrict__ sflags,
+                                 float2* __restrict__ lut, SnpConst* __restrict__ cst, uint8_t* __restrict__ sflags,
                                  double* __restrict__ maf_out, double* __restrict__ rstd_out) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_snp_pad) return;
     float2 L[4] = {make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
+    SnpConst K = {0.0, 0.0, 0.0, 0.0, 0.0};
     uint8_t fl = 0;
     if (j < n_snp) {
         const double qnan = __builtin_nan("");
@@ -105,6 +106,7 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const double* _
                     // every call missing: the reference's vectors are all NaN (MAF NaN passes the
                     // filter); they poison every window containing this SNP.
                     for (int c = 0; c < 4; ++c) L[c] = make_float2(qnan, 0.f);
+                    K = SnpConst{qnan, qnan, 0.0, 0.0, 0.0};
                 } else {
                     const double abar = (c1 + 2.0 * c2) / n_obs, dbar = 2.0 * (c1 + c2) / n_obs;
                     const double da0 = -abar, da1 = 1.0 - abar, da2 = 2.0 - abar;
@@ -128,6 +130,9 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const double* _
                     L[1] = make_float2(0.f, 0.f); // code 01 missing (imputed -> centred 0)
                     L[2] = make_float2(ib, rb);   // code 10 het
                     L[3] = make_float2(ic, rc);   // code 11 hom A2
+                    // exact path: A = (x - mu o) / sa,  R = (2h - beta x - c o) / s   (x, h, o integer)
+                    K = SnpConst{abar, sd_a, rpass ? dbar - beta * abar : 0.0, rpass ? beta : 0.0,
+                                 rpass ? rstd_d : 0.0};
                 }
             }
         }
@@ -135,6 +140,7 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const double* _
         rstd_out[j] = (fl & 1) ? rstd_d : qnan;
     }
     for (int c = 0; c < 4; ++c) lut[(size_t)j * 4 + c] = L[c];
+    cst[j] = K;
     sflags[j] = fl;
 }
 
@@ -171,7 +177,9 @@ struct BandLds {
     int wsa[NS_MAX], wsd[NS_MAX], wse[NS_MAX];
 };
 
-template <int NC, bool DOM>
+// DIAG0: column block 0 is the row block itself (J0 == I).  Its R_I^T X_I product is the
+// transpose of X_I^T R_I and is never needed, so those MFMAs are skipped.
+template <int NC, bool DOM, bool DIAG0>
 __device__ __forceinline__ void band_body(BandLds& sh, const int4 it, const uint32_t* __restrict__ geno,
                                           int pitch_words, int n_it, const float2* __restrict__ lut,
                                           const double* __restrict__ pos, const int* __restrict__ Lw,
@@ -267,7 +275,8 @@ __device__ __forceinline__ void band_body(BandLds& sh, const int4 it, const uint
                     aa[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(vr.x, vc.x, aa[b], 0, 0, 0);
                     if (DOM) {
                         ar[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(vr.x, vc.y, ar[b], 0, 0, 0);
-                        ra[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(vr.y, vc.x, ra[b], 0, 0, 0);
+                        if (!(DIAG0 && b == 0))
+                            ra[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(vr.y, vc.x, ra[b], 0, 0, 0);
                     }
                 }
             }
@@ -348,12 +357,182 @@ __global__ void __launch_bounds__(64, WPS) band_kernel(const uint32_t* __restric
                                                   int* __restrict__ ws_acc) {
     __shared__ BandLds sh;
     const int4 it = items[blockIdx.x];
-    if (it.z == 2)
-        band_body<2, DOM>(sh, it, geno, pitch_words, n_it, lut, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr,
-                          own_lo, own_hi, l2_acc, l2d_acc, ws_acc);
+#define NLDSC_BODY(NC_, DIAG_)                                                                                        \
+    band_body<NC_, DOM, DIAG_>(sh, it, geno, pitch_words, n_it, lut, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,     \
+                               rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc)
+    const bool diag = it.y == it.x;
+    if (it.z == 2) { if (diag) NLDSC_BODY(2, true); else NLDSC_BODY(2, false); }
+    else { if (diag) NLDSC_BODY(1, true); else NLDSC_BODY(1, false); }
+#undef NLDSC_BODY
+}
+
+// ------------------------------------------------------------------------------------------
+// 3b. exact-integer band kernel (int8 MFMA on genotype indicators)
+// ------------------------------------------------------------------------------------------
+// Per SNP and sample slot: x = additive count {0,1,2}, h = [genotype >= 1], o = [observed]; missing
+// calls and padding slots are all-zero.  The reference's standardised vectors are affine in these
+// (SnpConst), so every dot product it needs is an fp64 combination of 8 integer Gram entries per
+// SNP pair: x.x, x.o, o.x, o.o (additive) and x.h, o.h, h.x, h.o (dominance, both directions).
+// They are computed EXACTLY with v_mfma_i32_32x32x32_i8 (int32 sums, N < 2^29) — no rounding
+// before the fp64 epilogue.  One wave per (row block I, column block J): lane i&31 = its SNP,
+// lane>>5 = which 16-sample word of each K step it decodes.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+// 16 two-bit codes of one word -> x, h, o as 16 bytes each (byte b of dword k = bit pair k of byte b;
+// any fixed slot permutation is fine since A and B operands use the same one).
+__device__ __forceinline__ void decode16(uint32_t w, i32x4& X, i32x4& H, i32x4& O) {
+    const uint32_t hiw = (w >> 1) & 0x55555555u, low = w & 0x55555555u;
+    const uint32_t xw = hiw + (hiw & low);             // 00->0, 01->0, 10->1, 11->2 (no carries)
+    const uint32_t ow = (hiw | ~low) & 0x55555555u;     // 01 (missing / padding) -> 0
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        X[k] = (int)((xw >> (2 * k)) & 0x03030303u);
+        H[k] = (int)((hiw >> (2 * k)) & 0x01010101u);
+        O[k] = (int)((ow >> (2 * k)) & 0x01010101u);
+    }
+}
+
+struct BandI8Lds {
+    SnpSlot info[64];
+    SnpConst cst[64];
+    double l2[64], l2d[64];
+    int wsa[64], wsd[64], wse[64];
+};
+
+template <bool DOM, bool DIAG>
+__device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const uint32_t* __restrict__ geno,
+                                             int pitch_words, int n_it, const SnpConst* __restrict__ cst,
+                                             const double* __restrict__ pos, const int* __restrict__ Lw,
+                                             const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
+                                             int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
+                                             int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
+                                             int* __restrict__ ws_acc) {
+    const int lane = threadIdx.x;
+    const int i = lane & 31, h = lane >> 5;
+    const int I = it.x, J = it.y;
+    for (int s = lane; s < 64; s += 64) {
+        const int g = s < 32 ? I * 32 + s : J * 32 + (s - 32);
+        SnpSlot si;
+        si.g = g;
+        if (g < n_snp) {
+            si.pos = pos[g]; si.L = Lw[g]; si.R = Rw[g]; si.fl = sflags[g];
+        } else {
+            si.pos = 0.0; si.L = -1; si.R = -2; si.fl = 0;
+        }
+        sh.info[s] = si;
+        sh.cst[s] = cst[g];
+        sh.l2[s] = 0.0; sh.l2d[s] = 0.0;
+        sh.wsa[s] = 0; sh.wsd[s] = 0; sh.wse[s] = 0;
+    }
+    __syncthreads();
+
+    // Gram accumulators: additive xx, xo, ox, oo; dominance xh, oh (row -> col), hx, ho (col -> row)
+    i32x16 gxx = {}, gxo = {}, gox = {}, goo = {}, gxh = {}, goh = {}, ghx = {}, gho = {};
+    const uint4* rowp = reinterpret_cast<const uint4*>(geno + (size_t)(I * 32 + i) * (size_t)pitch_words) + h;
+    const uint4* colp = reinterpret_cast<const uint4*>(geno + (size_t)(J * 32 + i) * (size_t)pitch_words) + h;
+    uint4 nr = rowp[0], ncl = colp[0];
+    for (int t = 0; t < n_it; ++t) {
+        const uint4 wr4 = nr, wc4 = ncl;
+        if (t + 1 < n_it) {
+            nr = rowp[2 * (t + 1)];
+            ncl = colp[2 * (t + 1)];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t wr = q == 0 ? wr4.x : q == 1 ? wr4.y : q == 2 ? wr4.z : wr4.w;
+            const uint32_t wc = q == 0 ? wc4.x : q == 1 ? wc4.y : q == 2 ? wc4.z : wc4.w;
+            i32x4 Xi, Hi, Oi, Xj, Hj, Oj;
+            decode16(wr, Xi, Hi, Oi);
+            decode16(wc, Xj, Hj, Oj);
+            gxx = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Xj, gxx, 0, 0, 0);
+            gxo = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Oj, gxo, 0, 0, 0);
+            gox = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Xj, gox, 0, 0, 0);
+            goo = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Oj, goo, 0, 0, 0);
+            if (DOM) {
+                gxh = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Hj, gxh, 0, 0, 0);
+                goh = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Hj, goh, 0, 0, 0);
+                if (!DIAG) {  // on a diagonal block R_i . A_j is the transposed A_j . R_i
+                    ghx = __builtin_amdgcn_mfma_i32_32x32x32_i8(Hi, Xj, ghx, 0, 0, 0);
+                    gho = __builtin_amdgcn_mfma_i32_32x32x32_i8(Hi, Oj, gho, 0, 0, 0);
+                }
+            }
+        }
+    }
+
+    // ---- fused epilogue (fp64): standardised dots from the integer Gram, r2adj, masks, sums ----
+    const int sj = 32 + i;
+    const SnpSlot cj = sh.info[sj];
+    const SnpConst kj = sh.cst[sj];
+    const bool pj = cj.fl & 1, rpj = (cj.fl & 2) != 0;
+    const bool compj = cj.L >= 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int si = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const SnpSlot ci = sh.info[si];
+        const bool pi = ci.fl & 1, rpi = (ci.fl & 2) != 0;
+        const bool inwin = fabs(cj.pos - ci.pos) <= ld_wind && ci.g != cj.g;
+        const bool nij = inwin && ci.L >= 0 && cj.g >= ci.L && cj.g <= ci.R && pj;
+        const bool nji = !DIAG && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
+        if (nij || nji) {
+            const SnpConst ki = sh.cst[si];
+            const double xx = (double)gxx[r], xo = (double)gxo[r], ox = (double)gox[r], oo = (double)goo[r];
+            const double aa = (xx - kj.mu * xo - ki.mu * (ox - kj.mu * oo)) / (ki.sa * kj.sa);
+            const double r2 = r2_adjusted(aa, n_org);
+            if (nij) { atomicAdd(&sh.l2[si], r2); atomicAdd(&sh.wsa[si], 1); }
+            if (nji) { atomicAdd(&sh.l2[sj], r2); atomicAdd(&sh.wsa[sj], 1); }
+            if (DOM) {
+                if (nij && rpj) {  // A_i . R_j -> L2D_i (ldscalc.h:40-46)
+                    const double xh = (double)gxh[r], oh = (double)goh[r];
+                    const double ar = (2.0 * xh - kj.beta * xx - kj.c * xo -
+                                       ki.mu * (2.0 * oh - kj.beta * ox - kj.c * oo)) / (ki.sa * kj.s);
+                    const double rd = r2_adjusted(ar, n_org);
+                    atomicAdd(&sh.l2d[si], rd); atomicAdd(&sh.wsd[si], 1);
+                    if (rd > rsq_thr) atomicAdd(&sh.wse[si], 1);
+                }
+                if (!DIAG && nji && rpi) {  // R_i . A_j -> L2D_j
+                    const double hx = (double)ghx[r], ho = (double)gho[r];
+                    const double ra = (2.0 * hx - ki.beta * xx - ki.c * ox -
+                                       kj.mu * (2.0 * ho - ki.beta * xo - ki.c * oo)) / (ki.s * kj.sa);
+                    const double rd = r2_adjusted(ra, n_org);
+                    atomicAdd(&sh.l2d[sj], rd); atomicAdd(&sh.wsd[sj], 1);
+                    if (rd > rsq_thr) atomicAdd(&sh.wse[sj], 1);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int s = lane; s < 64; s += 64) {
+        const int g = sh.info[s].g;
+        if (g < own_lo || g >= own_hi || g >= n_snp) continue;
+        if (sh.wsa[s]) {
+            unsafeAtomicAdd(&l2_acc[g], sh.l2[s]);
+            atomicAdd(&ws_acc[g], sh.wsa[s]);
+        }
+        if (DOM && sh.wsd[s]) {
+            unsafeAtomicAdd(&l2d_acc[g], sh.l2d[s]);
+            atomicAdd(&ws_acc[(size_t)n_snp + g], sh.wsd[s]);
+            if (sh.wse[s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + g], sh.wse[s]);
+        }
+    }
+}
+
+template <bool DOM>
+__global__ void __launch_bounds__(64, 2) band_i8_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
+                                                        const SnpConst* __restrict__ cst, const int4* __restrict__ items,
+                                                        const double* __restrict__ pos, const int* __restrict__ Lw,
+                                                        const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
+                                                        int n_snp, double ld_wind, double n_org, double rsq_thr,
+                                                        int own_lo, int own_hi, double* __restrict__ l2_acc,
+                                                        double* __restrict__ l2d_acc, int* __restrict__ ws_acc) {
+    __shared__ BandI8Lds sh;
+    const int4 it = items[blockIdx.x];
+    if (it.y == it.x)
+        band_i8_body<DOM, true>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,
+                                rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc);
     else
-        band_body<1, DOM>(sh, it, geno, pitch_words, n_it, lut, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr,
-                          own_lo, own_hi, l2_acc, l2d_acc, ws_acc);
+        band_i8_body<DOM, false>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,
+                                 rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -449,11 +628,11 @@ hipError_t launch_repack_count(const uint8_t* rows, uint32_t* geno, int n_snp, i
 }
 
 hipError_t launch_snp_stats(const int* counts, const double* pos, int n_snp, int n_snp_pad, int n_org, double maf_thr,
-                            double std_thr, float2* lut, uint8_t* sflags, double* maf_out, double* rstd_out,
-                            hipStream_t st) {
+                            double std_thr, float2* lut, SnpConst* cst, uint8_t* sflags, double* maf_out,
+                            double* rstd_out, hipStream_t st) {
     const int blocks = (n_snp_pad + 255) / 256;
     hipLaunchKernelGGL(snp_stats_kernel, dim3(blocks), dim3(256), 0, st, counts, pos, n_snp, n_snp_pad, n_org, maf_thr,
-                       std_thr, lut, sflags, maf_out, rstd_out);
+                       std_thr, lut, cst, sflags, maf_out, rstd_out);
     return hipGetLastError();
 }
 
@@ -468,6 +647,22 @@ hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int
     if (dom) { if (wps == 2) NLDSC_BAND(true, 2); else NLDSC_BAND(true, 1); }
     else { if (wps == 2) NLDSC_BAND(false, 2); else NLDSC_BAND(false, 1); }
 #undef NLDSC_BAND
+    return hipGetLastError();
+}
+
+hipError_t launch_band_i8(bool dom, int n_items, const uint32_t* geno, int pitch_words, int n_it,
+                          const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
+                          const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
+                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, hipStream_t st) {
+    if (n_items <= 0) return hipSuccess;
+    if (dom)
+        hipLaunchKernelGGL((band_i8_kernel<true>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, cst, items,
+                           pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc,
+                           ws_acc);
+    else
+        hipLaunchKernelGGL((band_i8_kernel<false>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, cst,
+                           items, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc,
+                           l2d_acc, ws_acc);
     return hipGetLastError();
 }
 

@@ -15,8 +15,8 @@ from . import _lib
 
 
 class Engine:
-    def __init__(self, device: int = -1):
-        L = _lib.lib()
+    def __init__(self, device: int = -1, lib_path: str | None = None):
+        self._L = L = _lib.lib(lib_path)
         self._h = ctypes.c_void_p()
         err = _lib.errbuf()
         _lib.check(L.nldsc_engine_create(int(device), ctypes.byref(self._h), err, len(err)), err)
@@ -25,7 +25,7 @@ class Engine:
 
     def close(self):
         if self._h:
-            _lib.lib().nldsc_engine_destroy(self._h)
+            self._L.nldsc_engine_destroy(self._h)
             self._h = ctypes.c_void_p()
 
     def __del__(self):
@@ -43,21 +43,21 @@ class Engine:
     # ---- loading ------------------------------------------------------------------------
     def load_bed_file(self, path: str, n_snp: int, n_org: int):
         err = _lib.errbuf()
-        _lib.check(_lib.lib().nldsc_engine_load_bed_file(self._h, path.encode(), n_snp, n_org, err, len(err)), err)
+        _lib.check(self._L.nldsc_engine_load_bed_file(self._h, path.encode(), n_snp, n_org, err, len(err)), err)
         self.n_snp, self.n_org = n_snp, n_org
 
     def load_bed_bytes(self, bed, n_snp: int, n_org: int):
         """`bed`: the whole .bed content (bytes / uint8 numpy array), magic included."""
         buf = np.frombuffer(bed, dtype=np.uint8) if isinstance(bed, (bytes, bytearray)) else np.ascontiguousarray(bed, np.uint8)
         err = _lib.errbuf()
-        _lib.check(_lib.lib().nldsc_engine_load_bed_host(self._h, buf.ctypes.data, buf.nbytes, n_snp, n_org, err,
+        _lib.check(self._L.nldsc_engine_load_bed_host(self._h, buf.ctypes.data, buf.nbytes, n_snp, n_org, err,
                                                          len(err)), err)
         self.n_snp, self.n_org = n_snp, n_org
 
     def load_bed_device(self, ptr: int, nbytes: int, n_snp: int, n_org: int):
         """Copy a .bed image that already lives in this device's memory (e.g. a torch tensor)."""
         err = _lib.errbuf()
-        _lib.check(_lib.lib().nldsc_engine_load_bed_device(self._h, ctypes.c_void_p(ptr), nbytes, n_snp, n_org, err,
+        _lib.check(self._L.nldsc_engine_load_bed_device(self._h, ctypes.c_void_p(ptr), nbytes, n_snp, n_org, err,
                                                            len(err)), err)
         self.n_snp, self.n_org = n_snp, n_org
 
@@ -76,7 +76,7 @@ class Engine:
             res = _lib.Result(*(arrs[k].ctypes.data_as(d if arrs[k].dtype == np.float64 else i)
                                 for k in ("l2", "l2d", "maf", "residuals_std", "l2_ws", "l2d_ws", "l2d_wse")))
         err = _lib.errbuf()
-        _lib.check(_lib.lib().nldsc_engine_run(self._h, ctypes.byref(p), int(own[0]), int(own[1]),
+        _lib.check(self._L.nldsc_engine_run(self._h, ctypes.byref(p), int(own[0]), int(own[1]),
                                                ctypes.byref(res), err, len(err)), err)
         return arrs
 
@@ -84,11 +84,14 @@ class Engine:
         ms = (ctypes.c_double * 6)()
         flop, issued, pairs = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
         nl = ctypes.c_int32()
-        _lib.lib().nldsc_engine_timings(self._h, ms, ctypes.byref(flop), ctypes.byref(issued), ctypes.byref(pairs),
+        self._L.nldsc_engine_timings(self._h, ms, ctypes.byref(flop), ctypes.byref(issued), ctypes.byref(pairs),
                                         ctypes.byref(nl))
         keys = ("repack_ms", "stats_ms", "schedule_ms", "band_ms", "finalize_ms", "total_ms")
         d = {k: ms[i] for i, k in enumerate(keys)}
         d.update(flop_alg=flop.value, flop_issued=issued.value, pairs=pairs.value, band_items=nl.value)
+        ex, ops = ctypes.c_int32(), ctypes.c_double()
+        self._L.nldsc_engine_path(self._h, ctypes.byref(ex), ctypes.byref(ops))
+        d.update(exact_i8=bool(ex.value), ops_alg_i8=ops.value)
         return d
 
 

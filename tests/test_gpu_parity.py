@@ -32,10 +32,14 @@ def run_set(engine, name, flags=0, own=None):
     return got, meta, orc, f64, pos, bed
 
 
+MODES = {"f32": 8, "i8": 4}  # _lib.FLAG_FP32, _lib.FLAG_EXACT_I8
+
+
+@pytest.mark.parametrize("mode", sorted(MODES))
 @pytest.mark.parametrize("name", SETS)
-def test_golden_sets_vs_oracle_and_f64(engine, name):
-    got, meta, orc, f64, _, _ = run_set(engine, name)
-    record(f"golden_{name}", dict(vs_oracle=max_errors(got, orc), vs_f64=max_errors(got, f64)))
+def test_golden_sets_vs_oracle_and_f64(engine, name, mode):
+    got, meta, orc, f64, _, _ = run_set(engine, name, flags=MODES[mode])
+    record(f"golden_{name}_{mode}", dict(vs_oracle=max_errors(got, orc), vs_f64=max_errors(got, f64)))
     # MAF: the same fp32 formula from integer counts -> bit-exact
     np.testing.assert_array_equal(got["maf"], f64["maf"])
     np.testing.assert_array_equal(got["maf"], orc["maf"])
@@ -49,6 +53,12 @@ def test_golden_sets_vs_oracle_and_f64(engine, name):
     assert np.max(np.abs(got["l2d"][m] - f64["l2d"][m]), initial=0) < 5e-6
     m = ~np.isnan(f64["residuals_std"])
     np.testing.assert_allclose(got["residuals_std"][m], f64["residuals_std"][m], rtol=1e-12)
+    if mode == "i8":  # exact integer Gram + fp64 epilogue: equal to the fp64 restatement to rounding
+        for k in ("l2", "l2d"):
+            m = ~np.isnan(f64[k])
+            assert np.max(np.abs(got[k][m] - f64[k][m]), initial=0) < 1e-9, k
+        for k in ("l2_ws", "l2d_ws", "l2d_wse"):
+            np.testing.assert_array_equal(got[k], f64[k])
 
 
 @pytest.mark.parametrize("name", ["n1001", "n1003"])
@@ -135,8 +145,9 @@ def test_cli_end_to_end(tmp_path):
     assert int(m["MD"][0]) == int(len(sc) * (sc["WSDE"] / sc["WSA"]).mean())
 
 
+@pytest.mark.parametrize("mode", sorted(MODES))
 @pytest.mark.parametrize("seed", range(12))
-def test_random_small_configs_vs_f64(engine, seed):
+def test_random_small_configs_vs_f64(engine, seed, mode):
     """Ragged sizes: N from 3 (tiny K) to 700, M from 1 to 260, windows from a few SNPs to all."""
     from nldsc_amd import synth
     rng = np.random.default_rng(1000 + seed)
@@ -152,13 +163,16 @@ def test_random_small_configs_vs_f64(engine, seed):
     w = float(rng.choice([0.05, 0.5, 1.0, 100.0]))
     maf, std_thr, rsq = float(rng.choice([0.0, 0.01, 0.05])), float(rng.choice([0.0, 1e-5])), 0.5 / max(M, 11)
     engine.load_bed_bytes(synth.bed_bytes(rows), M, N)
-    got = engine.run(w, maf, std_thr, rsq, pos)
+    got = engine.run(w, maf, std_thr, rsq, pos, flags=MODES[mode])
     exp = O.run_f64(rows, N, w, maf, std_thr, rsq, pos)
     tol = dict(l2=(1e-4, 1e-5), l2d=(1e-5, 1e-5), residuals_std=(1e-12, 1e-10), maf=(0.0, 0.0))
+    if mode == "i8":
+        tol.update(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12))
     assert_ld_close(got, exp, tol=tol, wse_budget=0.02, label=f"seed{seed} N{N} M{M}")
 
 
-def test_full_size_spot_check_vs_oracle(engine):
+@pytest.mark.parametrize("mode", sorted(MODES))
+def test_full_size_spot_check_vs_oracle(engine, mode):
     """N = 315 599 (N % 4 = 3, BASELINE.json configs[2]) on a 2 000-SNP chromosome slice generated on the
     GPU: 12 SNPs against the oracle's targets mode, the rest by invariants."""
     from nldsc_amd import synth
@@ -166,20 +180,23 @@ def test_full_size_spot_check_vs_oracle(engine):
     buf, pos = synth.device_bed(M, N, seed=3, length_cm=7.0)
     engine.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
     w, maf, std_thr, rsq = 1.0, 1e-4, 1e-5, 1.0 / M
-    got = engine.run(w, maf, std_thr, rsq, pos)
+    got = engine.run(w, maf, std_thr, rsq, pos, flags=MODES[mode])
     bed = buf.cpu().numpy().tobytes()
     t = np.linspace(0, M - 1, 12).astype(np.int32)
     exp = O.run_c(bed, M, N, w, maf, std_thr, rsq, pos, targets=t)
     sub = {k: v[t] for k, v in got.items()}
     rows = np.frombuffer(bed, np.uint8, offset=3).reshape(M, -1)
     truth = O.run_f64_targets(rows, N, w, maf, std_thr, rsq, pos, t)
-    record("full_size", dict(n_org=N, n_snp=M, targets=t.tolist(), gpu_vs_oracle=max_errors(sub, exp),
+    record(f"full_size_{mode}", dict(n_org=N, n_snp=M, targets=t.tolist(), gpu_vs_oracle=max_errors(sub, exp),
                              gpu_vs_truth=max_errors(sub, truth), oracle_vs_truth=max_errors(exp, truth)))
     assert_ld_close(sub, truth, label="N=315599 vs fp64 truth")
+    if mode == "i8":
+        for k in ("l2", "l2d"):
+            assert np.max(np.abs(sub[k] - truth[k])) < 1e-8, k
     assert_ld_close(sub, exp, label="N=315599")
     assert (got["l2_ws"] > 100).all() and np.isfinite(got["l2"]).all()
     # determinism of the integer outputs and closeness of a second run
-    again = engine.run(w, maf, std_thr, rsq, pos)
+    again = engine.run(w, maf, std_thr, rsq, pos, flags=MODES[mode])
     np.testing.assert_array_equal(again["l2_ws"], got["l2_ws"])
     np.testing.assert_array_equal(again["l2d_wse"], got["l2d_wse"])
     np.testing.assert_allclose(again["l2"], got["l2"], rtol=1e-13)

@@ -2,7 +2,9 @@
 """Interleaved A/B of band-kernel variants in ONE process on the C3 workload (cdna_hip_programming.md
 §5.4 rule 24).  Variants are engine knobs read at engine creation (NLDSC_BAND_WPS, NLDSC_BAND_NC).
 
-    python tools/band_ab.py [--rounds 3] [--n-snp 20000] [--variants wps1:nc2,wps2:nc2,wps2:nc1]
+    python tools/band_ab.py [--rounds 3] [--n-snp 20000] [--variants wps1:nc2,wps2:nc2,v1=ab_libs/v1.so:wps2:nc2]
+
+A variant is `[label=][libpath:]wpsW:ncC`; `libpath` loads another build of libnldsc_amd.so (same ABI).
 """
 import argparse
 import json
@@ -32,11 +34,16 @@ def main():
     buf, pos = synth.device_bed(M, N, seed=7, length_cm=args.length_cm)
     engines = {}
     for v in args.variants.split(","):
-        wps = v.split(":")[0][3:]
-        nc = v.split(":")[1][2:]
-        os.environ["NLDSC_BAND_WPS"] = wps
-        os.environ["NLDSC_BAND_NC"] = nc
-        e = Engine(0)
+        label, spec = v.split("=", 1) if "=" in v else (v, v)
+        parts = spec.split(":")
+        lib = parts[0] if parts[0].endswith(".so") else None
+        knobs = dict((p[:3] if p.startswith("wps") else p[:2], p[3:] if p.startswith("wps") else p[2:])
+                     for p in parts if p.startswith(("wps", "nc")))
+        os.environ["NLDSC_BAND_WPS"] = knobs.get("wps", "2")
+        os.environ["NLDSC_BAND_NC"] = knobs.get("nc", "2")
+        os.environ["NLDSC_BAND_MODE"] = "i8" if "i8" in parts else "f32"
+        e = Engine(0, lib_path=lib)
+        v = label
         e.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
         engines[v] = e
     del buf
