@@ -110,6 +110,15 @@ int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, d
  * formulation, 2N (2 sum WSA + 2 sum WSD). */
 int nldsc_engine_path(const nldsc_engine* e, int32_t* exact_i8, double* ops_alg_i8);
 
+/* Host-only plan of the band kernel (no GPU needed; the engine calls the same code):
+ * replays the reference's sliding-window pointers (stream.h:131-155,182-197) from positions and
+ * MAF-pass flags (flags[j] bit 0) into L/R (n_snp each; L = -1 for SNPs the reference does not
+ * compute) and lists the work items (I, J0, nc, 0) covering every needed 32x32 block pair for the
+ * owned range.  Returns the item count; when it exceeds `cap` (or items == NULL) nothing is written
+ * to `items` and the count is returned; < 0 on bad arguments. */
+int nldsc_plan_band(const double* positions, const uint8_t* flags, int32_t n_snp, double ld_wind, int32_t own_begin,
+                    int32_t own_end, int32_t max_nc, int32_t* L, int32_t* R, int32_t* items, int32_t cap);
+
 /* Deterministic synthetic PLINK .bed on the device (benchmarks / full-size tests):
  * writes the complete file image (magic + rows) to `bed_dev` (len >= 3 + n_snp*ceil(n_org/4)).
  * Model as nldsc_amd/synth.py: latent AR(1) haplotypes, thr[j] = Phi^-1(p_j), `missing` rate. */

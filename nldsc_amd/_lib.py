@@ -26,7 +26,7 @@ EXPORTED = (
     "nldsc_ld_calculate", "nldsc_version", "nldsc_device_count", "nldsc_engine_create",
     "nldsc_engine_destroy", "nldsc_engine_load_bed_file", "nldsc_engine_load_bed_host",
     "nldsc_engine_load_bed_device", "nldsc_engine_run", "nldsc_engine_timings",
-    "nldsc_synth_bed_device", "nldsc_engine_path",
+    "nldsc_synth_bed_device", "nldsc_engine_path", "nldsc_plan_band",
 )
 
 
@@ -80,6 +80,8 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.nldsc_engine_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_int32)]
+        L.nldsc_plan_band.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.c_int32, vp, vp, vp, ctypes.c_int32]
         L.nldsc_engine_path.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)]
         L.nldsc_synth_bed_device.argtypes = [ctypes.c_int32, vp, ctypes.c_int32, ctypes.c_int32,
                                              ctypes.POINTER(ctypes.c_float), ctypes.c_float, ctypes.c_float,
@@ -123,3 +125,22 @@ def make_params(n_snp, n_org, ld_wind, maf, std_thr, rsq_thr, positions, *, bedf
                pos.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), float(maf), float(std_thr), float(rsq_thr),
                int(flags), int(device))
     return p, pos  # keep `pos` alive while p is used
+
+
+def plan_band(positions, pass_flags, ld_wind, own=None, max_nc=1):
+    """Host-only schedule (C ABI nldsc_plan_band): returns (L, R, items[k, 4])."""
+    pos = np.ascontiguousarray(positions, dtype=np.float64)
+    n = len(pos)
+    fl = np.ascontiguousarray(pass_flags, dtype=np.uint8)
+    own = (0, n) if own is None else own
+    L_ = np.empty(n, np.int32)
+    R_ = np.empty(n, np.int32)
+    args = (pos.ctypes.data, fl.ctypes.data, n, float(ld_wind), int(own[0]), int(own[1]), int(max_nc),
+            L_.ctypes.data, R_.ctypes.data)
+    k = lib().nldsc_plan_band(*args, None, 0)
+    if k < 0:
+        raise ValueError(f"nldsc_plan_band error {k}")
+    items = np.zeros((max(k, 1), 4), np.int32)
+    k2 = lib().nldsc_plan_band(*args, items.ctypes.data, len(items))
+    assert k2 == k
+    return L_, R_, items[:k]

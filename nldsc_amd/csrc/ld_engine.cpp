@@ -99,6 +99,7 @@ struct nldsc_engine {
     // tuning knobs (environment, read at engine creation): band kernel waves/SIMD, max column blocks
     int band_wps = 2, band_nc = 2;
     bool last_i8 = false;  // path of the last run
+    int band_i8_nc = 1;    // column blocks per exact-path item (NLDSC_BAND_I8_NC)
     bool band_i8 = true;   // default correlation path: exact int8 Gram (NLDSC_BAND_MODE=i8|f32)
 
     ~nldsc_engine() {
@@ -169,6 +170,75 @@ void replay_windows(const double* pos, const uint8_t* flags, int n, double w, in
     }
 }
 
+// Tile schedule of the band kernel.  A block pair (I <= J) is needed when it holds a pair (i < j)
+// with j in N(i) or i in N(j) and one of i, j is owned.  Rows need columns up to the last
+// in-window neighbour: R_i is the reference's (loose) cache bound — its extend_cache advances at
+// least one SNP per SNP, so R_i drifts past the window — so for sorted positions the bound is
+// tightened to the last index with pos <= pos_i + w (the kernel still masks with the exact
+// predicate).  Columns j need rows down to L_j (exact).
+void plan_items(const double* pos, const uint8_t* flags, int M, double w, const int* L, const int* R, int own_begin,
+                int own_end, int max_nc, std::vector<int4>& out) {
+    constexpr int B = 32;
+    const int nblk = (M + B - 1) / B;
+    std::vector<int> blk_pass(nblk, 0), blk_own(nblk, 0);
+    for (int j = 0; j < M; ++j) {
+        if (flags[j] & 1) blk_pass[j / B] = 1;
+        if (j >= own_begin && j < own_end) blk_own[j / B] = 1;
+    }
+    // sorted (non-decreasing over used SNPs)?  then the window's right edge is a binary search
+    std::vector<int> used_idx;
+    used_idx.reserve(M);
+    bool sorted = true;
+    for (int j = 0; j < M; ++j)
+        if (pos[j] >= 0) {
+            if (!used_idx.empty() && pos[j] < pos[used_idx.back()]) sorted = false;
+            used_idx.push_back(j);
+        }
+    std::vector<double> upos;
+    if (sorted) {
+        upos.reserve(used_idx.size());
+        for (int j : used_idx) upos.push_back(pos[j]);
+    }
+    auto row_bound = [&](int i) {
+        if (!sorted) return R[i];
+        // last used index with pos <= pos_i + w (ties inclusive, tools.h:41-49)
+        const size_t k = std::upper_bound(upos.begin(), upos.end(), pos[i] + w) - upos.begin();
+        const int hi = k == 0 ? -1 : used_idx[k - 1];
+        return std::min(R[i], hi);
+    };
+    std::vector<int> comp;
+    comp.reserve(M);
+    for (int j = 0; j < M; ++j) if (L[j] >= 0) comp.push_back(j);
+    int lo_row = own_begin;  // first row an owned SNP needs: min L_j over owned computed j
+    for (int j : comp) if (j >= own_begin && j < own_end) lo_row = std::min(lo_row, L[j]);
+    size_t cp = 0;
+    int run_rmax = -1;  // largest computed j with L_j <= current row (L non-decreasing over computed)
+    out.clear();
+    std::vector<int4> ones;
+    for (int I = std::max(0, lo_row / B); I < nblk && I * B < own_end; ++I) {
+        const int i_end = std::min(M, (I + 1) * B) - 1;
+        int jmax = -1;
+        for (int i = I * B; i <= i_end; ++i) if (L[i] >= 0) jmax = std::max(jmax, row_bound(i));
+        while (cp < comp.size() && L[comp[cp]] <= i_end) { run_rmax = comp[cp]; ++cp; }
+        jmax = std::max(jmax, run_rmax);
+        if (!blk_pass[I] || jmax < I * B) continue;
+        const int Jmax = std::min(nblk - 1, jmax / B);
+        auto useful = [&](int JJ) { return blk_pass[JJ] && (blk_own[I] || blk_own[JJ]); };
+        int J = I;
+        while (J <= Jmax) {
+            if (!useful(J)) { ++J; continue; }
+            if (max_nc == 2 && J + 1 <= Jmax && useful(J + 1)) {
+                out.push_back(make_int4(I, J, 2, 0));
+                J += 2;
+            } else {
+                ones.push_back(make_int4(I, J, 1, 0));
+                J += 1;
+            }
+        }
+    }
+    out.insert(out.end(), ones.begin(), ones.end());
+}
+
 }  // namespace
 
 extern "C" {
@@ -192,6 +262,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     e->device = d;
     if (const char* v = std::getenv("NLDSC_BAND_WPS")) e->band_wps = std::atoi(v) == 1 ? 1 : 2;
     if (const char* v = std::getenv("NLDSC_BAND_NC")) e->band_nc = std::atoi(v) == 1 ? 1 : 2;
+    if (const char* v = std::getenv("NLDSC_BAND_I8_NC")) e->band_i8_nc = std::atoi(v) == 2 ? 2 : 1;
     if (const char* v = std::getenv("NLDSC_BAND_MODE")) e->band_i8 = std::strcmp(v, "f32") != 0;
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     for (auto& ev : e->ev)
@@ -322,7 +393,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     const bool dom = !(p->flags & NLDSC_FLAG_ADDITIVE_ONLY);
     const bool strict = (p->flags & NLDSC_FLAG_STRICT_PLINK_ORDER) != 0;
     const bool use_i8 = (p->flags & NLDSC_FLAG_EXACT_I8) ? true : (p->flags & NLDSC_FLAG_FP32) ? false : e->band_i8;
-    const int max_nc = use_i8 ? 1 : e->band_nc;
+    const int max_nc = use_i8 ? e->band_i8_nc : e->band_nc;
     HIPCHK(hipSetDevice(e->device));
     hipStream_t st = e->stream;
 
@@ -374,47 +445,8 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     e->h_R.resize(M);
     replay_windows(p->positions, e->h_flags.data(), M, p->ld_wind, e->h_L.data(), e->h_R.data());
 
-    // Work items: row block I, column blocks [J0, J0 + nc).  A block pair (I <= J) is needed when
-    // it holds a pair (i < j) with j in N(i) or i in N(j) and one of i, j is owned.
-    std::vector<int> blk_pass(nblk, 0), blk_own(nblk, 0);
-    for (int j = 0; j < M; ++j) {
-        if (e->h_flags[j] & 1) blk_pass[j / BLK] = 1;
-        if (j >= own_begin && j < own_end) blk_own[j / BLK] = 1;
-    }
-    // colmax[x]: largest computed j with L_j <= x (L is non-decreasing over computed SNPs)
-    std::vector<int> comp;
-    comp.reserve(M);
-    for (int j = 0; j < M; ++j) if (e->h_L[j] >= 0) comp.push_back(j);
-    int lo_row = M;  // first row any owned SNP needs: min L_j over owned computed j
-    for (int j : comp) if (j >= own_begin && j < own_end) { lo_row = std::min(lo_row, e->h_L[j]); }
-    lo_row = std::min(lo_row, own_begin);
-    std::vector<int4> items2, items1;
-    size_t cp = 0;
-    int run_rmax = -1;
-    for (int I = std::max(0, lo_row / BLK); I < nblk && I * BLK < own_end + 0; ++I) {
-        const int i_end = std::min(M, (I + 1) * BLK) - 1;
-        int jmax = -1;
-        for (int i = I * BLK; i <= i_end; ++i) if (e->h_L[i] >= 0) jmax = std::max(jmax, e->h_R[i]);
-        while (cp < comp.size() && e->h_L[comp[cp]] <= i_end) { run_rmax = comp[cp]; ++cp; }
-        jmax = std::max(jmax, run_rmax);
-        if (!blk_pass[I] || jmax < I * BLK) continue;
-        const int Jmax = std::min(nblk - 1, jmax / BLK);
-        int J = I;
-        while (J <= Jmax) {
-            auto useful = [&](int JJ) { return blk_pass[JJ] && (blk_own[I] || blk_own[JJ]); };
-            if (!useful(J)) { ++J; continue; }
-            if (max_nc == 2 && J + 1 <= Jmax && useful(J + 1)) {
-                items2.push_back(make_int4(I, J, 2, 0));
-                J += 2;
-            } else {
-                items1.push_back(make_int4(I, J, 1, 0));
-                J += 1;
-            }
-        }
-    }
-    e->h_items.clear();
-    e->h_items.insert(e->h_items.end(), items2.begin(), items2.end());
-    e->h_items.insert(e->h_items.end(), items1.begin(), items1.end());
+    plan_items(p->positions, e->h_flags.data(), M, p->ld_wind, e->h_L.data(), e->h_R.data(), own_begin, own_end,
+               max_nc, e->h_items);
     // the band kernel reads rows [32 I, 32 (J0 + nc)) of geno / lut: check before launching
     if (pitch_words % 8 != 0 || n_it * 8 != pitch_words)
         return set_err(err, errlen, NLDSC_E_ARG, "internal: bad row pitch %d", pitch_words);
@@ -438,8 +470,8 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         double products = 0;  // 32x32 block products issued per sample slot
         for (const int4& it : e->h_items) {
             const bool dg = it.x == it.y;
-            if (use_i8)  // int8 Gram: xx, xo, ox, oo (+ xh, oh, and hx, ho off the diagonal)
-                products += dom ? (dg ? 6.0 : 8.0) : 4.0;
+            if (use_i8)  // int8 Gram: xx, xo, ox, oo (+ xh, oh, and hx, ho off the diagonal) per column block
+                products += it.z * (dom ? 8.0 : 4.0) - ((dom && dg) ? 2.0 : 0.0);
             else         // fp32: AA (+ AR, and RA off the diagonal)
                 products += it.z * (dom ? 3.0 : 1.0) - ((dom && dg) ? 1.0 : 0.0);
         }
@@ -447,7 +479,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     }
     if (!e->h_items.empty()) {
         if (use_i8)
-            HIPCHK(nldsc::launch_band_i8(dom, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, e->cst.p,
+            HIPCHK(nldsc::launch_band_i8(dom, max_nc, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, e->cst.p,
                                          e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
                                          (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                          e->ws_acc.p, st));
@@ -507,6 +539,21 @@ int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, d
     if (pairs) *pairs = e->pairs;
     if (n_band_items) *n_band_items = e->n_band_items;
     return NLDSC_OK;
+}
+
+int nldsc_plan_band(const double* positions, const uint8_t* flags, int32_t n_snp, double ld_wind, int32_t own_begin,
+                    int32_t own_end, int32_t max_nc, int32_t* L, int32_t* R, int32_t* items, int32_t cap) {
+    if (!positions || !flags || !L || !R || n_snp <= 0 || own_begin < 0 || own_end > n_snp || own_begin > own_end ||
+        (max_nc != 1 && max_nc != 2))
+        return NLDSC_E_ARG;
+    replay_windows(positions, flags, n_snp, ld_wind, L, R);
+    std::vector<int4> it;
+    plan_items(positions, flags, n_snp, ld_wind, L, R, own_begin, own_end, max_nc, it);
+    if ((int64_t)it.size() > (int64_t)cap || !items) return (int)std::min<size_t>(it.size(), INT32_MAX);
+    for (size_t k = 0; k < it.size(); ++k) {
+        items[4 * k] = it[k].x; items[4 * k + 1] = it[k].y; items[4 * k + 2] = it[k].z; items[4 * k + 3] = 0;
+    }
+    return (int)it.size();
 }
 
 int nldsc_engine_path(const nldsc_engine* e, int32_t* exact_i8, double* ops_alg_i8) {

@@ -21,7 +21,7 @@ hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int
                        const float2* lut, const int4* items, const double* pos, const int* Lw, const int* Rw,
                        const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                        int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, hipStream_t st);
-hipError_t launch_band_i8(bool dom, int n_items, const uint32_t* geno, int pitch_words, int n_it,
+hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, hipStream_t st);

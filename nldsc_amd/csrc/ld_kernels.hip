@@ -33,28 +33,60 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // is fine for dot products as long as every SNP uses the same one).  Bytes past the row and
 // the last byte's invalid bit pairs become 01 ("missing"), whose standardised value is exactly
 // 0 in both lookup tables, so they contribute nothing to any dot product.
+__device__ __forceinline__ void count_codes(uint32_t word, int& c0, int& c1, int& c2) {
+    const uint32_t hi = (word >> 1) & 0x55555555u, lo = word & 0x55555555u;
+    c0 += __popc(~hi & ~lo & 0x55555555u);  // 00 hom A1
+    c1 += __popc(hi & ~lo);                 // 10 het
+    c2 += __popc(hi & lo);                  // 11 hom A2
+}
+
+// One workgroup per SNP row; each thread builds 16-byte output chunks.  Interior chunks come from
+// 4-byte aligned loads of the (unaligned) .bed row recombined with v_alignbyte; the chunk holding
+// the row's last byte and the padding is built byte by byte.
 __global__ void __launch_bounds__(256) repack_count_kernel(const uint8_t* __restrict__ rows, uint32_t* __restrict__ geno,
                                                            int n_snp, int nb, int pitch_words, uint32_t tail_keep,
                                                            int* __restrict__ counts) {
     const int j = blockIdx.x;
     if (j >= n_snp) return;
     const uint8_t* src = rows + (size_t)j * (size_t)nb;
-    uint32_t* dst = geno + (size_t)j * (size_t)pitch_words;
+    uint4* dst = reinterpret_cast<uint4*>(geno + (size_t)j * (size_t)pitch_words);
+    const int n_chunks = pitch_words / 4;
+    const uintptr_t sa = reinterpret_cast<uintptr_t>(src);
+    const uint32_t off = (uint32_t)(sa & 3u);
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(sa - off);  // aligned, >= the buffer start
+    // chunk c reads aligned dwords base[4c .. 4c+4]; safe while they end before the row's last byte
+    const int fast_end = (int)(((long long)nb - 1 + off - 20) / 16) + 1;  // chunks c < fast_end are interior
     int c0 = 0, c1 = 0, c2 = 0;
-    for (int w = threadIdx.x; w < pitch_words; w += blockDim.x) {
-        uint32_t word = 0;
+    for (int c = threadIdx.x; c < n_chunks; c += blockDim.x) {
+        uint4 o;
+        if (c < fast_end && 16 * c + 20 <= nb - 1 + (int)off) {
+            const uint32_t d0 = base[4 * c], d1 = base[4 * c + 1], d2 = base[4 * c + 2], d3 = base[4 * c + 3],
+                           d4 = base[4 * c + 4];
+            o.x = __builtin_amdgcn_alignbyte(d1, d0, off);
+            o.y = __builtin_amdgcn_alignbyte(d2, d1, off);
+            o.z = __builtin_amdgcn_alignbyte(d3, d2, off);
+            o.w = __builtin_amdgcn_alignbyte(d4, d3, off);
+        } else {
+            uint32_t wv[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int p = 4 * w + k;
-            uint32_t b = p < nb ? (uint32_t)src[p] : 0x55u;
-            if (p == nb - 1) b = (b & tail_keep) | (0x55u & ~tail_keep);
-            word |= b << (8 * k);
+            for (int q = 0; q < 4; ++q) {
+                uint32_t word = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int p = 16 * c + 4 * q + k;
+                    uint32_t b = p < nb ? (uint32_t)src[p] : 0x55u;
+                    if (p == nb - 1) b = (b & tail_keep) | (0x55u & ~tail_keep);
+                    word |= b << (8 * k);
+                }
+                wv[q] = word;
+            }
+            o = make_uint4(wv[0], wv[1], wv[2], wv[3]);
         }
-        dst[w] = word;
-        const uint32_t hi = (word >> 1) & 0x55555555u, lo = word & 0x55555555u;
-        c0 += __popc(~hi & ~lo & 0x55555555u);  // 00 hom A1
-        c1 += __popc(hi & ~lo);                 // 10 het
-        c2 += __popc(hi & lo);                  // 11 hom A2
+        dst[c] = o;
+        count_codes(o.x, c0, c1, c2);
+        count_codes(o.y, c0, c1, c2);
+        count_codes(o.z, c0, c1, c2);
+        count_codes(o.w, c0, c1, c2);
     }
     // block reduction (4 waves of 64)
     for (int o = 32; o > 0; o >>= 1) {
@@ -394,13 +426,14 @@ __device__ __forceinline__ void decode16(uint32_t w, i32x4& X, i32x4& H, i32x4& 
 }
 
 struct BandI8Lds {
-    SnpSlot info[64];
-    SnpConst cst[64];
-    double l2[64], l2d[64];
-    int wsa[64], wsd[64], wse[64];
+    SnpSlot info[NS_MAX];
+    SnpConst cst[NS_MAX];
+    double l2[NS_MAX], l2d[NS_MAX];
+    int wsa[NS_MAX], wsd[NS_MAX], wse[NS_MAX];
 };
 
-template <bool DOM, bool DIAG>
+// NC column blocks J0 .. J0+NC-1 share the row decode; DIAG0: block 0 is the diagonal (J0 == I).
+template <bool DOM, int NC, bool DIAG0>
 __device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const uint32_t* __restrict__ geno,
                                              int pitch_words, int n_it, const SnpConst* __restrict__ cst,
                                              const double* __restrict__ pos, const int* __restrict__ Lw,
@@ -408,11 +441,12 @@ __device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const
                                              int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                                              int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
                                              int* __restrict__ ws_acc) {
+    constexpr int NS = 32 * (1 + NC);
     const int lane = threadIdx.x;
     const int i = lane & 31, h = lane >> 5;
-    const int I = it.x, J = it.y;
-    for (int s = lane; s < 64; s += 64) {
-        const int g = s < 32 ? I * 32 + s : J * 32 + (s - 32);
+    const int I = it.x, J0 = it.y;
+    for (int s = lane; s < NS; s += 64) {
+        const int g = s < 32 ? I * 32 + s : (J0 + (s - 32) / 32) * 32 + (s & 31);
         SnpSlot si;
         si.g = g;
         if (g < n_snp) {
@@ -428,81 +462,103 @@ __device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const
     __syncthreads();
 
     // Gram accumulators: additive xx, xo, ox, oo; dominance xh, oh (row -> col), hx, ho (col -> row)
-    i32x16 gxx = {}, gxo = {}, gox = {}, goo = {}, gxh = {}, goh = {}, ghx = {}, gho = {};
+    i32x16 gxx[NC], gxo[NC], gox[NC], goo[NC], gxh[NC], goh[NC], ghx[NC], gho[NC];
+#pragma unroll
+    for (int b = 0; b < NC; ++b) {
+        gxx[b] = gxo[b] = gox[b] = goo[b] = gxh[b] = goh[b] = ghx[b] = gho[b] = i32x16{};
+    }
     const uint4* rowp = reinterpret_cast<const uint4*>(geno + (size_t)(I * 32 + i) * (size_t)pitch_words) + h;
-    const uint4* colp = reinterpret_cast<const uint4*>(geno + (size_t)(J * 32 + i) * (size_t)pitch_words) + h;
-    uint4 nr = rowp[0], ncl = colp[0];
+    const uint4* colp[NC];
+#pragma unroll
+    for (int b = 0; b < NC; ++b)
+        colp[b] = reinterpret_cast<const uint4*>(geno + (size_t)((J0 + b) * 32 + i) * (size_t)pitch_words) + h;
+    uint4 nr = rowp[0], ncl[NC];
+#pragma unroll
+    for (int b = 0; b < NC; ++b) ncl[b] = colp[b][0];
     for (int t = 0; t < n_it; ++t) {
-        const uint4 wr4 = nr, wc4 = ncl;
+        const uint4 wr4 = nr;
+        uint4 wc4[NC];
+#pragma unroll
+        for (int b = 0; b < NC; ++b) wc4[b] = ncl[b];
         if (t + 1 < n_it) {
             nr = rowp[2 * (t + 1)];
-            ncl = colp[2 * (t + 1)];
+#pragma unroll
+            for (int b = 0; b < NC; ++b) ncl[b] = colp[b][2 * (t + 1)];
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint32_t wr = q == 0 ? wr4.x : q == 1 ? wr4.y : q == 2 ? wr4.z : wr4.w;
-            const uint32_t wc = q == 0 ? wc4.x : q == 1 ? wc4.y : q == 2 ? wc4.z : wc4.w;
-            i32x4 Xi, Hi, Oi, Xj, Hj, Oj;
+            i32x4 Xi, Hi, Oi;
             decode16(wr, Xi, Hi, Oi);
-            decode16(wc, Xj, Hj, Oj);
-            gxx = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Xj, gxx, 0, 0, 0);
-            gxo = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Oj, gxo, 0, 0, 0);
-            gox = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Xj, gox, 0, 0, 0);
-            goo = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Oj, goo, 0, 0, 0);
-            if (DOM) {
-                gxh = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Hj, gxh, 0, 0, 0);
-                goh = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Hj, goh, 0, 0, 0);
-                if (!DIAG) {  // on a diagonal block R_i . A_j is the transposed A_j . R_i
-                    ghx = __builtin_amdgcn_mfma_i32_32x32x32_i8(Hi, Xj, ghx, 0, 0, 0);
-                    gho = __builtin_amdgcn_mfma_i32_32x32x32_i8(Hi, Oj, gho, 0, 0, 0);
+#pragma unroll
+            for (int b = 0; b < NC; ++b) {
+                const uint32_t wc = q == 0 ? wc4[b].x : q == 1 ? wc4[b].y : q == 2 ? wc4[b].z : wc4[b].w;
+                i32x4 Xj, Hj, Oj;
+                decode16(wc, Xj, Hj, Oj);
+                gxx[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Xj, gxx[b], 0, 0, 0);
+                gxo[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Oj, gxo[b], 0, 0, 0);
+                gox[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Xj, gox[b], 0, 0, 0);
+                goo[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Oj, goo[b], 0, 0, 0);
+                if (DOM) {
+                    gxh[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Hj, gxh[b], 0, 0, 0);
+                    goh[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Hj, goh[b], 0, 0, 0);
+                    if (!(DIAG0 && b == 0)) {  // on a diagonal block R_i . A_j is the transposed A_j . R_i
+                        ghx[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Hi, Xj, ghx[b], 0, 0, 0);
+                        gho[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Hi, Oj, gho[b], 0, 0, 0);
+                    }
                 }
             }
         }
     }
 
     // ---- fused epilogue (fp64): standardised dots from the integer Gram, r2adj, masks, sums ----
-    const int sj = 32 + i;
-    const SnpSlot cj = sh.info[sj];
-    const SnpConst kj = sh.cst[sj];
-    const bool pj = cj.fl & 1, rpj = (cj.fl & 2) != 0;
-    const bool compj = cj.L >= 0;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int si = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const SnpSlot ci = sh.info[si];
-        const bool pi = ci.fl & 1, rpi = (ci.fl & 2) != 0;
-        const bool inwin = fabs(cj.pos - ci.pos) <= ld_wind && ci.g != cj.g;
-        const bool nij = inwin && ci.L >= 0 && cj.g >= ci.L && cj.g <= ci.R && pj;
-        const bool nji = !DIAG && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
-        if (nij || nji) {
-            const SnpConst ki = sh.cst[si];
-            const double xx = (double)gxx[r], xo = (double)gxo[r], ox = (double)gox[r], oo = (double)goo[r];
-            const double aa = (xx - kj.mu * xo - ki.mu * (ox - kj.mu * oo)) / (ki.sa * kj.sa);
-            const double r2 = r2_adjusted(aa, n_org);
-            if (nij) { atomicAdd(&sh.l2[si], r2); atomicAdd(&sh.wsa[si], 1); }
-            if (nji) { atomicAdd(&sh.l2[sj], r2); atomicAdd(&sh.wsa[sj], 1); }
-            if (DOM) {
-                if (nij && rpj) {  // A_i . R_j -> L2D_i (ldscalc.h:40-46)
-                    const double xh = (double)gxh[r], oh = (double)goh[r];
-                    const double ar = (2.0 * xh - kj.beta * xx - kj.c * xo -
-                                       ki.mu * (2.0 * oh - kj.beta * ox - kj.c * oo)) / (ki.sa * kj.s);
-                    const double rd = r2_adjusted(ar, n_org);
-                    atomicAdd(&sh.l2d[si], rd); atomicAdd(&sh.wsd[si], 1);
-                    if (rd > rsq_thr) atomicAdd(&sh.wse[si], 1);
-                }
-                if (!DIAG && nji && rpi) {  // R_i . A_j -> L2D_j
-                    const double hx = (double)ghx[r], ho = (double)gho[r];
-                    const double ra = (2.0 * hx - ki.beta * xx - ki.c * ox -
-                                       kj.mu * (2.0 * ho - ki.beta * xo - ki.c * oo)) / (ki.s * kj.sa);
-                    const double rd = r2_adjusted(ra, n_org);
-                    atomicAdd(&sh.l2d[sj], rd); atomicAdd(&sh.wsd[sj], 1);
-                    if (rd > rsq_thr) atomicAdd(&sh.wse[sj], 1);
+    for (int b = 0; b < NC; ++b) {
+        const bool diag = DIAG0 && b == 0;
+        const int sj = 32 + 32 * b + i;
+        const SnpSlot cj = sh.info[sj];
+        const SnpConst kj = sh.cst[sj];
+        const bool pj = cj.fl & 1, rpj = (cj.fl & 2) != 0;
+        const bool compj = cj.L >= 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int si = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const SnpSlot ci = sh.info[si];
+            const bool pi = ci.fl & 1, rpi = (ci.fl & 2) != 0;
+            const bool inwin = fabs(cj.pos - ci.pos) <= ld_wind && ci.g != cj.g;
+            const bool nij = inwin && ci.L >= 0 && cj.g >= ci.L && cj.g <= ci.R && pj;
+            const bool nji = !diag && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
+            if (nij || nji) {
+                const SnpConst ki = sh.cst[si];
+                const double xx = (double)gxx[b][r], xo = (double)gxo[b][r], ox = (double)gox[b][r],
+                             oo = (double)goo[b][r];
+                const double aa = (xx - kj.mu * xo - ki.mu * (ox - kj.mu * oo)) / (ki.sa * kj.sa);
+                const double r2 = r2_adjusted(aa, n_org);
+                if (nij) { atomicAdd(&sh.l2[si], r2); atomicAdd(&sh.wsa[si], 1); }
+                if (nji) { atomicAdd(&sh.l2[sj], r2); atomicAdd(&sh.wsa[sj], 1); }
+                if (DOM) {
+                    if (nij && rpj) {  // A_i . R_j -> L2D_i (ldscalc.h:40-46)
+                        const double xh = (double)gxh[b][r], oh = (double)goh[b][r];
+                        const double ar = (2.0 * xh - kj.beta * xx - kj.c * xo -
+                                           ki.mu * (2.0 * oh - kj.beta * ox - kj.c * oo)) / (ki.sa * kj.s);
+                        const double rd = r2_adjusted(ar, n_org);
+                        atomicAdd(&sh.l2d[si], rd); atomicAdd(&sh.wsd[si], 1);
+                        if (rd > rsq_thr) atomicAdd(&sh.wse[si], 1);
+                    }
+                    if (!diag && nji && rpi) {  // R_i . A_j -> L2D_j
+                        const double hx = (double)ghx[b][r], ho = (double)gho[b][r];
+                        const double ra = (2.0 * hx - ki.beta * xx - ki.c * ox -
+                                           kj.mu * (2.0 * ho - ki.beta * xo - ki.c * oo)) / (ki.s * kj.sa);
+                        const double rd = r2_adjusted(ra, n_org);
+                        atomicAdd(&sh.l2d[sj], rd); atomicAdd(&sh.wsd[sj], 1);
+                        if (rd > rsq_thr) atomicAdd(&sh.wse[sj], 1);
+                    }
                 }
             }
         }
     }
     __syncthreads();
-    for (int s = lane; s < 64; s += 64) {
+    for (int s = lane; s < NS; s += 64) {
         const int g = sh.info[s].g;
         if (g < own_lo || g >= own_hi || g >= n_snp) continue;
         if (sh.wsa[s]) {
@@ -517,8 +573,9 @@ __device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const
     }
 }
 
-template <bool DOM>
-__global__ void __launch_bounds__(64, 2) band_i8_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
+// WPS: waves per SIMD the register allocation must allow (NC=1 bodies fit 2, NC=2 bodies need 1).
+template <bool DOM, int WPS>
+__global__ void __launch_bounds__(64, WPS) band_i8_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
                                                         const SnpConst* __restrict__ cst, const int4* __restrict__ items,
                                                         const double* __restrict__ pos, const int* __restrict__ Lw,
                                                         const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
@@ -527,12 +584,13 @@ __global__ void __launch_bounds__(64, 2) band_i8_kernel(const uint32_t* __restri
                                                         double* __restrict__ l2d_acc, int* __restrict__ ws_acc) {
     __shared__ BandI8Lds sh;
     const int4 it = items[blockIdx.x];
-    if (it.y == it.x)
-        band_i8_body<DOM, true>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,
-                                rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc);
-    else
-        band_i8_body<DOM, false>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,
-                                 rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc);
+#define NLDSC_BODY(NC_, DIAG_)                                                                                        \
+    band_i8_body<DOM, NC_, DIAG_>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,  \
+                                  rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc)
+    const bool diag = it.y == it.x;
+    if (WPS == 1 && it.z == 2) { if (diag) NLDSC_BODY(2, true); else NLDSC_BODY(2, false); }
+    else { if (diag) NLDSC_BODY(1, true); else NLDSC_BODY(1, false); }
+#undef NLDSC_BODY
 }
 
 // ------------------------------------------------------------------------------------------
@@ -650,19 +708,18 @@ hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int
     return hipGetLastError();
 }
 
-hipError_t launch_band_i8(bool dom, int n_items, const uint32_t* geno, int pitch_words, int n_it,
+hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, hipStream_t st) {
     if (n_items <= 0) return hipSuccess;
-    if (dom)
-        hipLaunchKernelGGL((band_i8_kernel<true>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, cst, items,
-                           pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc,
-                           ws_acc);
-    else
-        hipLaunchKernelGGL((band_i8_kernel<false>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, cst,
-                           items, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc,
-                           l2d_acc, ws_acc);
+#define NLDSC_BAND(DOM_, WPS_)                                                                                      \
+    hipLaunchKernelGGL((band_i8_kernel<DOM_, WPS_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, cst,   \
+                       items, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, \
+                       ws_acc)
+    if (dom) { if (max_nc == 2) NLDSC_BAND(true, 1); else NLDSC_BAND(true, 2); }
+    else { if (max_nc == 2) NLDSC_BAND(false, 1); else NLDSC_BAND(false, 2); }
+#undef NLDSC_BAND
     return hipGetLastError();
 }
 

@@ -1,0 +1,83 @@
+"""Host-side plan of the band kernel (C ABI nldsc_plan_band; no GPU): the window replay equals the
+oracle's replay of the reference pointers, and the work items cover every block pair holding a
+needed (SNP, neighbour) pair for the owned range."""
+import numpy as np
+import pytest
+
+from conftest import load_set
+from oracle import oracle as O
+
+
+def needed_blocks(pos, passed, w, L, R, own):
+    """{(I, J)} block pairs (I <= J) that hold some j in N(i) with i owned (row) or ..."""
+    need = set()
+    for i in range(len(pos)):
+        if L[i] < 0 or not (own[0] <= i < own[1]):
+            continue
+        for k in range(L[i], R[i] + 1):
+            if k != i and passed[k] and abs(pos[k] - pos[i]) <= w:
+                a, b = sorted((i // 32, k // 32))
+                need.add((a, b))
+    return need
+
+
+def covered(items):
+    cov = set()
+    for I, J0, nc, _ in items:
+        assert I <= J0 and nc in (1, 2)
+        for b in range(nc):
+            cov.add((int(I), int(J0) + b))
+    return cov
+
+
+def check(pos, passed, w, own=None, max_nc=1):
+    from nldsc_amd import _lib
+    n = len(pos)
+    own = (0, n) if own is None else own
+    L, R, items = _lib.plan_band(pos, passed.astype(np.uint8), w, own=own, max_nc=max_nc)
+    Lp, Rp = O.replay_windows(pos, passed, w)
+    np.testing.assert_array_equal(L, Lp)
+    np.testing.assert_array_equal(R[L >= 0], Rp[Lp >= 0])
+    nblk = (n + 31) // 32
+    assert all(J0 + nc <= nblk for _, J0, nc, _ in items)
+    miss = needed_blocks(pos, passed, w, L, R, own) - covered(items)
+    assert not miss, sorted(miss)[:10]
+    return items
+
+
+@pytest.mark.parametrize("name", ["n1000", "n1003", "allmiss"])
+def test_plan_covers_golden_sets(name):
+    _, pos, meta, orc, _ = load_set(name)
+    passed = (pos >= 0) & ~(orc["maf"] <= meta["maf"])
+    for nc in (1, 2):
+        check(pos, passed, meta["ld_wind"], max_nc=nc)
+    M = meta["n_snp"]
+    for own in ((0, 100), (M // 3, 2 * M // 3), (M - 50, M)):
+        check(pos, passed, meta["ld_wind"], own=own)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_plan_covers_random_and_unsorted(seed):
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 400))
+    pos = np.cumsum(rng.exponential(0.02, n))
+    if seed % 2:  # unsorted: the reference's pointer semantics, the plan falls back to R as bound
+        pos = pos[rng.permutation(n)]
+    pos[rng.random(n) < 0.05] = -1.0
+    passed = (pos >= 0) & (rng.random(n) > 0.1)
+    w = float(rng.choice([0.01, 0.3, 5.0]))
+    check(pos, passed, w, max_nc=1 + seed % 2)
+    a = int(rng.integers(0, n))
+    check(pos, passed, w, own=(a, min(n, a + 57)))
+
+
+def test_plan_is_tight_on_c3_geometry():
+    """chr1-like C3 positions (80 000 SNPs over 280 cM, 1 cM): about 10.4 column blocks per row block
+    (the geometric minimum for 32-SNP blocks; the reference's loose cache bound R would give 12.5)."""
+    from nldsc_amd import _lib
+    rng = np.random.default_rng(7)
+    M = 80_000
+    rng.uniform(0.02, 0.5, size=M)
+    pos = np.round(np.cumsum(rng.exponential(280.0 / M, size=M)), 6)
+    _, _, items = _lib.plan_band(pos, np.ones(M, np.uint8), 1.0)
+    assert len(items) / ((M + 31) // 32) < 10.6

@@ -41,7 +41,8 @@ def main():
                      for p in parts if p.startswith(("wps", "nc")))
         os.environ["NLDSC_BAND_WPS"] = knobs.get("wps", "2")
         os.environ["NLDSC_BAND_NC"] = knobs.get("nc", "2")
-        os.environ["NLDSC_BAND_MODE"] = "i8" if "i8" in parts else "f32"
+        os.environ["NLDSC_BAND_MODE"] = "i8" if any(x.startswith("i8") for x in parts) else "f32"
+        os.environ["NLDSC_BAND_I8_NC"] = "2" if "i8nc2" in parts else "1"
         e = Engine(0, lib_path=lib)
         v = label
         e.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
