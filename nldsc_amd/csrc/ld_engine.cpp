@@ -194,18 +194,19 @@ void plan_items(const double* pos, const uint8_t* flags, int M, double w, const 
             if (!used_idx.empty() && pos[j] < pos[used_idx.back()]) sorted = false;
             used_idx.push_back(j);
         }
-    std::vector<double> upos;
+    // sorted: last used index with pos <= pos_i + w (ties inclusive, tools.h:41-49) by a two-pointer sweep
+    std::vector<int> hi_of;
     if (sorted) {
-        upos.reserve(used_idx.size());
-        for (int j : used_idx) upos.push_back(pos[j]);
+        hi_of.assign(M, -1);
+        size_t k = 0;
+        for (size_t u = 0; u < used_idx.size(); ++u) {
+            const double lim = pos[used_idx[u]] + w;
+            if (k < u) k = u;
+            while (k + 1 < used_idx.size() && pos[used_idx[k + 1]] <= lim) ++k;
+            hi_of[used_idx[u]] = used_idx[k];
+        }
     }
-    auto row_bound = [&](int i) {
-        if (!sorted) return R[i];
-        // last used index with pos <= pos_i + w (ties inclusive, tools.h:41-49)
-        const size_t k = std::upper_bound(upos.begin(), upos.end(), pos[i] + w) - upos.begin();
-        const int hi = k == 0 ? -1 : used_idx[k - 1];
-        return std::min(R[i], hi);
-    };
+    auto row_bound = [&](int i) { return sorted ? std::min(R[i], hi_of[i]) : R[i]; };
     std::vector<int> comp;
     comp.reserve(M);
     for (int j = 0; j < M; ++j) if (L[j] >= 0) comp.push_back(j);
