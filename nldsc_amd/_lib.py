@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 import numpy as np
 
@@ -58,6 +59,13 @@ def lib(path: str | None = None) -> ctypes.CDLL:
     e.g. for interleaved A/B timing of kernel variants in one process)."""
     path = path or LIB_PATH
     if path not in _libs:
+        # One HIP runtime per process: torch bundles its own libamdhip64.so.7 (same soname as ROCm's). If
+        # torch is already imported, make sure its runtime is initialised before ours binds to it.
+        if "torch" in sys.modules:
+            try:
+                sys.modules["torch"].cuda.init()
+            except Exception:  # no device: our own calls will report it
+                pass
         if not os.path.exists(path):
             raise ImportError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; "
                               f"g.build()'` (make -C nldsc_amd/csrc). nldsc_amd has no CPU fallback.")

@@ -472,14 +472,19 @@ __device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const
 #pragma unroll
     for (int b = 0; b < NC; ++b)
         colp[b] = reinterpret_cast<const uint4*>(geno + (size_t)((J0 + b) * 32 + i) * (size_t)pitch_words) + h;
-    uint4 nr = rowp[0], ncl[NC];
+    auto word_of = [](const uint4& w, int q) { return q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w; };
+    uint4 wr4 = rowp[0], wc4[NC];
 #pragma unroll
-    for (int b = 0; b < NC; ++b) ncl[b] = colp[b][0];
+    for (int b = 0; b < NC; ++b) wc4[b] = colp[b][0];
+    // operands of the current K step; the next step's are decoded while these feed the MFMAs
+    i32x4 Xi, Hi, Oi, Xj[NC], Hj[NC], Oj[NC];
+    decode16(wr4.x, Xi, Hi, Oi);
+#pragma unroll
+    for (int b = 0; b < NC; ++b) decode16(wc4[b].x, Xj[b], Hj[b], Oj[b]);
     for (int t = 0; t < n_it; ++t) {
-        const uint4 wr4 = nr;
-        uint4 wc4[NC];
+        uint4 nr = wr4, ncl[NC];
 #pragma unroll
-        for (int b = 0; b < NC; ++b) wc4[b] = ncl[b];
+        for (int b = 0; b < NC; ++b) ncl[b] = wc4[b];
         if (t + 1 < n_it) {
             nr = rowp[2 * (t + 1)];
 #pragma unroll
@@ -487,28 +492,38 @@ __device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t wr = q == 0 ? wr4.x : q == 1 ? wr4.y : q == 2 ? wr4.z : wr4.w;
-            i32x4 Xi, Hi, Oi;
-            decode16(wr, Xi, Hi, Oi);
+            i32x4 Xin, Hin, Oin, Xjn[NC], Hjn[NC], Ojn[NC];
+            decode16(q < 3 ? word_of(wr4, q + 1) : nr.x, Xin, Hin, Oin);
+#pragma unroll
+            for (int b = 0; b < NC; ++b) decode16(q < 3 ? word_of(wc4[b], q + 1) : ncl[b].x, Xjn[b], Hjn[b], Ojn[b]);
 #pragma unroll
             for (int b = 0; b < NC; ++b) {
-                const uint32_t wc = q == 0 ? wc4[b].x : q == 1 ? wc4[b].y : q == 2 ? wc4[b].z : wc4[b].w;
-                i32x4 Xj, Hj, Oj;
-                decode16(wc, Xj, Hj, Oj);
-                gxx[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Xj, gxx[b], 0, 0, 0);
-                gxo[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Oj, gxo[b], 0, 0, 0);
-                gox[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Xj, gox[b], 0, 0, 0);
-                goo[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Oj, goo[b], 0, 0, 0);
+                gxx[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Xj[b], gxx[b], 0, 0, 0);
+                gxo[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Oj[b], gxo[b], 0, 0, 0);
+                gox[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Xj[b], gox[b], 0, 0, 0);
+                goo[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Oj[b], goo[b], 0, 0, 0);
                 if (DOM) {
-                    gxh[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Hj, gxh[b], 0, 0, 0);
-                    goh[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Hj, goh[b], 0, 0, 0);
+                    gxh[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Hj[b], gxh[b], 0, 0, 0);
+                    goh[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Hj[b], goh[b], 0, 0, 0);
                     if (!(DIAG0 && b == 0)) {  // on a diagonal block R_i . A_j is the transposed A_j . R_i
-                        ghx[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Hi, Xj, ghx[b], 0, 0, 0);
-                        gho[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Hi, Oj, gho[b], 0, 0, 0);
+                        ghx[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Hi, Xj[b], ghx[b], 0, 0, 0);
+                        gho[b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Hi, Oj[b], gho[b], 0, 0, 0);
                     }
                 }
             }
+            // interleave: one MFMA, then a share of the next step's decode VALU (T19)
+#pragma unroll
+            for (int m = 0; m < 8 * NC; ++m) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
+            }
+            Xi = Xin; Hi = Hin; Oi = Oin;
+#pragma unroll
+            for (int b = 0; b < NC; ++b) { Xj[b] = Xjn[b]; Hj[b] = Hjn[b]; Oj[b] = Ojn[b]; }
         }
+        wr4 = nr;
+#pragma unroll
+        for (int b = 0; b < NC; ++b) wc4[b] = ncl[b];
     }
 
     // ---- fused epilogue (fp64): standardised dots from the integer Gram, r2adj, masks, sums ----

@@ -19,6 +19,10 @@ SETS = sorted(golden_sets())
 
 @pytest.fixture(scope="module")
 def engine():
+    # torch bundles its own libamdhip64.so.7; initialise it before libnldsc_amd.so pulls in ROCm's copy so
+    # the process has ONE HIP runtime (the full-size test allocates through torch)
+    import torch
+    torch.cuda.init()
     from nldsc_amd.engine import Engine
     e = Engine(0)
     yield e
