@@ -29,6 +29,23 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 den
 I8_MFMA_PEAK_TOPS = 5000.0     # MI355X_MICROARCH.md: int8 MFMA = 2x the 2.5 PF dense bf16 rate
 
 
+def pmc_traffic(kernel_key: str, n_org: int, n_snp: int):
+    """HBM-side bytes per launch of `kernel_key` from the newest committed rocprofv3 PMC summary
+    (profiles/*_pmc.json, measured on the same C3 workload), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True):
+        try:
+            doc = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if f"N={n_org}" not in doc.get("workload", "") or f"M={n_snp}" not in doc.get("workload", ""):
+            continue
+        for name, k in doc.get("kernels", {}).items():
+            if name.startswith(kernel_key):
+                return k["traffic_bytes"], os.path.relpath(path, REPO)
+    return None, None
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -154,7 +171,10 @@ def main():
             roof = {"bound": "mfma", "achieved": fp32_equiv, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "kernel": "band_kernel<true> (v_mfma_f32_32x32x2_f32)", "flop_alg_per_launch": flop}
             peak = FP32_MFMA_PEAK_TFLOPS
-        roof.update(frac=roof["achieved"] / peak, traffic=None, avg_launch_ms=band_ms,
+        traffic, traffic_src = pmc_traffic("band_i8_kernel" if exact else "band_kernel", N, M)
+        roof.update(frac=roof["achieved"] / peak, traffic=traffic, traffic_source=traffic_src,
+                    algorithmic_bytes_per_launch=M * 4 * ((((N + 3) // 4) + 31) // 32 * 8),
+                    avg_launch_ms=band_ms,
                     issued_per_launch=tims[-1]["flop_issued"], work_items=tims[-1]["band_items"],
                     mfma_pipe_frac=tims[-1]["flop_issued"] / (band_ms * 1e-3) / 1e12 / peak,
                     fp32_formulation_flop_per_launch=flop, fp32_equivalent_tflops=fp32_equiv,
