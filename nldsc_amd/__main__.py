@@ -35,7 +35,8 @@ def main():
 
 
 @main.command("ld", help="Estimate additive and non-additive LD Scores")
-@click.option("--bfile", help="Path prefix for PLINK .bed/.bim/.fam file or path to one of them", metavar="FILE",
+@click.option("--bfile", help="Path prefix for PLINK .bed/.bim/.fam file or path to one of them; '@' in place of "
+                               "the chromosome number runs every chromosome (then --out needs '@' too)", metavar="FILE",
               required=True)
 @click.option("-o", "--out", help="Output path of the LD score table", metavar="FILE")
 @click.option("-kb", "--ld-wind-kb", help="Window size in kilo-base pairs (kb)", metavar="W")
@@ -65,6 +66,11 @@ def est_ld(bfile, out, ld_wind_kb, ld_wind_cm, maf_thr, std_thr, rsq_thr, extra,
     from .ldscore import _ldscore, estimate_lds
     flags = (_ldscore.FLAG_STRICT_PLINK_ORDER if strict_plink_order else 0) | \
             (_ldscore.FLAG_ADDITIVE_ONLY if additive_only else 0)
+    if "@" in bfile:  # whole genome: one output per chromosome, chromosomes spread over GPUs
+        from .ldscore.genome import estimate_lds_genome
+        estimate_lds_genome(bfile, ld_wind=ld_wind, wind_metric=wind_metric, maf_thr=maf_thr, std_thr=std_thr,
+                            rsq_thr=rsq_thr, out=out, extra=extra, write_m=write_m, flags=flags, device=device)
+        return
     estimate_lds(bfile, ld_wind=ld_wind, wind_metric=wind_metric, maf_thr=maf_thr, std_thr=std_thr,
                  rsq_thr=rsq_thr, out=out, extra=extra, summary=True, write_m=write_m, flags=flags, device=device)
 
