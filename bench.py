@@ -91,6 +91,8 @@ def main():
                     help="correlation path: exact int8 Gram (default) or fp32 standardised values")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="collectives backend for N > 1 (gloo: rehearse several ranks on one GPU)")
     ap.add_argument("--workload", choices=("c3", "c4"), default="c3",
                     help="c3: one chr1-like chromosome per GPU (default, the BASELINE metric); c4: the 22-autosome "
                          "whole genome (sum M ~ 600k, BASELINE.json configs[3]) spread over the GPUs by LPT")
@@ -102,15 +104,21 @@ def main():
     import torch
     import torch.distributed as dist
 
+    if args.backend == "gloo":
+        local = 0  # rehearsal: every rank shares GPU 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group("gloo")
+    coll = "cuda" if args.backend == "nccl" else "cpu"
 
     from nldsc_amd import _lib, synth
     from nldsc_amd.engine import Engine
 
     if args.workload == "c4":
-        return whole_genome(args, world, rank, local)
+        return whole_genome(args, world, rank, local, coll)
     N, M = args.n_org, args.n_snp
     flags = (_lib.FLAG_ADDITIVE_ONLY if args.additive_only else 0) | \
         (_lib.FLAG_EXACT_I8 if args.path == "i8" else _lib.FLAG_FP32)
@@ -134,9 +142,9 @@ def main():
         if world > 1:  # assemble the score tables on rank 0 (RCCL over xGMI)
             tab = torch.from_numpy(np.stack([out["l2"], out["l2d"], out["maf"], out["residuals_std"],
                                              out["l2_ws"].astype(np.float64), out["l2d_ws"].astype(np.float64),
-                                             out["l2d_wse"].astype(np.float64)])).cuda()
-            gathered = torch.empty((world,) + tab.shape, dtype=tab.dtype, device=tab.device)
-            dist.all_gather_into_tensor(gathered, tab)
+                                             out["l2d_wse"].astype(np.float64)])).to(coll)
+            gathered = [torch.empty_like(tab) for _ in range(world)]
+            dist.all_gather(gathered, tab)
         return eng.timings()
 
     for _ in range(args.warmup):
@@ -150,8 +158,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    pairs_step = torch.tensor([tims[-1]["pairs"]], dtype=torch.float64, device="cuda")
+    el = torch.tensor([elapsed], dtype=torch.float64, device=coll)
+    pairs_step = torch.tensor([tims[-1]["pairs"]], dtype=torch.float64, device=coll)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(pairs_step, op=dist.ReduceOp.SUM)
@@ -230,7 +238,7 @@ AUTOSOME_CM = [278, 263, 224, 214, 209, 193, 184, 169, 167, 181, 158, 174, 126, 
                63, 72]
 
 
-def whole_genome(args, world, rank, local):
+def whole_genome(args, world, rank, local, coll):
     """C4: 22 autosomes, M_c proportional to genetic length (sum ~600k), N = 315 599, --ld-wind-cm 1.  Chromosome
     units are assigned to ranks by LPT; each rank keeps its units resident in HBM; one step = every unit of every
     rank computed; value = all ranks' pairs / max-over-ranks wall time."""
@@ -273,8 +281,8 @@ def whole_genome(args, world, rank, local):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
-    pr = torch.tensor([pairs], dtype=torch.float64, device="cuda")
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=coll)
+    pr = torch.tensor([pairs], dtype=torch.float64, device=coll)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(pr, op=dist.ReduceOp.SUM)
