@@ -27,6 +27,17 @@ sys.path.insert(0, REPO)
 METRIC = "SNP-pairs/sec + wall-clock, chr1 N=315k 1cM window, 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 I8_MFMA_PEAK_TOPS = 5000.0     # MI355X_MICROARCH.md: int8 MFMA = 2x the 2.5 PF dense bf16 rate
+F4_MFMA_PEAK_TFLOPS = 10000.0  # MI355X_MICROARCH.md: fp4 (block-scaled f8f6f4) ~10 PF dense
+
+# --path -> (engine flag name, MFMA peak, unit, dominant kernel, dtype)
+PATHS = {
+    "f4": ("FLAG_EXACT_F4", F4_MFMA_PEAK_TFLOPS, "TFLOP/s",
+           "band_f4_kernel<true> (v_mfma_scale_f32_32x32x64_f8f6f4, e2m1 operands, exact integer Gram in fp32)",
+           "fp4"),
+    "i8": ("FLAG_EXACT_I8", I8_MFMA_PEAK_TOPS, "TOP/s",
+           "band_i8_kernel<true> (v_mfma_i32_32x32x32_i8, exact int32 Gram)", "i8"),
+    "f32": ("FLAG_FP32", FP32_MFMA_PEAK_TFLOPS, "TFLOP/s", "band_kernel<true> (v_mfma_f32_32x32x2_f32)", "f32"),
+}
 
 
 def pmc_traffic(kernel_key: str, n_org: int, n_snp: int):
@@ -87,8 +98,9 @@ def main():
     ap.add_argument("--maf", type=float, default=1e-4)
     ap.add_argument("--std-thr", type=float, default=1e-5)
     ap.add_argument("--additive-only", action="store_true")
-    ap.add_argument("--path", choices=("i8", "f32"), default="i8",
-                    help="correlation path: exact int8 Gram (default) or fp32 standardised values")
+    ap.add_argument("--path", choices=tuple(PATHS), default="f4",
+                    help="correlation path: exact Gram on fp4 MFMAs (default), on int8 MFMAs, or fp32 "
+                         "standardised values")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
@@ -120,8 +132,7 @@ def main():
     if args.workload == "c4":
         return whole_genome(args, world, rank, local, coll)
     N, M = args.n_org, args.n_snp
-    flags = (_lib.FLAG_ADDITIVE_ONLY if args.additive_only else 0) | \
-        (_lib.FLAG_EXACT_I8 if args.path == "i8" else _lib.FLAG_FP32)
+    flags = (_lib.FLAG_ADDITIVE_ONLY if args.additive_only else 0) | getattr(_lib, PATHS[args.path][0])
     t = time.perf_counter()
     buf, pos = synth.device_bed(M, N, seed=7 + rank, length_cm=args.length_cm, device=local)
     eng = Engine(local)
@@ -171,20 +182,18 @@ def main():
         band_ms = float(np.mean([x["band_ms"] for x in tims]))
         flop = tims[-1]["flop_alg"]
         fp32_equiv = flop / (band_ms * 1e-3) / 1e12
-        exact = tims[-1]["exact_i8"]
-        if exact:
+        path = tims[-1]["path"]
+        _, peak, unit, kname, dtype = PATHS[path]
+        if path != "f32":
             ops = tims[-1]["ops_alg_i8"]
-            roof = {"bound": "mfma", "achieved": ops / (band_ms * 1e-3) / 1e12, "peak": I8_MFMA_PEAK_TOPS,
-                    "unit": "TOP/s", "kernel": "band_i8_kernel<true> (v_mfma_i32_32x32x32_i8, exact int32 Gram)",
-                    "ops_alg_per_launch": ops,
+            roof = {"bound": "mfma", "achieved": ops / (band_ms * 1e-3) / 1e12, "peak": peak, "unit": unit,
+                    "kernel": kname, "ops_alg_per_launch": ops,
                     "ops_alg_definition": "2N(4*(1/2)sumWSA + 2*sumWSD): 4 integer dots per unordered additive "
                                           "pair (xx,xo,ox,oo), 2 per ordered dominance pair (xh,oh)"}
-            peak = I8_MFMA_PEAK_TOPS
         else:
-            roof = {"bound": "mfma", "achieved": fp32_equiv, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "kernel": "band_kernel<true> (v_mfma_f32_32x32x2_f32)", "flop_alg_per_launch": flop}
-            peak = FP32_MFMA_PEAK_TFLOPS
-        traffic, traffic_src = pmc_traffic("band_i8_kernel" if exact else "band_kernel", N, M)
+            roof = {"bound": "mfma", "achieved": fp32_equiv, "peak": peak, "unit": unit,
+                    "kernel": kname, "flop_alg_per_launch": flop}
+        traffic, traffic_src = pmc_traffic(kname.split("<")[0], N, M)
         roof.update(frac=roof["achieved"] / peak, traffic=traffic, traffic_source=traffic_src,
                     algorithmic_bytes_per_launch=M * 4 * ((((N + 3) // 4) + 31) // 32 * 8),
                     avg_launch_ms=band_ms,
@@ -207,7 +216,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "i8" if exact else "f32",
+            "dtype": dtype,
             "data": "synthetic (GPU-generated PLINK .bed, AR(1) haplotypes, 1% missing; one chromosome per GPU)",
             "config": {
                 "workload": ("C3 (BASELINE.json configs[2]): chr1-like N=315599 individuals, M=%d SNPs over %.0f cM, "
@@ -252,7 +261,7 @@ def whole_genome(args, world, rank, local, coll):
     L = np.array(AUTOSOME_CM, dtype=float)
     Mc = np.maximum(1000, np.round(total * L / L.sum())).astype(int)
     mine = assign_units(list(Mc * 1.0), world)[rank]
-    flags = _lib.FLAG_EXACT_I8 if args.path == "i8" else _lib.FLAG_FP32
+    flags = getattr(_lib, PATHS[args.path][0])
     units = []
     t = time.perf_counter()
     for u in mine:
@@ -292,7 +301,7 @@ def whole_genome(args, world, rank, local, coll):
             "metric": METRIC, "value": float(pr.item()) / t_max, "unit": "SNP-pairs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * t_max / args.steps,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-            "dtype": "i8" if args.path == "i8" else "f32",
+            "dtype": PATHS[args.path][4],
             "data": "synthetic (GPU-generated PLINK .bed per autosome)",
             "config": {"workload": "C4 (BASELINE.json configs[3]): 22 autosomes, sum M=%d (M_c proportional to cM "
                                    "length), N=%d, --ld-wind-cm %g, additive+dominance, chromosome units over GPUs "

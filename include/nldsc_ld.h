@@ -43,7 +43,10 @@ extern "C" {
 #define NLDSC_FLAG_ADDITIVE_ONLY 2u      /* skip the dominance terms: l2d = NaN, l2d_ws = l2d_wse = -1 */
 #define NLDSC_FLAG_EXACT_I8 4u           /* correlations from exact integer Gram products (int8 MFMA) */
 #define NLDSC_FLAG_FP32 8u               /* correlations from fp32 standardised values (fp32 MFMA) */
-/* Neither EXACT_I8 nor FP32: the engine default, EXACT_I8 ($NLDSC_BAND_MODE = i8 | f32 overrides it). */
+#define NLDSC_FLAG_EXACT_F4 16u          /* exact integer Gram products on fp4 MFMAs (n_org < 2^22; larger
+                                            cohorts fall back to EXACT_I8) */
+/* None of EXACT_F4, EXACT_I8, FP32: the engine default, EXACT_F4 ($NLDSC_BAND_MODE = f4 | i8 | f32
+ * overrides it). */
 
 typedef struct nldsc_ld_params {
     const char* bedfile;      /* LDScoreParams::bedfile   (data.h:34) */
@@ -106,15 +109,17 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
  * (sum WSA) of the last run, and the band kernel's work-item count. */
 int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, double* flop_issued,
                          double* pairs, int32_t* n_band_items);
-/* Path of the last run: 1 = exact int8 Gram, 0 = fp32; *ops_alg_i8 = algorithmic int8 ops of the exact
- * formulation, 2N (2 sum WSA + 2 sum WSD). */
+/* Path of the last run: 2 = exact Gram on fp4 MFMAs, 1 = exact Gram on int8 MFMAs, 0 = fp32;
+ * *ops_alg_i8 = algorithmic ops of the exact formulation, 2N (2 sum WSA + 2 sum WSD). */
 int nldsc_engine_path(const nldsc_engine* e, int32_t* exact_i8, double* ops_alg_i8);
 
 /* Host-only plan of the band kernel (no GPU needed; the engine calls the same code):
  * replays the reference's sliding-window pointers (stream.h:131-155,182-197) from positions and
  * MAF-pass flags (flags[j] bit 0) into L/R (n_snp each; L = -1 for SNPs the reference does not
  * compute) and lists the work items (I, J0, nc, 0) covering every needed 32x32 block pair for the
- * owned range.  Returns the item count; when it exceeds `cap` (or items == NULL) nothing is written
+ * owned range (max_nc 1 or 2).  max_nc = 4 lists the skewed 2x2 tiles of the exact path instead:
+ * (I, J, mask, 0), bit w of mask scheduling block pair (I, J), (I, J+1), (I+1, J+1), (I+1, J+2)
+ * for w = 0..3.  Returns the item count; when it exceeds `cap` (or items == NULL) nothing is written
  * to `items` and the count is returned; < 0 on bad arguments. */
 int nldsc_plan_band(const double* positions, const uint8_t* flags, int32_t n_snp, double ld_wind, int32_t own_begin,
                     int32_t own_end, int32_t max_nc, int32_t* L, int32_t* R, int32_t* items, int32_t cap);

@@ -21,6 +21,7 @@ FLAG_STRICT_PLINK_ORDER = 1
 FLAG_ADDITIVE_ONLY = 2
 FLAG_EXACT_I8 = 4
 FLAG_FP32 = 8
+FLAG_EXACT_F4 = 16
 
 # every symbol include/nldsc_ld.h declares (tests check the library exports all of them)
 EXPORTED = (

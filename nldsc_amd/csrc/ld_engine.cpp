@@ -25,7 +25,8 @@
 namespace {
 
 constexpr int BLK = 32;             // SNPs per MFMA block
-constexpr int ROW_ALIGN_BYTES = 32; // one K-loop chunk of a 2-bit row (16 B per lane half)
+constexpr int CHUNK_BYTES = 32;     // one K-loop chunk of a 2-bit row (16 B per lane half)
+constexpr int ROW_ALIGN_BYTES = 64; // rows hold an even number of chunks (the fp4 loop takes two at a time)
 
 // Message of BedStreamReader::check_plink_magic_number (stream.h:88-102), verbatim.
 const char* kBadMagic =
@@ -98,9 +99,13 @@ struct nldsc_engine {
     int32_t n_band_items = 0;
     // tuning knobs (environment, read at engine creation): band kernel waves/SIMD, max column blocks
     int band_wps = 2, band_nc = 2;
-    bool last_i8 = false;  // path of the last run
+    int last_path = 0;     // path of the last run: 0 fp32, 1 exact int8, 2 exact fp4
     int band_i8_nc = 1;    // column blocks per exact-path item (NLDSC_BAND_I8_NC)
-    bool band_i8 = true;   // default correlation path: exact int8 Gram (NLDSC_BAND_MODE=i8|f32)
+    int band_mode = 2;     // default correlation path (NLDSC_BAND_MODE=f32|i8|f4): exact fp4
+                           // (int8 above N = 2^22)
+    bool band_tile = false;  // exact path on skewed 2x2 tiles sharing decoded strips (NLDSC_BAND_TILE)
+    bool xcd = true;         // XCD-contiguous workgroup -> item order (NLDSC_XCD=0 disables)
+    std::vector<int4> h_ones;
 
     ~nldsc_engine() {
         (void)hipSetDevice(device);
@@ -240,6 +245,29 @@ void plan_items(const double* pos, const uint8_t* flags, int M, double w, const 
     out.insert(out.end(), ones.begin(), ones.end());
 }
 
+// Skewed 2x2 tiles of the exact path (band_tile_kernel) from the single-block-pair items: pair
+// (a, b), a <= b, goes to tile I = a & ~1, J = I + 2 * ((b - a) >> 1), wave 2 (a - I) + ((b - a) & 1)
+// (waves: (I, J), (I, J+1), (I+1, J+1), (I+1, J+2)).  Each pair lands in exactly one tile slot.
+void plan_tiles(const std::vector<int4>& ones, int nblk, std::vector<int4>& out) {
+    std::vector<std::pair<int64_t, int>> key;
+    key.reserve(ones.size());
+    for (const int4& it : ones) {
+        const int a = it.x, b = it.y;
+        const int I = a & ~1, d = b - a;
+        key.emplace_back((int64_t)I * (nblk + 1) + (d >> 1), 1 << (2 * (a - I) + (d & 1)));
+    }
+    std::sort(key.begin(), key.end());
+    out.clear();
+    for (size_t k = 0; k < key.size();) {
+        int mask = 0;
+        size_t e = k;
+        for (; e < key.size() && key[e].first == key[k].first; ++e) mask |= key[e].second;
+        const int I = (int)(key[k].first / (nblk + 1)), t = (int)(key[k].first % (nblk + 1));
+        out.push_back(make_int4(I, I + 2 * t, mask, 0));
+        k = e;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -264,7 +292,10 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_BAND_WPS")) e->band_wps = std::atoi(v) == 1 ? 1 : 2;
     if (const char* v = std::getenv("NLDSC_BAND_NC")) e->band_nc = std::atoi(v) == 1 ? 1 : 2;
     if (const char* v = std::getenv("NLDSC_BAND_I8_NC")) e->band_i8_nc = std::atoi(v) == 2 ? 2 : 1;
-    if (const char* v = std::getenv("NLDSC_BAND_MODE")) e->band_i8 = std::strcmp(v, "f32") != 0;
+    if (const char* v = std::getenv("NLDSC_BAND_MODE"))
+        e->band_mode = std::strcmp(v, "f32") == 0 ? 0 : std::strcmp(v, "f4") == 0 ? 2 : 1;
+    if (const char* v = std::getenv("NLDSC_BAND_TILE")) e->band_tile = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_XCD")) e->xcd = std::atoi(v) != 0;
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     for (auto& ev : e->ev)
         if (he == hipSuccess) he = hipEventCreate(&ev);
@@ -393,15 +424,19 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         return set_err(err, errlen, NLDSC_E_ARG, "owned range [%d, %d) outside [0, %d)", own_begin, own_end, M);
     const bool dom = !(p->flags & NLDSC_FLAG_ADDITIVE_ONLY);
     const bool strict = (p->flags & NLDSC_FLAG_STRICT_PLINK_ORDER) != 0;
-    const bool use_i8 = (p->flags & NLDSC_FLAG_EXACT_I8) ? true : (p->flags & NLDSC_FLAG_FP32) ? false : e->band_i8;
-    const int max_nc = use_i8 ? e->band_i8_nc : e->band_nc;
+    int path = (p->flags & NLDSC_FLAG_EXACT_F4) ? 2 : (p->flags & NLDSC_FLAG_EXACT_I8) ? 1
+             : (p->flags & NLDSC_FLAG_FP32) ? 0 : e->band_mode;
+    if (path == 2 && N >= (1 << 22)) path = 1;  // fp32 accumulators are exact integers only below 2^24 >= 4N
+    const bool use_i8 = path != 0, use_f4 = path == 2;
+    const bool tiled = path == 1 && e->band_tile;
+    const int max_nc = (tiled || use_f4) ? 1 : use_i8 ? e->band_i8_nc : e->band_nc;
     HIPCHK(hipSetDevice(e->device));
     hipStream_t st = e->stream;
 
     const int nb = N / 4 + (N % 4 > 0);
     const int row_bytes = (nb + ROW_ALIGN_BYTES - 1) / ROW_ALIGN_BYTES * ROW_ALIGN_BYTES;
     const int pitch_words = row_bytes / 4;
-    const int n_it = row_bytes / ROW_ALIGN_BYTES;
+    const int n_it = row_bytes / CHUNK_BYTES;
     const int nblk = (M + BLK - 1) / BLK;
     const int Mpad = nblk * BLK;
     // last .bed byte: bit pairs that are individuals for the reference (high pairs first,
@@ -455,6 +490,14 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         if (it.x < 0 || it.y < it.x || (it.z != 1 && it.z != 2) || it.y + it.z > nblk)
             return set_err(err, errlen, NLDSC_E_ARG, "internal: bad work item (%d, %d, %d) for %d blocks", it.x,
                            it.y, it.z, nblk);
+    if (tiled) {
+        e->h_ones.swap(e->h_items);
+        plan_tiles(e->h_ones, nblk, e->h_items);
+        for (const int4& it : e->h_items)  // the tile kernel clamps strips past the last block itself
+            if (it.x < 0 || it.x >= nblk || it.y < it.x || it.y >= nblk || it.z <= 0 || it.z > 15)
+                return set_err(err, errlen, NLDSC_E_ARG, "internal: bad tile (%d, %d, %d) for %d blocks", it.x, it.y,
+                               it.z, nblk);
+    }
     HIPCHK(e->items.ensure(std::max<size_t>(e->h_items.size(), 1)));
     HIPCHK(hipMemcpyAsync(e->Lw.p, e->h_L.data(), sizeof(int) * M, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(e->Rw.p, e->h_R.data(), sizeof(int) * M, hipMemcpyHostToDevice, st));
@@ -469,7 +512,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     e->n_band_items = (int32_t)e->h_items.size();
     {
         double products = 0;  // 32x32 block products issued per sample slot
-        for (const int4& it : e->h_items) {
+        for (const int4& it : tiled ? e->h_ones : e->h_items) {
             const bool dg = it.x == it.y;
             if (use_i8)  // int8 Gram: xx, xo, ox, oo (+ xh, oh, and hx, ho off the diagonal) per column block
                 products += it.z * (dom ? 8.0 : 4.0) - ((dom && dg) ? 2.0 : 0.0);
@@ -479,18 +522,28 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         e->flop_issued = products * 2.0 * BLK * BLK * (double)row_bytes * 4.0;
     }
     if (!e->h_items.empty()) {
-        if (use_i8)
+        if (tiled)
+            HIPCHK(nldsc::launch_band_tile(dom, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, nblk, e->cst.p,
+                                           e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
+                                           (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
+                                           e->ws_acc.p, e->xcd, st));
+        else if (use_f4)
+            HIPCHK(nldsc::launch_band_f4(dom, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, e->cst.p,
+                                         e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
+                                         (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
+                                         e->ws_acc.p, e->xcd, st));
+        else if (use_i8)
             HIPCHK(nldsc::launch_band_i8(dom, max_nc, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, e->cst.p,
                                          e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
                                          (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
-                                         e->ws_acc.p, st));
+                                         e->ws_acc.p, e->xcd, st));
         else
             HIPCHK(nldsc::launch_band(dom, e->band_wps, (int)e->h_items.size(), e->geno.p, pitch_words, n_it,
                                       e->lut.p, e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
                                       (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                       e->ws_acc.p, st));
     }
-    e->last_i8 = use_i8;
+    e->last_path = path;
     HIPCHK(hipEventRecord(e->ev[4], st));
     HIPCHK(nldsc::launch_finalize(e->Lw.p, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, own_begin, own_end, dom,
                                   e->l2.p, e->l2d.p, e->ws3.p, st));
@@ -545,11 +598,16 @@ int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, d
 int nldsc_plan_band(const double* positions, const uint8_t* flags, int32_t n_snp, double ld_wind, int32_t own_begin,
                     int32_t own_end, int32_t max_nc, int32_t* L, int32_t* R, int32_t* items, int32_t cap) {
     if (!positions || !flags || !L || !R || n_snp <= 0 || own_begin < 0 || own_end > n_snp || own_begin > own_end ||
-        (max_nc != 1 && max_nc != 2))
+        (max_nc != 1 && max_nc != 2 && max_nc != 4))
         return NLDSC_E_ARG;
     replay_windows(positions, flags, n_snp, ld_wind, L, R);
     std::vector<int4> it;
-    plan_items(positions, flags, n_snp, ld_wind, L, R, own_begin, own_end, max_nc, it);
+    plan_items(positions, flags, n_snp, ld_wind, L, R, own_begin, own_end, max_nc == 4 ? 1 : max_nc, it);
+    if (max_nc == 4) {
+        std::vector<int4> ones;
+        ones.swap(it);
+        plan_tiles(ones, (n_snp + BLK - 1) / BLK, it);
+    }
     if ((int64_t)it.size() > (int64_t)cap || !items) return (int)std::min<size_t>(it.size(), INT32_MAX);
     for (size_t k = 0; k < it.size(); ++k) {
         items[4 * k] = it[k].x; items[4 * k + 1] = it[k].y; items[4 * k + 2] = it[k].z; items[4 * k + 3] = 0;
@@ -559,7 +617,7 @@ int nldsc_plan_band(const double* positions, const uint8_t* flags, int32_t n_snp
 
 int nldsc_engine_path(const nldsc_engine* e, int32_t* exact_i8, double* ops_alg_i8) {
     if (!e) return NLDSC_E_ARG;
-    if (exact_i8) *exact_i8 = e->last_i8 ? 1 : 0;
+    if (exact_i8) *exact_i8 = e->last_path;
     if (ops_alg_i8) *ops_alg_i8 = e->ops_alg_i8;
     return NLDSC_OK;
 }

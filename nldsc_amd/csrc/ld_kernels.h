@@ -24,7 +24,17 @@ hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int
 hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
-                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, hipStream_t st);
+                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st);
+// exact path on fp4 MFMAs (N < 2^22), single block-pair items (I, J, 1, 0)
+hipError_t launch_band_f4(bool dom, int n_items, const uint32_t* geno, int pitch_words, int n_it, const SnpConst* cst,
+                          const int4* items, const double* pos, const int* Lw, const int* Rw, const uint8_t* sflags,
+                          int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo, int own_hi,
+                          double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st);
+// skewed 2x2 tiles (I, J, mask) of the exact path, one 256-thread workgroup each
+hipError_t launch_band_tile(bool dom, int n_tiles, const uint32_t* geno, int pitch_words, int n_it, int nblk,
+                            const SnpConst* cst, const int4* tiles, const double* pos, const int* Lw, const int* Rw,
+                            const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
+                            int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st);
 hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2d_acc, const int* ws_acc, int n_snp,
                            int own_lo, int own_hi, bool dom, double* l2, double* l2d, int* ws3, hipStream_t st);
 hipError_t launch_synth_bed(uint8_t* rows, int n_snp, int n_org, int nb, const float* thr, float rho, float missing,

@@ -425,6 +425,65 @@ __device__ __forceinline__ void decode16(uint32_t w, i32x4& X, i32x4& H, i32x4& 
     }
 }
 
+// The dispatcher places workgroup b on XCD b % 8, each XCD with its own L2.  xcd_slot gives every
+// XCD a contiguous run of the (row-major) schedule instead, so the workgroups resident on one XCD
+// work on neighbouring blocks of the band and share their strips in that XCD's L2.
+__device__ __forceinline__ int xcd_slot(int b, int n) {
+    const int per = n >> 3, rem = n & 7, x = b & 7;
+    return x * per + min(x, rem) + (b >> 3);
+}
+
+// Epilogue of one 32x32 block pair (row slots rb.., column slots cb.. of the LDS slot tables):
+// standardised dots from the 8 integer Gram entries in fp64, r2adj, window/pointer masks, and
+// per-SNP sums (ldscalc.h:33-55).  diag: the pair is a diagonal block (row block == column block).
+template <bool DOM, class Acc>
+__device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpConst* cst, double* s_l2, double* s_l2d,
+                                              int* s_wsa, int* s_wsd, int* s_wse, int rb, int cb, bool diag, int i,
+                                              int h, const Acc& gxx, const Acc& gxo, const Acc& gox, const Acc& goo,
+                                              const Acc& gxh, const Acc& goh, const Acc& ghx, const Acc& gho,
+                                              double ld_wind, double n_org, double rsq_thr) {
+    const int sj = cb + i;
+    const SnpSlot cj = info[sj];
+    const SnpConst kj = cst[sj];
+    const bool pj = cj.fl & 1, rpj = (cj.fl & 2) != 0;
+    const bool compj = cj.L >= 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int si = rb + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const SnpSlot ci = info[si];
+        const bool pi = ci.fl & 1, rpi = (ci.fl & 2) != 0;
+        const bool inwin = fabs(cj.pos - ci.pos) <= ld_wind && ci.g != cj.g;
+        const bool nij = inwin && ci.L >= 0 && cj.g >= ci.L && cj.g <= ci.R && pj;
+        const bool nji = !diag && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
+        if (nij || nji) {
+            const SnpConst ki = cst[si];
+            const double xx = (double)gxx[r], xo = (double)gxo[r], ox = (double)gox[r], oo = (double)goo[r];
+            const double aa = (xx - kj.mu * xo - ki.mu * (ox - kj.mu * oo)) / (ki.sa * kj.sa);
+            const double r2 = r2_adjusted(aa, n_org);
+            if (nij) { atomicAdd(&s_l2[si], r2); atomicAdd(&s_wsa[si], 1); }
+            if (nji) { atomicAdd(&s_l2[sj], r2); atomicAdd(&s_wsa[sj], 1); }
+            if (DOM) {
+                if (nij && rpj) {  // A_i . R_j -> L2D_i (ldscalc.h:40-46)
+                    const double xh = (double)gxh[r], oh = (double)goh[r];
+                    const double ar = (2.0 * xh - kj.beta * xx - kj.c * xo -
+                                       ki.mu * (2.0 * oh - kj.beta * ox - kj.c * oo)) / (ki.sa * kj.s);
+                    const double rd = r2_adjusted(ar, n_org);
+                    atomicAdd(&s_l2d[si], rd); atomicAdd(&s_wsd[si], 1);
+                    if (rd > rsq_thr) atomicAdd(&s_wse[si], 1);
+                }
+                if (!diag && nji && rpi) {  // R_i . A_j -> L2D_j
+                    const double hx = (double)ghx[r], ho = (double)gho[r];
+                    const double ra = (2.0 * hx - ki.beta * xx - ki.c * ox -
+                                       kj.mu * (2.0 * ho - ki.beta * xo - ki.c * oo)) / (ki.s * kj.sa);
+                    const double rd = r2_adjusted(ra, n_org);
+                    atomicAdd(&s_l2d[sj], rd); atomicAdd(&s_wsd[sj], 1);
+                    if (rd > rsq_thr) atomicAdd(&s_wse[sj], 1);
+                }
+            }
+        }
+    }
+}
+
 struct BandI8Lds {
     SnpSlot info[NS_MAX];
     SnpConst cst[NS_MAX];
@@ -528,50 +587,9 @@ __device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const
 
     // ---- fused epilogue (fp64): standardised dots from the integer Gram, r2adj, masks, sums ----
 #pragma unroll
-    for (int b = 0; b < NC; ++b) {
-        const bool diag = DIAG0 && b == 0;
-        const int sj = 32 + 32 * b + i;
-        const SnpSlot cj = sh.info[sj];
-        const SnpConst kj = sh.cst[sj];
-        const bool pj = cj.fl & 1, rpj = (cj.fl & 2) != 0;
-        const bool compj = cj.L >= 0;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int si = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const SnpSlot ci = sh.info[si];
-            const bool pi = ci.fl & 1, rpi = (ci.fl & 2) != 0;
-            const bool inwin = fabs(cj.pos - ci.pos) <= ld_wind && ci.g != cj.g;
-            const bool nij = inwin && ci.L >= 0 && cj.g >= ci.L && cj.g <= ci.R && pj;
-            const bool nji = !diag && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
-            if (nij || nji) {
-                const SnpConst ki = sh.cst[si];
-                const double xx = (double)gxx[b][r], xo = (double)gxo[b][r], ox = (double)gox[b][r],
-                             oo = (double)goo[b][r];
-                const double aa = (xx - kj.mu * xo - ki.mu * (ox - kj.mu * oo)) / (ki.sa * kj.sa);
-                const double r2 = r2_adjusted(aa, n_org);
-                if (nij) { atomicAdd(&sh.l2[si], r2); atomicAdd(&sh.wsa[si], 1); }
-                if (nji) { atomicAdd(&sh.l2[sj], r2); atomicAdd(&sh.wsa[sj], 1); }
-                if (DOM) {
-                    if (nij && rpj) {  // A_i . R_j -> L2D_i (ldscalc.h:40-46)
-                        const double xh = (double)gxh[b][r], oh = (double)goh[b][r];
-                        const double ar = (2.0 * xh - kj.beta * xx - kj.c * xo -
-                                           ki.mu * (2.0 * oh - kj.beta * ox - kj.c * oo)) / (ki.sa * kj.s);
-                        const double rd = r2_adjusted(ar, n_org);
-                        atomicAdd(&sh.l2d[si], rd); atomicAdd(&sh.wsd[si], 1);
-                        if (rd > rsq_thr) atomicAdd(&sh.wse[si], 1);
-                    }
-                    if (!diag && nji && rpi) {  // R_i . A_j -> L2D_j
-                        const double hx = (double)ghx[b][r], ho = (double)gho[b][r];
-                        const double ra = (2.0 * hx - ki.beta * xx - ki.c * ox -
-                                           kj.mu * (2.0 * ho - ki.beta * xo - ki.c * oo)) / (ki.s * kj.sa);
-                        const double rd = r2_adjusted(ra, n_org);
-                        atomicAdd(&sh.l2d[sj], rd); atomicAdd(&sh.wsd[sj], 1);
-                        if (rd > rsq_thr) atomicAdd(&sh.wse[sj], 1);
-                    }
-                }
-            }
-        }
-    }
+    for (int b = 0; b < NC; ++b)
+        pair_epilogue<DOM>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * b, DIAG0 && b == 0, i,
+                           h, gxx[b], gxo[b], gox[b], goo[b], gxh[b], goh[b], ghx[b], gho[b], ld_wind, n_org, rsq_thr);
     __syncthreads();
     for (int s = lane; s < NS; s += 64) {
         const int g = sh.info[s].g;
@@ -596,9 +614,10 @@ __global__ void __launch_bounds__(64, WPS) band_i8_kernel(const uint32_t* __rest
                                                         const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
                                                         int n_snp, double ld_wind, double n_org, double rsq_thr,
                                                         int own_lo, int own_hi, double* __restrict__ l2_acc,
-                                                        double* __restrict__ l2d_acc, int* __restrict__ ws_acc) {
+                                                        double* __restrict__ l2d_acc, int* __restrict__ ws_acc,
+                                                        int xcd) {
     __shared__ BandI8Lds sh;
-    const int4 it = items[blockIdx.x];
+    const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
 #define NLDSC_BODY(NC_, DIAG_)                                                                                        \
     band_i8_body<DOM, NC_, DIAG_>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,  \
                                   rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc)
@@ -606,6 +625,309 @@ __global__ void __launch_bounds__(64, WPS) band_i8_kernel(const uint32_t* __rest
     if (WPS == 1 && it.z == 2) { if (diag) NLDSC_BODY(2, true); else NLDSC_BODY(2, false); }
     else { if (diag) NLDSC_BODY(1, true); else NLDSC_BODY(1, false); }
 #undef NLDSC_BODY
+}
+
+// ---- exact path on fp4 MFMAs: v_mfma_scale_f32_32x32x64_f8f6f4 with e2m1 operands ----
+// x in {0, 1, 2} and h, o in {0, 1} are exact e2m1 values (0000, 0010 = 1.0, 0100 = 2.0) and every
+// product is an integer in {0, 1, 2, 4}, so the fp32 accumulators hold exact integer Gram entries
+// as long as they stay below 2^24: entries are <= 4N, so the engine uses this path for N < 2^22.
+// One K step = 64 sample slots = two 16-code words per lane (twice the int8 step, same 32-cycle
+// MFMA), and the 2-bit -> 4-bit spread needs no shuffles because any fixed slot permutation is
+// fine: even code pairs go to the nibbles of one dword, odd pairs to another (11 VALU per word
+// against 27 for the int8 byte spread).
+typedef float f32x16v __attribute__((ext_vector_type(16)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+constexpr int E8M0_ONE = 127;  // block scale 2^0
+
+struct F4Frag {
+    i32x4 x, h, o;
+};
+
+__device__ __forceinline__ void decode_f4_word(uint32_t w, int& x0, int& x1, int& h0, int& h1, int& o0, int& o1) {
+    constexpr uint32_t M = 0x22222222u;  // bit 1 of every nibble
+    const uint32_t t0 = w << 1, w2 = w >> 2, t1 = w >> 1;  // lo of even pairs / hi, lo of odd pairs -> bit 1
+    h0 = (int)(w & M);
+    o0 = (int)((w | ~t0) & M);             // 01 (missing / padding) -> 0
+    x0 = (int)((w & M) + (w & t0 & M));    // 10 -> 0010 (1.0), 11 -> 0100 (2.0)
+    h1 = (int)(w2 & M);
+    o1 = (int)((w2 | ~t1) & M);
+    x1 = (int)((w2 & M) + (w2 & t1 & M));
+}
+
+__device__ __forceinline__ F4Frag decode_f4(uint32_t wa, uint32_t wb) {
+    int x0, x1, x2, x3, h0, h1, h2, h3, o0, o1, o2, o3;
+    decode_f4_word(wa, x0, x1, h0, h1, o0, o1);
+    decode_f4_word(wb, x2, x3, h2, h3, o2, o3);
+    F4Frag f;
+    f.x = i32x4{x0, x1, x2, x3};
+    f.h = i32x4{h0, h1, h2, h3};
+    f.o = i32x4{o0, o1, o2, o3};
+    return f;
+}
+
+__device__ __forceinline__ f32x16v mfma_f4(const i32x4& a, const i32x4& b, const f32x16v& c) {
+    const i32x8 A = {a[0], a[1], a[2], a[3], 0, 0, 0, 0}, B = {b[0], b[1], b[2], b[3], 0, 0, 0, 0};
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, c, 4, 4, 0, E8M0_ONE, 0, E8M0_ONE);
+}
+
+template <bool DOM, bool DIAG0>
+__device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const uint32_t* __restrict__ geno,
+                                             int pitch_words, int n_it, const SnpConst* __restrict__ cst,
+                                             const double* __restrict__ pos, const int* __restrict__ Lw,
+                                             const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
+                                             int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
+                                             int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
+                                             int* __restrict__ ws_acc) {
+    constexpr int NS = 64;
+    const int lane = threadIdx.x;
+    const int i = lane & 31, h = lane >> 5;
+    const int I = it.x, J0 = it.y;
+    for (int s = lane; s < NS; s += 64) {
+        const int g = s < 32 ? I * 32 + s : J0 * 32 + (s & 31);
+        SnpSlot si;
+        si.g = g;
+        if (g < n_snp) {
+            si.pos = pos[g]; si.L = Lw[g]; si.R = Rw[g]; si.fl = sflags[g];
+        } else {
+            si.pos = 0.0; si.L = -1; si.R = -2; si.fl = 0;
+        }
+        sh.info[s] = si;
+        sh.cst[s] = cst[g];
+        sh.l2[s] = 0.0; sh.l2d[s] = 0.0;
+        sh.wsa[s] = 0; sh.wsd[s] = 0; sh.wse[s] = 0;
+    }
+    __syncthreads();
+
+    f32x16v gxx{}, gxo{}, gox{}, goo{}, gxh{}, goh{}, ghx{}, gho{};
+    const uint4* rowp = reinterpret_cast<const uint4*>(geno + (size_t)(I * 32 + i) * (size_t)pitch_words) + h;
+    const uint4* colp = reinterpret_cast<const uint4*>(geno + (size_t)(J0 * 32 + i) * (size_t)pitch_words) + h;
+    // n_it is even (rows are padded to 64 bytes).  Two chunk buffers: P holds even chunks, Q odd
+    // ones; each is reloaded right after its last word is decoded and read again three K steps
+    // later, with no register copies of loads in flight (those would force vmcnt(0)).
+    const int last = n_it - 1;
+    uint4 pr = rowp[0], pc = colp[0], qr = rowp[2], qc = colp[2];
+    // operands of the current K step; the next step's are decoded while these feed the MFMAs
+    F4Frag a = decode_f4(pr.x, pr.y), b = decode_f4(pc.x, pc.y);
+    auto step = [&](const F4Frag& an, const F4Frag& bn) {
+        gxx = mfma_f4(a.x, b.x, gxx);
+        gxo = mfma_f4(a.x, b.o, gxo);
+        gox = mfma_f4(a.o, b.x, gox);
+        goo = mfma_f4(a.o, b.o, goo);
+        if (DOM) {
+            gxh = mfma_f4(a.x, b.h, gxh);
+            goh = mfma_f4(a.o, b.h, goh);
+            if (!DIAG0) {  // on a diagonal block R_i . A_j is the transposed A_j . R_i
+                ghx = mfma_f4(a.h, b.x, ghx);
+                gho = mfma_f4(a.h, b.o, gho);
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+        }
+        a = an;
+        b = bn;
+    };
+    for (int t = 0; t < n_it; t += 2) {
+        step(decode_f4(pr.z, pr.w), decode_f4(pc.z, pc.w));  // K step 2t   (chunk t, words 0-1)
+        pr = rowp[2 * min(t + 2, last)];
+        pc = colp[2 * min(t + 2, last)];
+        step(decode_f4(qr.x, qr.y), decode_f4(qc.x, qc.y));  // K step 2t+1 (chunk t, words 2-3)
+        step(decode_f4(qr.z, qr.w), decode_f4(qc.z, qc.w));  // K step 2t+2 (chunk t+1, words 0-1)
+        qr = rowp[2 * min(t + 3, last)];
+        qc = colp[2 * min(t + 3, last)];
+        step(decode_f4(pr.x, pr.y), decode_f4(pc.x, pc.y));  // K step 2t+3 (chunk t+1, words 2-3)
+    }
+    pair_epilogue<DOM>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32, DIAG0, i, h, gxx, gxo, gox, goo,
+                       gxh, goh, ghx, gho, ld_wind, n_org, rsq_thr);
+    __syncthreads();
+    for (int s = lane; s < NS; s += 64) {
+        const int g = sh.info[s].g;
+        if (g < own_lo || g >= own_hi || g >= n_snp) continue;
+        if (sh.wsa[s]) {
+            unsafeAtomicAdd(&l2_acc[g], sh.l2[s]);
+            atomicAdd(&ws_acc[g], sh.wsa[s]);
+        }
+        if (DOM && sh.wsd[s]) {
+            unsafeAtomicAdd(&l2d_acc[g], sh.l2d[s]);
+            atomicAdd(&ws_acc[(size_t)n_snp + g], sh.wsd[s]);
+            if (sh.wse[s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + g], sh.wse[s]);
+        }
+    }
+}
+
+template <bool DOM>
+__global__ void __launch_bounds__(64, 2) band_f4_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
+                                                      const SnpConst* __restrict__ cst, const int4* __restrict__ items,
+                                                      const double* __restrict__ pos, const int* __restrict__ Lw,
+                                                      const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
+                                                      int n_snp, double ld_wind, double n_org, double rsq_thr,
+                                                      int own_lo, int own_hi, double* __restrict__ l2_acc,
+                                                      double* __restrict__ l2d_acc, int* __restrict__ ws_acc, int xcd) {
+    __shared__ BandI8Lds sh;
+    const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
+    if (it.y == it.x)
+        band_f4_body<DOM, true>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,
+                                rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc);
+    else
+        band_f4_body<DOM, false>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,
+                                 rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc);
+}
+
+// ---- skewed 2x2 tiles: the four waves of a workgroup share every decoded strip through LDS ----
+// Tile (I, J, mask): wave 0 -> block pair (I, J), 1 -> (I, J+1), 2 -> (I+1, J+1), 3 -> (I+1, J+2);
+// bit w of mask = wave w's pair is scheduled.  The shape follows the band (row I+1's columns are
+// row I's shifted by one block): on the C3 geometry 94.5% of the slots are needed pairs, and the
+// five strips R0=I, R1=I+1, C0=J, C1=J+1, C2=J+2 are decoded ONCE per K step for four MFMA waves
+// (1.25 words per thread and step instead of 2, and each strip fetched once per tile).
+// Thread (w, lane) decodes strip w (R0, R1, C0, C1) for its own MFMA lane slot; strip C2 is split
+// by K step: wave w decodes its word q == w of every 4-step chunk.
+constexpr int TS = 5;  // strips per tile
+
+struct TileLds {
+    i32x4 ring[2][TS][3][64];  // [K step & 1][strip][x, h, o][lane]: decoded MFMA operands
+    SnpSlot info[TS * 32];
+    SnpConst cst[TS * 32];
+    double l2[TS * 32], l2d[TS * 32];
+    int wsa[TS * 32], wsd[TS * 32], wse[TS * 32];
+};
+
+// workgroup barrier that orders LDS only (no wait on the global prefetch in flight)
+__device__ __forceinline__ void tile_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ void tile_put(TileLds& sh, bool dom, int slot, int strip, int lane, uint32_t word) {
+    i32x4 X, H, O;
+    decode16(word, X, H, O);
+    sh.ring[slot][strip][0][lane] = X;
+    if (dom) sh.ring[slot][strip][1][lane] = H;
+    sh.ring[slot][strip][2][lane] = O;
+}
+
+// K loop of one wave.  Step k's operands live in ring slot k & 1: written (decoded) during step
+// k - 2, read into registers during step k - 1, consumed by the MFMAs of step k; one barrier per
+// step.  MODE 0: full pair, 1: diagonal pair (R_i . A_j skipped), 2: unscheduled pair (this wave
+// only decodes for the others).
+template <bool DOM, int MODE>
+__device__ __forceinline__ void tile_kloop(TileLds& sh, int w, int lane, int rs, int cs, const uint4* __restrict__ own_p,
+                                           const uint32_t* __restrict__ c2_p, int n_it, i32x16 (&g)[8]) {
+    auto ld4 = [&](int t) { return own_p[2 * min(t, n_it - 1)]; };
+    auto ld1 = [&](int t) { return c2_p[8 * min(t, n_it - 1)]; };
+    uint4 g0 = ld4(0), g1 = ld4(1), g2 = ld4(2);
+    uint32_t c0 = ld1(0), c1 = ld1(1), c2 = ld1(2);
+    i32x4 Xi{}, Hi{}, Oi{}, Xj{}, Hj{}, Oj{};
+    // prologue: step 0 into slot 0, read it; step 1 into slot 1
+    tile_put(sh, DOM, 0, w, lane, g0.x);
+    if (w == 0) tile_put(sh, DOM, 0, 4, lane, c0);
+    tile_sync();
+    if (MODE != 2) {
+        Xi = sh.ring[0][rs][0][lane]; Oi = sh.ring[0][rs][2][lane];
+        Xj = sh.ring[0][cs][0][lane]; Oj = sh.ring[0][cs][2][lane];
+        if (DOM) { Hi = sh.ring[0][rs][1][lane]; Hj = sh.ring[0][cs][1][lane]; }
+    }
+    tile_put(sh, DOM, 1, w, lane, g0.y);
+    if (w == 1) tile_put(sh, DOM, 1, 4, lane, c0);
+    tile_sync();
+    for (int t = 0; t < n_it; ++t) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int cur = q & 1, nxt = cur ^ 1;
+            i32x4 Xin{}, Hin{}, Oin{}, Xjn{}, Hjn{}, Ojn{};
+            if (MODE != 2) {  // step k+1's operands (its slot was completed before the last barrier)
+                Xin = sh.ring[nxt][rs][0][lane]; Oin = sh.ring[nxt][rs][2][lane];
+                Xjn = sh.ring[nxt][cs][0][lane]; Ojn = sh.ring[nxt][cs][2][lane];
+                if (DOM) { Hin = sh.ring[nxt][rs][1][lane]; Hjn = sh.ring[nxt][cs][1][lane]; }
+            }
+            {  // decode step k+2 into the slot step k's operands were read from (steps K, K+1 are
+               // decoded from the clamped last chunk into slots nobody reads)
+                const uint32_t wd = q == 0 ? g0.z : q == 1 ? g0.w : q == 2 ? g1.x : g1.y;
+                tile_put(sh, DOM, cur, w, lane, wd);
+                if (w == ((q + 2) & 3)) tile_put(sh, DOM, cur, 4, lane, q < 2 ? c0 : c1);
+            }
+            if (MODE != 2) {
+                g[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Xj, g[0], 0, 0, 0);
+                g[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Oj, g[1], 0, 0, 0);
+                g[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Xj, g[2], 0, 0, 0);
+                g[3] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Oj, g[3], 0, 0, 0);
+                if (DOM) {
+                    g[4] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Hj, g[4], 0, 0, 0);
+                    g[5] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Hj, g[5], 0, 0, 0);
+                    if (MODE == 0) {
+                        g[6] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Hi, Xj, g[6], 0, 0, 0);
+                        g[7] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Hi, Oj, g[7], 0, 0, 0);
+                    }
+                }
+            }
+            tile_sync();
+            if (MODE != 2) {
+                Xi = Xin; Hi = Hin; Oi = Oin; Xj = Xjn; Hj = Hjn; Oj = Ojn;
+            }
+        }
+        g0 = g1; g1 = g2; g2 = ld4(t + 3);
+        c0 = c1; c1 = c2; c2 = ld1(t + 3);
+    }
+}
+
+template <bool DOM>
+__global__ void __launch_bounds__(256, 2) band_tile_kernel(
+    const uint32_t* __restrict__ geno, int pitch_words, int n_it, const SnpConst* __restrict__ cst,
+    const int4* __restrict__ items, const double* __restrict__ pos, const int* __restrict__ Lw,
+    const int* __restrict__ Rw, const uint8_t* __restrict__ sflags, int n_snp, int nblk, double ld_wind, double n_org,
+    double rsq_thr, int own_lo, int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
+    int* __restrict__ ws_acc, int xcd) {
+    __shared__ TileLds sh;
+    const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
+    const int i = lane & 31, h = lane >> 5;
+    const int I = it.x, J = it.y, mask = it.z;
+    // strip s -> block (strips past the last block are clamped; their pairs are never scheduled)
+    auto strip_blk = [&](int s) { return min(s < 2 ? I + s : J + s - 2, nblk - 1); };
+    for (int s = tid; s < TS * 32; s += 256) {
+        const int g = strip_blk(s >> 5) * 32 + (s & 31);
+        SnpSlot si;
+        si.g = g;
+        if (g < n_snp) {
+            si.pos = pos[g]; si.L = Lw[g]; si.R = Rw[g]; si.fl = sflags[g];
+        } else {
+            si.pos = 0.0; si.L = -1; si.R = -2; si.fl = 0;
+        }
+        sh.info[s] = si;
+        sh.cst[s] = cst[g];
+        sh.l2[s] = 0.0; sh.l2d[s] = 0.0;
+        sh.wsa[s] = 0; sh.wsd[s] = 0; sh.wse[s] = 0;
+    }
+    const int rs = w >> 1, cs = 2 + (w & 1) + rs;  // this wave's row strip and column strip
+    const uint4* own_p = reinterpret_cast<const uint4*>(geno + (size_t)(strip_blk(w) * 32 + i) * pitch_words) + h;
+    const uint32_t* c2_p = geno + (size_t)(strip_blk(4) * 32 + i) * pitch_words + 4 * h + w;
+    i32x16 g[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) g[b] = i32x16{};
+    const bool active = (mask >> w) & 1, diag = J == I && !(w & 1);
+    if (!active) tile_kloop<DOM, 2>(sh, w, lane, rs, cs, own_p, c2_p, n_it, g);
+    else if (diag) tile_kloop<DOM, 1>(sh, w, lane, rs, cs, own_p, c2_p, n_it, g);
+    else tile_kloop<DOM, 0>(sh, w, lane, rs, cs, own_p, c2_p, n_it, g);
+    if (active)
+        pair_epilogue<DOM>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, rs * 32, cs * 32, diag, i, h, g[0],
+                           g[1], g[2], g[3], g[4], g[5], g[6], g[7], ld_wind, n_org, rsq_thr);
+    __syncthreads();
+    for (int s = tid; s < TS * 32; s += 256) {
+        const int gg = sh.info[s].g;
+        if (gg < own_lo || gg >= own_hi || gg >= n_snp) continue;
+        if (sh.wsa[s]) {
+            unsafeAtomicAdd(&l2_acc[gg], sh.l2[s]);
+            atomicAdd(&ws_acc[gg], sh.wsa[s]);
+        }
+        if (DOM && sh.wsd[s]) {
+            unsafeAtomicAdd(&l2d_acc[gg], sh.l2d[s]);
+            atomicAdd(&ws_acc[(size_t)n_snp + gg], sh.wsd[s]);
+            if (sh.wse[s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + gg], sh.wse[s]);
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -726,14 +1048,42 @@ hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int
 hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
-                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, hipStream_t st) {
+                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st) {
     if (n_items <= 0) return hipSuccess;
 #define NLDSC_BAND(DOM_, WPS_)                                                                                      \
     hipLaunchKernelGGL((band_i8_kernel<DOM_, WPS_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, cst,   \
                        items, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, \
-                       ws_acc)
+                       ws_acc, xcd ? 1 : 0)
     if (dom) { if (max_nc == 2) NLDSC_BAND(true, 1); else NLDSC_BAND(true, 2); }
     else { if (max_nc == 2) NLDSC_BAND(false, 1); else NLDSC_BAND(false, 2); }
+#undef NLDSC_BAND
+    return hipGetLastError();
+}
+
+hipError_t launch_band_f4(bool dom, int n_items, const uint32_t* geno, int pitch_words, int n_it, const SnpConst* cst,
+                          const int4* items, const double* pos, const int* Lw, const int* Rw, const uint8_t* sflags,
+                          int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo, int own_hi,
+                          double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st) {
+    if (n_items <= 0) return hipSuccess;
+#define NLDSC_BAND(DOM_)                                                                                            \
+    hipLaunchKernelGGL((band_f4_kernel<DOM_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, cst, items,    \
+                       pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, \
+                       xcd ? 1 : 0)
+    if (dom) NLDSC_BAND(true); else NLDSC_BAND(false);
+#undef NLDSC_BAND
+    return hipGetLastError();
+}
+
+hipError_t launch_band_tile(bool dom, int n_tiles, const uint32_t* geno, int pitch_words, int n_it, int nblk,
+                            const SnpConst* cst, const int4* tiles, const double* pos, const int* Lw, const int* Rw,
+                            const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
+                            int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st) {
+    if (n_tiles <= 0) return hipSuccess;
+#define NLDSC_BAND(DOM_)                                                                                            \
+    hipLaunchKernelGGL((band_tile_kernel<DOM_>), dim3(n_tiles), dim3(256), 0, st, geno, pitch_words, n_it, cst, tiles, \
+                       pos, Lw, Rw, sflags, n_snp, nblk, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc,   \
+                       ws_acc, xcd ? 1 : 0)
+    if (dom) NLDSC_BAND(true); else NLDSC_BAND(false);
 #undef NLDSC_BAND
     return hipGetLastError();
 }

@@ -128,4 +128,7 @@ PYBIND11_MODULE(_ldscore, m) {
     m.attr("__version__") = nldsc_version();
     m.attr("FLAG_STRICT_PLINK_ORDER") = NLDSC_FLAG_STRICT_PLINK_ORDER;
     m.attr("FLAG_ADDITIVE_ONLY") = NLDSC_FLAG_ADDITIVE_ONLY;
+    m.attr("FLAG_EXACT_I8") = NLDSC_FLAG_EXACT_I8;
+    m.attr("FLAG_FP32") = NLDSC_FLAG_FP32;
+    m.attr("FLAG_EXACT_F4") = NLDSC_FLAG_EXACT_F4;
 }

@@ -36,7 +36,8 @@ def run_set(engine, name, flags=0, own=None):
     return got, meta, orc, f64, pos, bed
 
 
-MODES = {"f32": 8, "i8": 4}  # _lib.FLAG_FP32, _lib.FLAG_EXACT_I8
+MODES = {"f32": 8, "i8": 4, "f4": 16}  # _lib.FLAG_FP32, _lib.FLAG_EXACT_I8, _lib.FLAG_EXACT_F4
+EXACT = ("i8", "f4")  # integer Gram paths: exact up to the fp64 epilogue
 
 
 @pytest.mark.parametrize("mode", sorted(MODES))
@@ -170,7 +171,7 @@ def test_random_small_configs_vs_f64(engine, seed, mode):
     got = engine.run(w, maf, std_thr, rsq, pos, flags=MODES[mode])
     exp = O.run_f64(rows, N, w, maf, std_thr, rsq, pos)
     tol = dict(l2=(1e-4, 1e-5), l2d=(1e-5, 1e-5), residuals_std=(1e-12, 1e-10), maf=(0.0, 0.0))
-    if mode == "i8":
+    if mode in EXACT:
         tol.update(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12))
     assert_ld_close(got, exp, tol=tol, wse_budget=0.02, label=f"seed{seed} N{N} M{M}")
 
@@ -194,7 +195,7 @@ def test_full_size_spot_check_vs_oracle(engine, mode):
     record(f"full_size_{mode}", dict(n_org=N, n_snp=M, targets=t.tolist(), gpu_vs_oracle=max_errors(sub, exp),
                              gpu_vs_truth=max_errors(sub, truth), oracle_vs_truth=max_errors(exp, truth)))
     assert_ld_close(sub, truth, label="N=315599 vs fp64 truth")
-    if mode == "i8":
+    if mode in EXACT:
         for k in ("l2", "l2d"):
             assert np.max(np.abs(sub[k] - truth[k])) < 1e-8, k
     assert_ld_close(sub, exp, label="N=315599")
@@ -204,3 +205,37 @@ def test_full_size_spot_check_vs_oracle(engine, mode):
     np.testing.assert_array_equal(again["l2_ws"], got["l2_ws"])
     np.testing.assert_array_equal(again["l2d_wse"], got["l2d_wse"])
     np.testing.assert_allclose(again["l2"], got["l2"], rtol=1e-13)
+
+
+def test_f4_gram_is_bitwise_the_int8_gram(engine):
+    """The fp4 path's fp32 accumulators hold the same exact integers as the int8 path's int32 ones
+    (N < 2^22), and the fp64 epilogue is the same code: integer outputs, MAF and residual std are
+    identical, and L2 / L2D differ only by the order of the fp64 atomic sums (two runs of one path
+    differ the same way; one wrong Gram entry would move r2 by ~1e-6) — at N = 315 599 and on ragged
+    small cases (tiny K, padding slots, missing calls)."""
+    from nldsc_amd import synth
+    N, M = 315_599, 1200
+    buf, pos = synth.device_bed(M, N, seed=5, length_cm=4.0)
+    engine.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
+    args = (1.0, 1e-4, 1e-5, 1.0 / M, pos)
+    a, b = engine.run(*args, flags=MODES["i8"]), engine.run(*args, flags=MODES["f4"])
+    assert engine.timings()["path"] == "f4"
+    same_gram(a, b, "N=315599")
+    rng = np.random.default_rng(77)
+    for N in (3, 5, 64, 129, 1001):
+        M = int(rng.integers(40, 200))
+        spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=3.0, seed=N, missing=0.05)
+        rows = synth.pack_bed_rows(synth.genotypes(spec))
+        pos = synth.positions_cm(spec)
+        engine.load_bed_bytes(synth.bed_bytes(rows), M, N)
+        args = (1.0, 0.0, 0.0, 0.01, pos)
+        a, b = engine.run(*args, flags=MODES["i8"]), engine.run(*args, flags=MODES["f4"])
+        same_gram(a, b, f"N={N}")
+
+
+def same_gram(a, b, label):
+    for k in ("maf", "residuals_std", "l2_ws", "l2d_ws", "l2d_wse"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=f"{label} {k}")
+    for k in ("l2", "l2d"):
+        np.testing.assert_array_equal(np.isnan(a[k]), np.isnan(b[k]), err_msg=f"{label} {k}")
+        np.testing.assert_allclose(a[k], b[k], rtol=1e-13, atol=1e-14, equal_nan=True, err_msg=f"{label} {k}")
