@@ -42,9 +42,9 @@ PATHS = {
 
 def pmc_traffic(kernel_key: str, n_org: int, n_snp: int):
     """HBM-side bytes per launch of `kernel_key` from the newest committed rocprofv3 PMC summary
-    (profiles/*_pmc.json, measured on the same C3 workload), or None."""
+    (profiles/*_pmc*.json, measured on the same C3 workload), or None."""
     import glob
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc*.json")), reverse=True):
         try:
             doc = json.load(open(path))
         except (OSError, ValueError):

@@ -83,14 +83,14 @@ struct nldsc_engine {
     int32_t n_snp = 0, n_org = 0;
     // work buffers
     DevBuf<uint32_t> geno;
-    DevBuf<int> counts, Lw, Rw, ws_acc, ws3;
+    DevBuf<int> counts, Lw, Rw, Aw, ws_acc, ws3;
     DevBuf<float2> lut;
     DevBuf<nldsc::SnpConst> cst;
     DevBuf<uint8_t> sflags;
     DevBuf<double> pos, maf, rstd, l2_acc, l2d_acc, l2, l2d;
     DevBuf<int4> items;
     // host scratch
-    std::vector<uint8_t> h_flags;
+    std::vector<uint8_t> h_flags, h_all_pass;
     std::vector<int> h_L, h_R;
     std::vector<int4> h_items;
     // timings of the last run
@@ -100,7 +100,8 @@ struct nldsc_engine {
     // tuning knobs (environment, read at engine creation): band kernel waves/SIMD, max column blocks
     int band_wps = 2, band_nc = 2;
     int last_path = 0;     // path of the last run: 0 fp32, 1 exact int8, 2 exact fp4
-    int band_i8_nc = 1;    // column blocks per exact-path item (NLDSC_BAND_I8_NC)
+    int band_i8_nc = 1;    // column blocks per int8-path item (NLDSC_BAND_I8_NC)
+    int band_f4_nc = 1;    // column blocks per fp4-path item (NLDSC_BAND_F4_NC)
     int band_mode = 2;     // default correlation path (NLDSC_BAND_MODE=f32|i8|f4): exact fp4
                            // (int8 above N = 2^22)
     bool band_tile = false;  // exact path on skewed 2x2 tiles sharing decoded strips (NLDSC_BAND_TILE)
@@ -109,7 +110,7 @@ struct nldsc_engine {
 
     ~nldsc_engine() {
         (void)hipSetDevice(device);
-        bed.release(); geno.release(); counts.release(); Lw.release(); Rw.release(); ws_acc.release();
+        bed.release(); geno.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
         ws3.release(); lut.release(); cst.release(); sflags.release(); pos.release(); maf.release(); rstd.release();
         l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
@@ -173,6 +174,17 @@ void replay_windows(const double* pos, const uint8_t* flags, int n, double w, in
         L[j] = left;
         R[j] = right;
     }
+}
+
+// Positions non-decreasing over the used SNPs (pos >= 0)?
+bool positions_sorted(const double* pos, int M) {
+    double last = -1.0;
+    for (int j = 0; j < M; ++j)
+        if (pos[j] >= 0) {
+            if (pos[j] < last) return false;
+            last = pos[j];
+        }
+    return true;
 }
 
 // Tile schedule of the band kernel.  A block pair (I <= J) is needed when it holds a pair (i < j)
@@ -292,6 +304,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_BAND_WPS")) e->band_wps = std::atoi(v) == 1 ? 1 : 2;
     if (const char* v = std::getenv("NLDSC_BAND_NC")) e->band_nc = std::atoi(v) == 1 ? 1 : 2;
     if (const char* v = std::getenv("NLDSC_BAND_I8_NC")) e->band_i8_nc = std::atoi(v) == 2 ? 2 : 1;
+    if (const char* v = std::getenv("NLDSC_BAND_F4_NC")) e->band_f4_nc = std::atoi(v) == 2 ? 2 : 1;
     if (const char* v = std::getenv("NLDSC_BAND_MODE"))
         e->band_mode = std::strcmp(v, "f32") == 0 ? 0 : std::strcmp(v, "f4") == 0 ? 2 : 1;
     if (const char* v = std::getenv("NLDSC_BAND_TILE")) e->band_tile = std::atoi(v) != 0;
@@ -429,7 +442,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     if (path == 2 && N >= (1 << 22)) path = 1;  // fp32 accumulators are exact integers only below 2^24 >= 4N
     const bool use_i8 = path != 0, use_f4 = path == 2;
     const bool tiled = path == 1 && e->band_tile;
-    const int max_nc = (tiled || use_f4) ? 1 : use_i8 ? e->band_i8_nc : e->band_nc;
+    const int max_nc = tiled ? 1 : use_f4 ? e->band_f4_nc : use_i8 ? e->band_i8_nc : e->band_nc;
     HIPCHK(hipSetDevice(e->device));
     hipStream_t st = e->stream;
 
@@ -472,17 +485,31 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
                                    e->sflags.p, e->maf.p, e->rstd.p, st));
     HIPCHK(hipEventRecord(e->ev[2], st));
 
-    // ---- window replay + schedule on the host (needs the MAF-pass flags) ----
+    // ---- window replay + schedule ----
     auto t_host0 = std::chrono::steady_clock::now();
-    e->h_flags.resize(Mpad);
-    HIPCHK(hipMemcpyAsync(e->h_flags.data(), e->sflags.p, Mpad, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
     e->h_L.resize(M);
     e->h_R.resize(M);
-    replay_windows(p->positions, e->h_flags.data(), M, p->ld_wind, e->h_L.data(), e->h_R.data());
-
-    plan_items(p->positions, e->h_flags.data(), M, p->ld_wind, e->h_L.data(), e->h_R.data(), own_begin, own_end,
-               max_nc, e->h_items);
+    const bool sorted = positions_sorted(p->positions, M);
+    if (sorted) {
+        // Sorted positions: nothing waits for the GPU.  The right pointers and the all-pass left
+        // pointers do not depend on the MAF flags, and SNPs failing MAF only shrink the set of needed
+        // block pairs (their L_j grow, their rows and columns drop), so the all-pass schedule is a
+        // superset of the exact one; it is planned here while the GPU repacks, and the exact left
+        // pointers come from the device flags (left_pointer_kernel).  The kernels mask every pair
+        // with the exact pointers.
+        e->h_all_pass.assign(M, 1);
+        replay_windows(p->positions, e->h_all_pass.data(), M, p->ld_wind, e->h_L.data(), e->h_R.data());
+        plan_items(p->positions, e->h_all_pass.data(), M, p->ld_wind, e->h_L.data(), e->h_R.data(), own_begin,
+                   own_end, max_nc, e->h_items);
+    } else {
+        // unsorted positions: the reference's sequential pointer semantics need the MAF flags first
+        e->h_flags.resize(Mpad);
+        HIPCHK(hipMemcpyAsync(e->h_flags.data(), e->sflags.p, Mpad, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        replay_windows(p->positions, e->h_flags.data(), M, p->ld_wind, e->h_L.data(), e->h_R.data());
+        plan_items(p->positions, e->h_flags.data(), M, p->ld_wind, e->h_L.data(), e->h_R.data(), own_begin, own_end,
+                   max_nc, e->h_items);
+    }
     // the band kernel reads rows [32 I, 32 (J0 + nc)) of geno / lut: check before launching
     if (pitch_words % 8 != 0 || n_it * 8 != pitch_words)
         return set_err(err, errlen, NLDSC_E_ARG, "internal: bad row pitch %d", pitch_words);
@@ -499,7 +526,13 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
                                it.z, nblk);
     }
     HIPCHK(e->items.ensure(std::max<size_t>(e->h_items.size(), 1)));
-    HIPCHK(hipMemcpyAsync(e->Lw.p, e->h_L.data(), sizeof(int) * M, hipMemcpyHostToDevice, st));
+    if (sorted) {
+        HIPCHK(e->Aw.ensure((size_t)M));
+        HIPCHK(hipMemcpyAsync(e->Aw.p, e->h_L.data(), sizeof(int) * M, hipMemcpyHostToDevice, st));
+        HIPCHK(nldsc::launch_left_pointers(e->Aw.p, e->sflags.p, e->pos.p, M, e->Lw.p, st));
+    } else {
+        HIPCHK(hipMemcpyAsync(e->Lw.p, e->h_L.data(), sizeof(int) * M, hipMemcpyHostToDevice, st));
+    }
     HIPCHK(hipMemcpyAsync(e->Rw.p, e->h_R.data(), sizeof(int) * M, hipMemcpyHostToDevice, st));
     if (!e->h_items.empty())
         HIPCHK(hipMemcpyAsync(e->items.p, e->h_items.data(), sizeof(int4) * e->h_items.size(), hipMemcpyHostToDevice, st));
@@ -528,7 +561,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
                                            (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                            e->ws_acc.p, e->xcd, st));
         else if (use_f4)
-            HIPCHK(nldsc::launch_band_f4(dom, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, e->cst.p,
+            HIPCHK(nldsc::launch_band_f4(dom, max_nc, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, e->cst.p,
                                          e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
                                          (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                          e->ws_acc.p, e->xcd, st));

@@ -17,6 +17,8 @@ hipError_t launch_repack_count(const uint8_t* rows, uint32_t* geno, int n_snp, i
 hipError_t launch_snp_stats(const int* counts, const double* pos, int n_snp, int n_snp_pad, int n_org, double maf_thr,
                             double std_thr, float2* lut, SnpConst* cst, uint8_t* sflags, double* maf_out,
                             double* rstd_out, hipStream_t st);
+// exact left pointers L from the all-pass replay's A and the device MAF flags (sorted positions)
+hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const double* pos, int n, int* L, hipStream_t st);
 hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                        const float2* lut, const int4* items, const double* pos, const int* Lw, const int* Rw,
                        const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
@@ -25,11 +27,11 @@ hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st);
-// exact path on fp4 MFMAs (N < 2^22), single block-pair items (I, J, 1, 0)
-hipError_t launch_band_f4(bool dom, int n_items, const uint32_t* geno, int pitch_words, int n_it, const SnpConst* cst,
-                          const int4* items, const double* pos, const int* Lw, const int* Rw, const uint8_t* sflags,
-                          int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo, int own_hi,
-                          double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st);
+// exact path on fp4 MFMAs (N < 2^22), items (I, J0, nc <= max_nc, 0)
+hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* geno, int pitch_words, int n_it,
+                          const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
+                          const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
+                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st);
 // skewed 2x2 tiles (I, J, mask) of the exact path, one 256-thread workgroup each
 hipError_t launch_band_tile(bool dom, int n_tiles, const uint32_t* geno, int pitch_words, int n_it, int nblk,
                             const SnpConst* cst, const int4* tiles, const double* pos, const int* Lw, const int* Rw,

@@ -176,6 +176,23 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const double* _
     sflags[j] = fl;
 }
 
+// Exact left pointer of ChunkwiseReader (stream.h:182-197) for positions sorted over the used SNPs,
+// from the flag-independent all-pass replay: A_j = the all-pass left pointer (the first used SNP in
+// j's window), -1 where the reference never computes j whatever the MAF flags (unused SNP, or its
+// lagging right pointer).  Then L_j = the first used MAF-passing SNP in [A_j, j), or j itself, and
+// -1 for SNPs failing MAF (tests/test_plan.py checks this against the sequential replay).
+__global__ void left_pointer_kernel(const int* __restrict__ A, const uint8_t* __restrict__ sflags,
+                                    const double* __restrict__ pos, int n, int* __restrict__ L) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    int l = -1;
+    if (A[j] >= 0 && (sflags[j] & 1)) {
+        l = A[j];
+        while (l < j && !((sflags[l] & 1) && pos[l] >= 0.0)) ++l;
+    }
+    L[j] = l;
+}
+
 // ------------------------------------------------------------------------------------------
 // 3. band correlation kernel
 // ------------------------------------------------------------------------------------------
@@ -670,7 +687,8 @@ __device__ __forceinline__ f32x16v mfma_f4(const i32x4& a, const i32x4& b, const
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, c, 4, 4, 0, E8M0_ONE, 0, E8M0_ONE);
 }
 
-template <bool DOM, bool DIAG0>
+// NC column blocks J0 .. J0+NC-1 share the row strip's decode; DIAG0: block 0 is the diagonal.
+template <bool DOM, int NC, bool DIAG0>
 __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const uint32_t* __restrict__ geno,
                                              int pitch_words, int n_it, const SnpConst* __restrict__ cst,
                                              const double* __restrict__ pos, const int* __restrict__ Lw,
@@ -678,12 +696,12 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
                                              int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                                              int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
                                              int* __restrict__ ws_acc) {
-    constexpr int NS = 64;
+    constexpr int NS = 32 * (1 + NC);
     const int lane = threadIdx.x;
     const int i = lane & 31, h = lane >> 5;
     const int I = it.x, J0 = it.y;
     for (int s = lane; s < NS; s += 64) {
-        const int g = s < 32 ? I * 32 + s : J0 * 32 + (s & 31);
+        const int g = s < 32 ? I * 32 + s : (J0 + (s - 32) / 32) * 32 + (s & 31);
         SnpSlot si;
         si.g = g;
         if (g < n_snp) {
@@ -698,52 +716,76 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     }
     __syncthreads();
 
-    f32x16v gxx{}, gxo{}, gox{}, goo{}, gxh{}, goh{}, ghx{}, gho{};
+    f32x16v gxx[NC], gxo[NC], gox[NC], goo[NC], gxh[NC], goh[NC], ghx[NC], gho[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) gxx[c] = gxo[c] = gox[c] = goo[c] = gxh[c] = goh[c] = ghx[c] = gho[c] = f32x16v{};
     const uint4* rowp = reinterpret_cast<const uint4*>(geno + (size_t)(I * 32 + i) * (size_t)pitch_words) + h;
-    const uint4* colp = reinterpret_cast<const uint4*>(geno + (size_t)(J0 * 32 + i) * (size_t)pitch_words) + h;
+    const uint4* colp[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+        colp[c] = reinterpret_cast<const uint4*>(geno + (size_t)((J0 + c) * 32 + i) * (size_t)pitch_words) + h;
     // n_it is even (rows are padded to 64 bytes).  Two chunk buffers: P holds even chunks, Q odd
     // ones; each is reloaded right after its last word is decoded and read again two K steps
     // later, with no register copies of loads in flight (those would force vmcnt(0)).
     const int last = n_it - 1;
-    uint4 pr = rowp[0], pc = colp[0], qr = rowp[2], qc = colp[2];
+    uint4 pr = rowp[0], qr = rowp[2], pc[NC], qc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) { pc[c] = colp[c][0]; qc[c] = colp[c][2]; }
     // two named fragment sets: set 1 is decoded while set 0 feeds the MFMAs and vice versa, so no
     // fragment is copied (a single rotating set costs ~12 v_mov per K step)
-    F4Frag a0 = decode_f4(pr.x, pr.y), b0 = decode_f4(pc.x, pc.y), a1, b1;
-    auto mfmas = [&](const F4Frag& a, const F4Frag& b) {
-        gxx = mfma_f4(a.x, b.x, gxx);
-        gxo = mfma_f4(a.x, b.o, gxo);
-        gox = mfma_f4(a.o, b.x, gox);
-        goo = mfma_f4(a.o, b.o, goo);
-        if (DOM) {
-            gxh = mfma_f4(a.x, b.h, gxh);
-            goh = mfma_f4(a.o, b.h, goh);
-            if (!DIAG0) {  // on a diagonal block R_i . A_j is the transposed A_j . R_i
-                ghx = mfma_f4(a.h, b.x, ghx);
-                gho = mfma_f4(a.h, b.o, gho);
+    F4Frag a0 = decode_f4(pr.x, pr.y), a1, b0[NC], b1[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) b0[c] = decode_f4(pc[c].x, pc[c].y);
+    auto mfmas = [&](const F4Frag& a, const F4Frag (&b)[NC]) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            gxx[c] = mfma_f4(a.x, b[c].x, gxx[c]);
+            gxo[c] = mfma_f4(a.x, b[c].o, gxo[c]);
+            gox[c] = mfma_f4(a.o, b[c].x, gox[c]);
+            goo[c] = mfma_f4(a.o, b[c].o, goo[c]);
+            if (DOM) {
+                gxh[c] = mfma_f4(a.x, b[c].h, gxh[c]);
+                goh[c] = mfma_f4(a.o, b[c].h, goh[c]);
+                if (!(DIAG0 && c == 0)) {  // on a diagonal block R_i . A_j is the transposed A_j . R_i
+                    ghx[c] = mfma_f4(a.h, b[c].x, ghx[c]);
+                    gho[c] = mfma_f4(a.h, b[c].o, gho[c]);
+                }
             }
         }
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
+        for (int m = 0; m < 8 * NC; ++m) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, NC == 1 ? 5 : 4, 0);
         }
     };
     for (int t = 0; t < n_it; t += 2) {
-        a1 = decode_f4(pr.z, pr.w); b1 = decode_f4(pc.z, pc.w);
-        mfmas(a0, b0);                                      // K step 2t   (chunk t, words 0-1)
+        a1 = decode_f4(pr.z, pr.w);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) b1[c] = decode_f4(pc[c].z, pc[c].w);
+        mfmas(a0, b0);  // K step 2t   (chunk t, words 0-1)
         pr = rowp[2 * min(t + 2, last)];
-        pc = colp[2 * min(t + 2, last)];
-        a0 = decode_f4(qr.x, qr.y); b0 = decode_f4(qc.x, qc.y);
-        mfmas(a1, b1);                                      // K step 2t+1 (chunk t, words 2-3)
-        a1 = decode_f4(qr.z, qr.w); b1 = decode_f4(qc.z, qc.w);
-        mfmas(a0, b0);                                      // K step 2t+2 (chunk t+1, words 0-1)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) pc[c] = colp[c][2 * min(t + 2, last)];
+        a0 = decode_f4(qr.x, qr.y);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) b0[c] = decode_f4(qc[c].x, qc[c].y);
+        mfmas(a1, b1);  // K step 2t+1 (chunk t, words 2-3)
+        a1 = decode_f4(qr.z, qr.w);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) b1[c] = decode_f4(qc[c].z, qc[c].w);
+        mfmas(a0, b0);  // K step 2t+2 (chunk t+1, words 0-1)
         qr = rowp[2 * min(t + 3, last)];
-        qc = colp[2 * min(t + 3, last)];
-        a0 = decode_f4(pr.x, pr.y); b0 = decode_f4(pc.x, pc.y);
-        mfmas(a1, b1);                                      // K step 2t+3 (chunk t+1, words 2-3)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) qc[c] = colp[c][2 * min(t + 3, last)];
+        a0 = decode_f4(pr.x, pr.y);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) b0[c] = decode_f4(pc[c].x, pc[c].y);
+        mfmas(a1, b1);  // K step 2t+3 (chunk t+1, words 2-3)
     }
-    pair_epilogue<DOM>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32, DIAG0, i, h, gxx, gxo, gox, goo,
-                       gxh, goh, ghx, gho, ld_wind, n_org, rsq_thr);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+        pair_epilogue<DOM>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * c, DIAG0 && c == 0, i,
+                           h, gxx[c], gxo[c], gox[c], goo[c], gxh[c], goh[c], ghx[c], gho[c], ld_wind, n_org, rsq_thr);
     __syncthreads();
     for (int s = lane; s < NS; s += 64) {
         const int g = sh.info[s].g;
@@ -760,22 +802,25 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     }
 }
 
-template <bool DOM>
-__global__ void __launch_bounds__(64, 2) band_f4_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
-                                                      const SnpConst* __restrict__ cst, const int4* __restrict__ items,
-                                                      const double* __restrict__ pos, const int* __restrict__ Lw,
-                                                      const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
-                                                      int n_snp, double ld_wind, double n_org, double rsq_thr,
-                                                      int own_lo, int own_hi, double* __restrict__ l2_acc,
-                                                      double* __restrict__ l2d_acc, int* __restrict__ ws_acc, int xcd) {
+// WPS 2: single block-pair items; WPS 1: items of up to 2 column blocks (1 wave per SIMD, the
+// 2 x 128 accumulator registers in AGPRs).
+template <bool DOM, int WPS>
+__global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
+                                                        const SnpConst* __restrict__ cst, const int4* __restrict__ items,
+                                                        const double* __restrict__ pos, const int* __restrict__ Lw,
+                                                        const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
+                                                        int n_snp, double ld_wind, double n_org, double rsq_thr,
+                                                        int own_lo, int own_hi, double* __restrict__ l2_acc,
+                                                        double* __restrict__ l2d_acc, int* __restrict__ ws_acc, int xcd) {
     __shared__ BandI8Lds sh;
     const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
-    if (it.y == it.x)
-        band_f4_body<DOM, true>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,
-                                rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc);
-    else
-        band_f4_body<DOM, false>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,
-                                 rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc);
+#define NLDSC_BODY(NC_, DIAG_)                                                                                        \
+    band_f4_body<DOM, NC_, DIAG_>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,  \
+                                  rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc)
+    const bool diag = it.y == it.x;
+    if (WPS == 1 && it.z == 2) { if (diag) NLDSC_BODY(2, true); else NLDSC_BODY(2, false); }
+    else { if (diag) NLDSC_BODY(1, true); else NLDSC_BODY(1, false); }
+#undef NLDSC_BODY
 }
 
 // ---- skewed 2x2 tiles: the four waves of a workgroup share every decoded strip through LDS ----
@@ -1034,6 +1079,12 @@ hipError_t launch_snp_stats(const int* counts, const double* pos, int n_snp, int
     return hipGetLastError();
 }
 
+hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const double* pos, int n, int* L, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(left_pointer_kernel, dim3((n + 255) / 256), dim3(256), 0, st, A, sflags, pos, n, L);
+    return hipGetLastError();
+}
+
 hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                        const float2* lut, const int4* items, const double* pos, const int* Lw, const int* Rw,
                        const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
@@ -1063,16 +1114,17 @@ hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* gen
     return hipGetLastError();
 }
 
-hipError_t launch_band_f4(bool dom, int n_items, const uint32_t* geno, int pitch_words, int n_it, const SnpConst* cst,
-                          const int4* items, const double* pos, const int* Lw, const int* Rw, const uint8_t* sflags,
-                          int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo, int own_hi,
-                          double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st) {
+hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* geno, int pitch_words, int n_it,
+                          const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
+                          const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
+                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st) {
     if (n_items <= 0) return hipSuccess;
-#define NLDSC_BAND(DOM_)                                                                                            \
-    hipLaunchKernelGGL((band_f4_kernel<DOM_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, cst, items,    \
-                       pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, \
-                       xcd ? 1 : 0)
-    if (dom) NLDSC_BAND(true); else NLDSC_BAND(false);
+#define NLDSC_BAND(DOM_, WPS_)                                                                                      \
+    hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, cst,   \
+                       items, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, \
+                       ws_acc, xcd ? 1 : 0)
+    if (dom) { if (max_nc == 2) NLDSC_BAND(true, 1); else NLDSC_BAND(true, 2); }
+    else { if (max_nc == 2) NLDSC_BAND(false, 1); else NLDSC_BAND(false, 2); }
 #undef NLDSC_BAND
     return hipGetLastError();
 }

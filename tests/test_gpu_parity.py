@@ -239,3 +239,28 @@ def same_gram(a, b, label):
     for k in ("l2", "l2d"):
         np.testing.assert_array_equal(np.isnan(a[k]), np.isnan(b[k]), err_msg=f"{label} {k}")
         np.testing.assert_allclose(a[k], b[k], rtol=1e-13, atol=1e-14, equal_nan=True, err_msg=f"{label} {k}")
+
+
+@pytest.mark.parametrize("order", ["sorted", "unsorted"])
+def test_heavy_maf_failure_both_schedule_paths(engine, order):
+    """Sorted positions take the no-sync path (all-pass schedule + device left pointers), unsorted ones
+    the sequential host replay; both must match the fp64 truth with a third of the SNPs failing MAF and
+    some unused (pos < 0)."""
+    from nldsc_amd import synth
+    rng = np.random.default_rng(91)
+    N, M = 200, 240
+    spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=6.0, seed=91, missing=0.02)
+    spec.negative_pos = [int(x) for x in rng.integers(0, M, 6)]
+    g = synth.genotypes(spec)
+    rows = synth.pack_bed_rows(g)
+    pos = synth.positions_cm(spec)
+    if order == "unsorted":
+        k = rng.permutation(M)[:20]
+        pos[k] = pos[k[::-1]]
+    engine.load_bed_bytes(synth.bed_bytes(rows), M, N)
+    exp = O.run_f64(rows, N, 1.0, 0.2, 1e-5, 0.01, pos)
+    assert np.isnan(exp["l2"]).sum() > M // 5  # many SNPs fail MAF 0.2
+    for mode in EXACT:
+        got = engine.run(1.0, 0.2, 1e-5, 0.01, pos, flags=MODES[mode])
+        assert_ld_close(got, exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
+                                           maf=(0.0, 0.0)), label=f"{order} {mode}")

@@ -124,3 +124,36 @@ def test_tiles_fill_on_c3_geometry():
     _, _, ones = _lib.plan_band(pos, np.ones(M, np.uint8), 1.0)
     _, _, tiles = _lib.plan_band(pos, np.ones(M, np.uint8), 1.0, max_nc=4)
     assert len(ones) / (4 * len(tiles)) > 0.93
+
+
+def left_pointers_from_all_pass(pos, passed, A):
+    """The rule left_pointer_kernel applies (sorted positions): L_j = first used passing SNP in
+    [A_j, j), else j; -1 where A_j < 0 or j fails MAF."""
+    used = pos >= 0
+    L = np.full(len(pos), -1)
+    for j in range(len(pos)):
+        if A[j] < 0 or not passed[j]:
+            continue
+        i = A[j]
+        while i < j and not (passed[i] and used[i]):
+            i += 1
+        L[j] = i
+    return L
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_left_pointers_from_all_pass_replay(seed):
+    """Sorted positions: the sequential replay's (L, R) equal (rule above, all-pass R) — ties, unused SNPs
+    (pos < 0, including the lagging right pointer they cause), w = 0 and heavy MAF failure included."""
+    rng = np.random.default_rng(500 + seed)
+    n = int(rng.integers(1, 300))
+    pos = np.cumsum(rng.exponential(rng.choice([0.005, 0.05, 0.5]), n))
+    if seed % 3 == 0:
+        pos = np.round(pos, 1)
+    pos[rng.random(n) < rng.choice([0, 0.05, 0.3, 0.7])] = -1.0
+    passed = rng.random(n) > rng.choice([0, 0.1, 0.6])
+    w = float(rng.choice([0.0, 0.01, 0.1, 1.0, 10.0]))
+    L, R = O.replay_windows(pos, passed, w)
+    A, Ra = O.replay_windows(pos, np.ones(n, bool), w)
+    np.testing.assert_array_equal(L, left_pointers_from_all_pass(pos, passed, A))
+    np.testing.assert_array_equal(R[L >= 0], Ra[L >= 0])

@@ -6,7 +6,8 @@
 
 A variant is `[label=][libpath:]token:token...`; `libpath` loads another build of libnldsc_amd.so (same
 ABI).  Tokens: wpsW, ncC (fp32 path), i8 (exact path), i8nc2, tile (exact path on skewed 2x2 tiles),
-xcd (XCD-contiguous item order), f4 (exact path on fp4 MFMAs).
+xcd (XCD-contiguous item order), f4 (exact path on fp4 MFMAs), f4nc2 (fp4 items of two column
+blocks).
 """
 import argparse
 import json
@@ -43,9 +44,10 @@ def main():
                      for p in parts if p.startswith(("wps", "nc")))
         os.environ["NLDSC_BAND_WPS"] = knobs.get("wps", "2")
         os.environ["NLDSC_BAND_NC"] = knobs.get("nc", "2")
-        os.environ["NLDSC_BAND_MODE"] = ("f4" if "f4" in parts else
+        os.environ["NLDSC_BAND_MODE"] = ("f4" if any(x.startswith("f4") for x in parts) else
                                          "i8" if any(x.startswith("i8") or x == "tile" for x in parts) else "f32")
         os.environ["NLDSC_BAND_I8_NC"] = "2" if "i8nc2" in parts else "1"
+        os.environ["NLDSC_BAND_F4_NC"] = "2" if "f4nc2" in parts else "1"
         os.environ["NLDSC_BAND_TILE"] = "1" if "tile" in parts else "0"
         os.environ["NLDSC_XCD"] = "1" if "xcd" in parts else "0"
         e = Engine(0, lib_path=lib)
