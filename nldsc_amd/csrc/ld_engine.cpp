@@ -106,6 +106,12 @@ struct nldsc_engine {
                            // (int8 above N = 2^22)
     bool band_tile = false;  // exact path on skewed 2x2 tiles sharing decoded strips (NLDSC_BAND_TILE)
     bool xcd = true;         // XCD-contiguous workgroup -> item order (NLDSC_XCD=0 disables)
+    int f4_grp = -1;         // fp4 path on 4-wave workgroups of skewed 2x2 tiles (NLDSC_BAND_F4_GRP = barrier
+                             // period in chunk pairs, 0: no barriers; -1: one wave per block pair)
+    int f4_ring = 0;         // fp4 strips through a per-wave LDS ring of this depth (NLDSC_BAND_F4_RING, 0: registers)
+    int band_round = 0;      // exact-path items per launch (NLDSC_BAND_ROUND; 0: one launch, -1: one
+                             // launch per round of resident waves)
+    int n_cu = 256;
     std::vector<int4> h_ones;
 
     ~nldsc_engine() {
@@ -309,6 +315,14 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
         e->band_mode = std::strcmp(v, "f32") == 0 ? 0 : std::strcmp(v, "f4") == 0 ? 2 : 1;
     if (const char* v = std::getenv("NLDSC_BAND_TILE")) e->band_tile = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_XCD")) e->xcd = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_BAND_ROUND")) e->band_round = std::atoi(v);
+    if (const char* v = std::getenv("NLDSC_BAND_F4_GRP")) e->f4_grp = std::atoi(v);
+    if (const char* v = std::getenv("NLDSC_BAND_F4_RING")) e->f4_ring = std::atoi(v);
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
+            e->n_cu = prop.multiProcessorCount;
+    }
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     for (auto& ev : e->ev)
         if (he == hipSuccess) he = hipEventCreate(&ev);
@@ -441,7 +455,8 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
              : (p->flags & NLDSC_FLAG_FP32) ? 0 : e->band_mode;
     if (path == 2 && N >= (1 << 22)) path = 1;  // fp32 accumulators are exact integers only below 2^24 >= 4N
     const bool use_i8 = path != 0, use_f4 = path == 2;
-    const bool tiled = path == 1 && e->band_tile;
+    const bool f4_grp = use_f4 && e->f4_grp >= 0;
+    const bool tiled = (path == 1 && e->band_tile) || f4_grp;
     const int max_nc = tiled ? 1 : use_f4 ? e->band_f4_nc : use_i8 ? e->band_i8_nc : e->band_nc;
     HIPCHK(hipSetDevice(e->device));
     hipStream_t st = e->stream;
@@ -555,16 +570,38 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         e->flop_issued = products * 2.0 * BLK * BLK * (double)row_bytes * 4.0;
     }
     if (!e->h_items.empty()) {
-        if (tiled)
+        if (f4_grp) {
+            const int n_tiles = (int)e->h_items.size();
+            const int per = e->band_round < 0 ? e->n_cu * 2 : e->band_round > 0 ? e->band_round : n_tiles;
+            for (int off = 0; off < n_tiles; off += per)
+                HIPCHK(nldsc::launch_band_f4_grp(dom, e->f4_grp, std::min(per, n_tiles - off), e->geno.p, pitch_words,
+                                                 n_it, nblk, e->cst.p, e->items.p + off, e->pos.p, e->Lw.p, e->Rw.p,
+                                                 e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end,
+                                                 e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, e->xcd, st));
+        } else if (tiled)
             HIPCHK(nldsc::launch_band_tile(dom, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, nblk, e->cst.p,
                                            e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
                                            (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                            e->ws_acc.p, e->xcd, st));
-        else if (use_f4)
-            HIPCHK(nldsc::launch_band_f4(dom, max_nc, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, e->cst.p,
-                                         e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
-                                         (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
-                                         e->ws_acc.p, e->xcd, st));
+        else if (use_f4) {
+            // Items of one launch start together and stream through the samples in near lockstep, so
+            // the strips they share stay in their XCD's L2; a round = the waves resident at once.
+            const int n_items = (int)e->h_items.size();
+            const int per = e->band_round < 0 ? e->n_cu * 4 * (max_nc == 2 ? 1 : 2)
+                          : e->band_round > 0 ? e->band_round : n_items;
+            for (int off = 0; off < n_items; off += per)
+                if (e->f4_ring > 0 && max_nc == 1)
+                    HIPCHK(nldsc::launch_band_f4_ring(dom, e->f4_ring, std::min(per, n_items - off), e->geno.p,
+                                                      pitch_words, n_it, e->cst.p, e->items.p + off, e->pos.p, e->Lw.p,
+                                                      e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr,
+                                                      own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p,
+                                                      e->xcd, st));
+                else
+                HIPCHK(nldsc::launch_band_f4(dom, max_nc, std::min(per, n_items - off), e->geno.p, pitch_words, n_it,
+                                             e->cst.p, e->items.p + off, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
+                                             p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p,
+                                             e->l2d_acc.p, e->ws_acc.p, e->xcd, st));
+        }
         else if (use_i8)
             HIPCHK(nldsc::launch_band_i8(dom, max_nc, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, e->cst.p,
                                          e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,

@@ -8,8 +8,11 @@ namespace nldsc {
 // Per-SNP constants of the exact-integer path: with x = additive count, h = [genotype >= 1],
 // o = [observed] (all 0 for missing calls and padding), the reference's standardised vectors are
 // A = (x - mu o) / sa and R = (2h - beta x - c o) / s.
+// X, H, Ob: sums of x, h, o over the SNP's sample slots (the fp4 path's Gram uses the missing
+// indicator m = 1 - o over all slots, so o-products are recovered as X - x.m, Ob_i + Ob_j - K + m.m, ...).
 struct SnpConst {
     double mu, sa, c, beta, s;
+    double X, H, Ob;
 };
 
 hipError_t launch_repack_count(const uint8_t* rows, uint32_t* geno, int n_snp, int nb, int pitch_words,
@@ -32,6 +35,19 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st);
+// fp4 exact path, one wave per block pair, strips through a `ring`-deep (3..5) per-wave LDS ring (LDS-DMA)
+hipError_t launch_band_f4_ring(bool dom, int ring, int n_items, const uint32_t* geno, int pitch_words, int n_it,
+                               const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
+                               const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr,
+                               int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd,
+                               hipStream_t st);
+// fp4 exact path on skewed 2x2 tiles (I, J, mask): one wave per block pair, four per workgroup sharing
+// strips through the CU's caches; `sync` = chunk pairs between workgroup barriers (0: none)
+hipError_t launch_band_f4_grp(bool dom, int sync, int n_tiles, const uint32_t* geno, int pitch_words, int n_it,
+                              int nblk, const SnpConst* cst, const int4* tiles, const double* pos, const int* Lw,
+                              const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind, double n_org,
+                              double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc,
+                              bool xcd, hipStream_t st);
 // skewed 2x2 tiles (I, J, mask) of the exact path, one 256-thread workgroup each
 hipError_t launch_band_tile(bool dom, int n_tiles, const uint32_t* geno, int pitch_words, int n_it, int nblk,
                             const SnpConst* cst, const int4* tiles, const double* pos, const int* Lw, const int* Rw,

@@ -118,9 +118,14 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const double* _
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_snp_pad) return;
     float2 L[4] = {make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
-    SnpConst K = {0.0, 0.0, 0.0, 0.0, 0.0};
+    SnpConst K = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     uint8_t fl = 0;
+    double sX = 0.0, sH = 0.0, sOb = 0.0;
     if (j < n_snp) {
+        const int* cj = counts + 4 * (size_t)j;
+        sX = (double)cj[1] + 2.0 * cj[2];
+        sH = (double)cj[1] + cj[2];
+        sOb = (double)cj[0] + cj[1] + cj[2];
         const double qnan = __builtin_nan("");
         double maf_d = qnan, rstd_d = qnan;
         if (pos[j] >= 0.0) {  // SNPFilter::is_used (tools.h:15-23)
@@ -138,7 +143,7 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const double* _
                     // every call missing: the reference's vectors are all NaN (MAF NaN passes the
                     // filter); they poison every window containing this SNP.
                     for (int c = 0; c < 4; ++c) L[c] = make_float2(qnan, 0.f);
-                    K = SnpConst{qnan, qnan, 0.0, 0.0, 0.0};
+                    K = SnpConst{qnan, qnan, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
                 } else {
                     const double abar = (c1 + 2.0 * c2) / n_obs, dbar = 2.0 * (c1 + c2) / n_obs;
                     const double da0 = -abar, da1 = 1.0 - abar, da2 = 2.0 - abar;
@@ -164,7 +169,7 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const double* _
                     L[3] = make_float2(ic, rc);   // code 11 hom A2
                     // exact path: A = (x - mu o) / sa,  R = (2h - beta x - c o) / s   (x, h, o integer)
                     K = SnpConst{abar, sd_a, rpass ? dbar - beta * abar : 0.0, rpass ? beta : 0.0,
-                                 rpass ? rstd_d : 0.0};
+                                 rpass ? rstd_d : 0.0, 0.0, 0.0, 0.0};
                 }
             }
         }
@@ -172,6 +177,7 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const double* _
         rstd_out[j] = (fl & 1) ? rstd_d : qnan;
     }
     for (int c = 0; c < 4; ++c) lut[(size_t)j * 4 + c] = L[c];
+    K.X = sX; K.H = sH; K.Ob = sOb;
     cst[j] = K;
     sflags[j] = fl;
 }
@@ -453,12 +459,14 @@ __device__ __forceinline__ int xcd_slot(int b, int n) {
 // Epilogue of one 32x32 block pair (row slots rb.., column slots cb.. of the LDS slot tables):
 // standardised dots from the 8 integer Gram entries in fp64, r2adj, window/pointer masks, and
 // per-SNP sums (ldscalc.h:33-55).  diag: the pair is a diagonal block (row block == column block).
-template <bool DOM, class Acc>
+// MB: the Gram is in the missing basis {x, h, m} (fp4 path): gxo holds x.m, gox m.x, goo m.m, goh m.h,
+// gho h.m, and `kslots` is the number of sample slots; o = 1 - m over every slot.
+template <bool DOM, class Acc, bool MB = false>
 __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpConst* cst, double* s_l2, double* s_l2d,
                                               int* s_wsa, int* s_wsd, int* s_wse, int rb, int cb, bool diag, int i,
                                               int h, const Acc& gxx, const Acc& gxo, const Acc& gox, const Acc& goo,
                                               const Acc& gxh, const Acc& goh, const Acc& ghx, const Acc& gho,
-                                              double ld_wind, double n_org, double rsq_thr) {
+                                              double ld_wind, double n_org, double rsq_thr, double kslots = 0.0) {
     const int sj = cb + i;
     const SnpSlot cj = info[sj];
     const SnpConst kj = cst[sj];
@@ -474,14 +482,17 @@ __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpCons
         const bool nji = !diag && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
         if (nij || nji) {
             const SnpConst ki = cst[si];
-            const double xx = (double)gxx[r], xo = (double)gxo[r], ox = (double)gox[r], oo = (double)goo[r];
+            const double xx = (double)gxx[r];
+            const double xo = MB ? ki.X - (double)gxo[r] : (double)gxo[r];
+            const double ox = MB ? kj.X - (double)gox[r] : (double)gox[r];
+            const double oo = MB ? ki.Ob + kj.Ob - kslots + (double)goo[r] : (double)goo[r];
             const double aa = (xx - kj.mu * xo - ki.mu * (ox - kj.mu * oo)) / (ki.sa * kj.sa);
             const double r2 = r2_adjusted(aa, n_org);
             if (nij) { atomicAdd(&s_l2[si], r2); atomicAdd(&s_wsa[si], 1); }
             if (nji) { atomicAdd(&s_l2[sj], r2); atomicAdd(&s_wsa[sj], 1); }
             if (DOM) {
                 if (nij && rpj) {  // A_i . R_j -> L2D_i (ldscalc.h:40-46)
-                    const double xh = (double)gxh[r], oh = (double)goh[r];
+                    const double xh = (double)gxh[r], oh = MB ? kj.H - (double)goh[r] : (double)goh[r];
                     const double ar = (2.0 * xh - kj.beta * xx - kj.c * xo -
                                        ki.mu * (2.0 * oh - kj.beta * ox - kj.c * oo)) / (ki.sa * kj.s);
                     const double rd = r2_adjusted(ar, n_org);
@@ -489,7 +500,7 @@ __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpCons
                     if (rd > rsq_thr) atomicAdd(&s_wse[si], 1);
                 }
                 if (!diag && nji && rpi) {  // R_i . A_j -> L2D_j
-                    const double hx = (double)ghx[r], ho = (double)gho[r];
+                    const double hx = (double)ghx[r], ho = MB ? ki.H - (double)gho[r] : (double)gho[r];
                     const double ra = (2.0 * hx - ki.beta * xx - ki.c * ox -
                                        kj.mu * (2.0 * ho - ki.beta * xo - ki.c * oo)) / (ki.s * kj.sa);
                     const double rd = r2_adjusted(ra, n_org);
@@ -652,9 +663,16 @@ __global__ void __launch_bounds__(64, WPS) band_i8_kernel(const uint32_t* __rest
 // MFMA), and the 2-bit -> 4-bit spread needs no shuffles because any fixed slot permutation is
 // fine: even code pairs go to the nibbles of one dword, odd pairs to another (11 VALU per word
 // against 27 for the int8 byte spread).
+// The third plane is the missing indicator m = [code 01] (missing call or padding slot) rather than
+// o = 1 - m: genotypes are mostly observed, so o is mostly ones while m is mostly zeros, and an MFMA
+// on mostly-zero operands draws less power (the chip holds a higher clock under this load).  The
+// o-products follow exactly from per-SNP sums (pair_epilogue<.., MB = true>).
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 constexpr int E8M0_ONE = 127;  // block scale 2^0
+#ifndef NLDSC_F4_VPM
+#define NLDSC_F4_VPM 5  // VALU instructions interleaved after each MFMA of a one-column-block item
+#endif
 
 struct F4Frag {
     i32x4 x, h, o;
@@ -664,14 +682,21 @@ __device__ __forceinline__ void decode_f4_word(uint32_t w, int& x0, int& x1, int
     constexpr uint32_t M = 0x22222222u;  // bit 1 of every nibble
     const uint32_t t0 = w << 1, w2 = w >> 2, t1 = w >> 1;  // lo of even pairs / hi, lo of odd pairs -> bit 1
     h0 = (int)(w & M);
-    o0 = (int)((w | ~t0) & M);             // 01 (missing / padding) -> 0
+    o0 = (int)(t0 & ~w & M);               // m: 01 (missing / padding) -> 0010 (1.0), else 0
     x0 = (int)((w & M) + (w & t0 & M));    // 10 -> 0010 (1.0), 11 -> 0100 (2.0)
     h1 = (int)(w2 & M);
-    o1 = (int)((w2 | ~t1) & M);
+    o1 = (int)(t1 & ~w2 & M);
     x1 = (int)((w2 & M) + (w2 & t1 & M));
 }
 
 __device__ __forceinline__ F4Frag decode_f4(uint32_t wa, uint32_t wb) {
+#ifdef NLDSC_F4_DIAG_NODECODE  // diagnostic build: raw words as operands (timing only)
+    F4Frag g;
+    g.x = i32x4{(int)wa, (int)wb, (int)(wa ^ wb), (int)wa};
+    g.h = i32x4{(int)wb, (int)wa, (int)wa, (int)wb};
+    g.o = i32x4{(int)(wa | wb), (int)wb, (int)wa, (int)(wa & wb)};
+    return g;
+#endif
     int x0, x1, x2, x3, h0, h1, h2, h3, o0, o1, o2, o3;
     decode_f4_word(wa, x0, x1, h0, h1, o0, o1);
     decode_f4_word(wb, x2, x3, h2, h3, o2, o3);
@@ -687,17 +712,46 @@ __device__ __forceinline__ f32x16v mfma_f4(const i32x4& a, const i32x4& b, const
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, c, 4, 4, 0, E8M0_ONE, 0, E8M0_ONE);
 }
 
+// ---- per-wave LDS ring of raw 2-bit chunks filled by LDS-DMA (global_load_lds_dwordx4) ----
+// hipcc waits vmcnt(0) before every ds_read that may alias a pending LDS-DMA, which would drain the
+// ring, so the DMA and the ring reads are inline asm with their own counted waits
+// (cdna_hip_programming.md §5.7): the wave's only vector-memory ops in the K loop are its DMAs.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+__device__ __forceinline__ uint32_t lds_addr(void* p) { return (uint32_t)(uintptr_t)(lds_void_ptr)p; }
+
+// 64 lanes x 16 B from per-lane global addresses into LDS [dst, dst + 1 KiB), lane-linear
+__device__ __forceinline__ void dma16(const void* src, uint32_t dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+}
+
+// wait until at most VM DMAs are in flight, then read this lane's 16 B of the row and column chunk
+template <int VM>
+__device__ __forceinline__ void ring_read(uint32_t row_addr, uint32_t col_addr, u32x4& wr, u32x4& wc) {
+    asm volatile("s_waitcnt vmcnt(%4)\n\tds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(wr), "=&v"(wc) : "v"(row_addr), "v"(col_addr), "i"(VM) : "memory");
+}
+
 // NC column blocks J0 .. J0+NC-1 share the row strip's decode; DIAG0: block 0 is the diagonal.
-template <bool DOM, int NC, bool DIAG0>
+// RING > 0 (NC == 1 only): the strips' chunks stream through a RING-deep per-wave LDS ring by LDS-DMA
+// instead of registers, RING chunk pairs ahead of their decode.
+// SYNC > 0 (workgroups of several waves, band_f4_grp_kernel): a workgroup barrier every SYNC
+// chunk pairs keeps the waves that share strips at the same samples, so the strips they share are
+// served from the CU's L1 / the XCD's L2; an inactive wave (!active) only keeps the barrier count.
+template <bool DOM, int NC, bool DIAG0, int SYNC = 0, int RING = 0>
 __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const uint32_t* __restrict__ geno,
                                              int pitch_words, int n_it, const SnpConst* __restrict__ cst,
                                              const double* __restrict__ pos, const int* __restrict__ Lw,
                                              const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
                                              int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                                              int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
-                                             int* __restrict__ ws_acc) {
+                                             int* __restrict__ ws_acc, bool active = true,
+                                             uint4* ring = nullptr) {
     constexpr int NS = 32 * (1 + NC);
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const int i = lane & 31, h = lane >> 5;
     const int I = it.x, J0 = it.y;
     for (int s = lane; s < NS; s += 64) {
@@ -715,27 +769,34 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         sh.wsa[s] = 0; sh.wsd[s] = 0; sh.wse[s] = 0;
     }
     __syncthreads();
+    if (!active) {
+        if (SYNC > 0)
+            for (int t = 0; t < n_it; t += 2)
+                if ((t >> 1) % (SYNC > 0 ? SYNC : 1) == 0) __builtin_amdgcn_s_barrier();
+        __syncthreads();
+        return;
+    }
 
     f32x16v gxx[NC], gxo[NC], gox[NC], goo[NC], gxh[NC], goh[NC], ghx[NC], gho[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) gxx[c] = gxo[c] = gox[c] = goo[c] = gxh[c] = goh[c] = ghx[c] = gho[c] = f32x16v{};
+#ifdef NLDSC_F4_DIAG_SAMEROWS  // diagnostic build: every item streams the same two strips (L2-resident)
+    const uint4* rowp = reinterpret_cast<const uint4*>(geno + (size_t)(i) * (size_t)pitch_words) + h;
+    const uint4* colp[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+        colp[c] = reinterpret_cast<const uint4*>(geno + (size_t)((1 + c) * 32 + i) * (size_t)pitch_words) + h;
+#else
     const uint4* rowp = reinterpret_cast<const uint4*>(geno + (size_t)(I * 32 + i) * (size_t)pitch_words) + h;
     const uint4* colp[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c)
         colp[c] = reinterpret_cast<const uint4*>(geno + (size_t)((J0 + c) * 32 + i) * (size_t)pitch_words) + h;
+#endif
     // n_it is even (rows are padded to 64 bytes).  Two chunk buffers: P holds even chunks, Q odd
     // ones; each is reloaded right after its last word is decoded and read again two K steps
     // later, with no register copies of loads in flight (those would force vmcnt(0)).
     const int last = n_it - 1;
-    uint4 pr = rowp[0], qr = rowp[2], pc[NC], qc[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) { pc[c] = colp[c][0]; qc[c] = colp[c][2]; }
-    // two named fragment sets: set 1 is decoded while set 0 feeds the MFMAs and vice versa, so no
-    // fragment is copied (a single rotating set costs ~12 v_mov per K step)
-    F4Frag a0 = decode_f4(pr.x, pr.y), a1, b0[NC], b1[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) b0[c] = decode_f4(pc[c].x, pc[c].y);
     auto mfmas = [&](const F4Frag& a, const F4Frag (&b)[NC]) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
@@ -755,10 +816,48 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
 #pragma unroll
         for (int m = 0; m < 8 * NC; ++m) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, NC == 1 ? 5 : 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, NC == 1 ? NLDSC_F4_VPM : 4, 0);
         }
     };
+    if constexpr (RING > 0 && NC == 1) {
+        // ring slot k: row chunk at [k][0][lane], column chunk at [k][1][lane] (uint4 ring[RING][2][64])
+        const uint32_t rb = lds_addr(ring), lane_off = (uint32_t)lane * 16u;
+        for (int k = 0; k < RING; ++k) {
+            dma16(rowp + 2 * min(k, last), rb + (uint32_t)k * 2048u);
+            dma16(colp[0] + 2 * min(k, last), rb + (uint32_t)k * 2048u + 1024u);
+        }
+        u32x4 wr, wc;
+        ring_read<2 * (RING - 1)>(rb + lane_off, rb + 1024u + lane_off, wr, wc);
+        dma16(rowp + 2 * min(RING, last), rb);
+        dma16(colp[0] + 2 * min(RING, last), rb + 1024u);
+        F4Frag a0 = decode_f4(wr.x, wr.y), a1, b0[1], b1[1];
+        b0[0] = decode_f4(wc.x, wc.y);
+        int slot = 1 % RING;
+        for (int t = 0; t < n_it; ++t) {  // chunk t is in (wr, wc)
+            a1 = decode_f4(wr.z, wr.w);
+            b1[0] = decode_f4(wc.z, wc.w);
+            mfmas(a0, b0);  // K step 2t
+            const uint32_t sa = rb + (uint32_t)slot * 2048u;
+            ring_read<2 * (RING - 1)>(sa + lane_off, sa + 1024u + lane_off, wr, wc);  // chunk t+1
+            dma16(rowp + 2 * min(t + 1 + RING, last), sa);
+            dma16(colp[0] + 2 * min(t + 1 + RING, last), sa + 1024u);
+            slot = slot + 1 == RING ? 0 : slot + 1;
+            a0 = decode_f4(wr.x, wr.y);
+            b0[0] = decode_f4(wc.x, wc.y);
+            mfmas(a1, b1);  // K step 2t+1
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
+    } else {
+    uint4 pr = rowp[0], qr = rowp[2], pc[NC], qc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) { pc[c] = colp[c][0]; qc[c] = colp[c][2]; }
+    // two named fragment sets: set 1 is decoded while set 0 feeds the MFMAs and vice versa, so no
+    // fragment is copied (a single rotating set costs ~12 v_mov per K step)
+    F4Frag a0 = decode_f4(pr.x, pr.y), a1, b0[NC], b1[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) b0[c] = decode_f4(pc[c].x, pc[c].y);
     for (int t = 0; t < n_it; t += 2) {
+        if (SYNC > 0 && (t >> 1) % (SYNC > 0 ? SYNC : 1) == 0) __builtin_amdgcn_s_barrier();
         a1 = decode_f4(pr.z, pr.w);
 #pragma unroll
         for (int c = 0; c < NC; ++c) b1[c] = decode_f4(pc[c].z, pc[c].w);
@@ -782,10 +881,12 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         for (int c = 0; c < NC; ++c) b0[c] = decode_f4(pc[c].x, pc[c].y);
         mfmas(a1, b1);  // K step 2t+3 (chunk t+1, words 2-3)
     }
+    }
 #pragma unroll
     for (int c = 0; c < NC; ++c)
-        pair_epilogue<DOM>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * c, DIAG0 && c == 0, i,
-                           h, gxx[c], gxo[c], gox[c], goo[c], gxh[c], goh[c], ghx[c], gho[c], ld_wind, n_org, rsq_thr);
+        pair_epilogue<DOM, f32x16v, true>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * c,
+                                          DIAG0 && c == 0, i, h, gxx[c], gxo[c], gox[c], goo[c], gxh[c], goh[c],
+                                          ghx[c], gho[c], ld_wind, n_org, rsq_thr, 128.0 * n_it);
     __syncthreads();
     for (int s = lane; s < NS; s += 64) {
         const int g = sh.info[s].g;
@@ -800,6 +901,48 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
             if (sh.wse[s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + g], sh.wse[s]);
         }
     }
+}
+
+// One wave per block pair (items (I, J, 1, 0)), strips streamed through a RING-deep LDS ring.
+template <bool DOM, int RING>
+__global__ void __launch_bounds__(64, 2) band_f4_ring_kernel(
+    const uint32_t* __restrict__ geno, int pitch_words, int n_it, const SnpConst* __restrict__ cst,
+    const int4* __restrict__ items, const double* __restrict__ pos, const int* __restrict__ Lw,
+    const int* __restrict__ Rw, const uint8_t* __restrict__ sflags, int n_snp, double ld_wind, double n_org,
+    double rsq_thr, int own_lo, int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
+    int* __restrict__ ws_acc, int xcd) {
+    __shared__ BandI8Lds sh;
+    __shared__ uint4 ring[RING * 2 * 64];
+    const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
+#define NLDSC_BODY(DIAG_)                                                                                           \
+    band_f4_body<DOM, 1, DIAG_, 0, RING>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, \
+                                         n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, true, ring)
+    if (it.x == it.y) NLDSC_BODY(true); else NLDSC_BODY(false);
+#undef NLDSC_BODY
+}
+
+// Skewed 2x2 tiles (I, J, mask) of single block pairs, one wave per pair (wave 0 -> (I, J), 1 -> (I, J+1),
+// 2 -> (I+1, J+1), 3 -> (I+1, J+2); bit w of mask = wave w's pair is scheduled): the four waves of a
+// workgroup run on one CU and read five strips between them instead of eight, so every strip
+// they share is fetched beyond the CU once.  Each wave decodes its own operands (no LDS traffic).
+template <bool DOM, int SYNC>
+__global__ void __launch_bounds__(256, 2) band_f4_grp_kernel(
+    const uint32_t* __restrict__ geno, int pitch_words, int n_it, const SnpConst* __restrict__ cst,
+    const int4* __restrict__ tiles, const double* __restrict__ pos, const int* __restrict__ Lw,
+    const int* __restrict__ Rw, const uint8_t* __restrict__ sflags, int n_snp, int nblk, double ld_wind,
+    double n_org, double rsq_thr, int own_lo, int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
+    int* __restrict__ ws_acc, int xcd) {
+    __shared__ BandI8Lds sh[4];
+    const int4 tile = tiles[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int a = min(tile.x + (w >> 1), nblk - 1), b = min(tile.y + (w & 1) + (w >> 1), nblk - 1);
+    const bool active = (tile.z >> w) & 1;
+    const int4 it = make_int4(a, b, 1, 0);
+#define NLDSC_BODY(DIAG_)                                                                                           \
+    band_f4_body<DOM, 1, DIAG_, SYNC>(sh[w], it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, \
+                                      n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, active)
+    if (a == b) NLDSC_BODY(true); else NLDSC_BODY(false);
+#undef NLDSC_BODY
 }
 
 // WPS 2: single block-pair items; WPS 1: items of up to 2 column blocks (1 wave per SIMD, the
@@ -1125,6 +1268,43 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                        ws_acc, xcd ? 1 : 0)
     if (dom) { if (max_nc == 2) NLDSC_BAND(true, 1); else NLDSC_BAND(true, 2); }
     else { if (max_nc == 2) NLDSC_BAND(false, 1); else NLDSC_BAND(false, 2); }
+#undef NLDSC_BAND
+    return hipGetLastError();
+}
+
+hipError_t launch_band_f4_ring(bool dom, int ring, int n_items, const uint32_t* geno, int pitch_words, int n_it,
+                               const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
+                               const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr,
+                               int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd,
+                               hipStream_t st) {
+    if (n_items <= 0) return hipSuccess;
+#define NLDSC_BAND(DOM_, RING_)                                                                                      \
+    hipLaunchKernelGGL((band_f4_ring_kernel<DOM_, RING_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it,  \
+                       cst, items, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc,     \
+                       l2d_acc, ws_acc, xcd ? 1 : 0)
+    if (dom) { if (ring >= 5) NLDSC_BAND(true, 5); else if (ring == 4) NLDSC_BAND(true, 4); else NLDSC_BAND(true, 3); }
+    else { if (ring >= 5) NLDSC_BAND(false, 5); else if (ring == 4) NLDSC_BAND(false, 4); else NLDSC_BAND(false, 3); }
+#undef NLDSC_BAND
+    return hipGetLastError();
+}
+
+hipError_t launch_band_f4_grp(bool dom, int sync, int n_tiles, const uint32_t* geno, int pitch_words, int n_it,
+                              int nblk, const SnpConst* cst, const int4* tiles, const double* pos, const int* Lw,
+                              const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind, double n_org,
+                              double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc,
+                              bool xcd, hipStream_t st) {
+    if (n_tiles <= 0) return hipSuccess;
+#define NLDSC_BAND(DOM_, SYNC_)                                                                                      \
+    hipLaunchKernelGGL((band_f4_grp_kernel<DOM_, SYNC_>), dim3(n_tiles), dim3(256), 0, st, geno, pitch_words, n_it,   \
+                       cst, tiles, pos, Lw, Rw, sflags, n_snp, nblk, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, \
+                       l2d_acc, ws_acc, xcd ? 1 : 0)
+    if (dom) {
+        if (sync >= 8) NLDSC_BAND(true, 8); else if (sync >= 2) NLDSC_BAND(true, 2); else if (sync == 1) NLDSC_BAND(true, 1);
+        else NLDSC_BAND(true, 0);
+    } else {
+        if (sync >= 8) NLDSC_BAND(false, 8); else if (sync >= 2) NLDSC_BAND(false, 2); else if (sync == 1) NLDSC_BAND(false, 1);
+        else NLDSC_BAND(false, 0);
+    }
 #undef NLDSC_BAND
     return hipGetLastError();
 }

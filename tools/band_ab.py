@@ -7,7 +7,9 @@
 A variant is `[label=][libpath:]token:token...`; `libpath` loads another build of libnldsc_amd.so (same
 ABI).  Tokens: wpsW, ncC (fp32 path), i8 (exact path), i8nc2, tile (exact path on skewed 2x2 tiles),
 xcd (XCD-contiguous item order), f4 (exact path on fp4 MFMAs), f4nc2 (fp4 items of two column
-blocks).
+blocks), roundR (R fp4 items per launch; round-1 = one launch per round of resident waves), grpS (fp4 on
+4-wave workgroups of skewed 2x2 tiles, a barrier every S chunk pairs; grp0: no barriers), ringD (fp4
+strips through a D-deep per-wave LDS ring filled by LDS-DMA).
 """
 import argparse
 import json
@@ -28,6 +30,9 @@ def main():
     ap.add_argument("--length-cm", type=float, default=70.0)
     ap.add_argument("--variants", default="wps1:nc2,wps2:nc2,wps2:nc1,wps1:nc1")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--major", action="store_true",
+                    help="swap hom-A1/hom-A2 codes of every SNP (.bim A2 = the major allele, as in PLINK's usual "
+                         "A1 = minor convention)")
     args = ap.parse_args()
     import torch
 
@@ -35,6 +40,10 @@ def main():
     from nldsc_amd.engine import Engine
     N, M = args.n_org, args.n_snp
     buf, pos = synth.device_bed(M, N, seed=7, length_cm=args.length_cm)
+    if args.major:  # 00 <-> 11 in every bit pair (het 10 and missing 01 unchanged)
+        body = buf[3:]
+        eq = torch.bitwise_and(torch.bitwise_not(torch.bitwise_xor(body, body >> 1)), 0x55)
+        body.bitwise_xor_(torch.bitwise_or(eq, eq << 1))
     engines = {}
     for v in args.variants.split(","):
         label, spec = v.split("=", 1) if "=" in v else (v, v)
@@ -50,6 +59,12 @@ def main():
         os.environ["NLDSC_BAND_F4_NC"] = "2" if "f4nc2" in parts else "1"
         os.environ["NLDSC_BAND_TILE"] = "1" if "tile" in parts else "0"
         os.environ["NLDSC_XCD"] = "1" if "xcd" in parts else "0"
+        grp = [p[3:] for p in parts if p.startswith("grp")]
+        os.environ["NLDSC_BAND_F4_GRP"] = grp[0] if grp else "-1"
+        ring = [p[4:] for p in parts if p.startswith("ring")]
+        os.environ["NLDSC_BAND_F4_RING"] = ring[0] if ring else "0"
+        rnd = [p[5:] for p in parts if p.startswith("round")]
+        os.environ["NLDSC_BAND_ROUND"] = rnd[0] if rnd else "0"
         e = Engine(0, lib_path=lib)
         v = label
         e.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
