@@ -105,9 +105,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                     help="collectives backend for N > 1 (gloo: rehearse several ranks on one GPU)")
-    ap.add_argument("--workload", choices=("c3", "c4"), default="c3",
+    ap.add_argument("--workload", choices=("c3", "c4", "c5"), default="c3",
                     help="c3: one chr1-like chromosome per GPU (default, the BASELINE metric); c4: the 22-autosome "
-                         "whole genome (sum M ~ 600k, BASELINE.json configs[3]) spread over the GPUs by LPT")
+                         "whole genome (sum M ~ 600k, BASELINE.json configs[3]) spread over the GPUs by LPT; c5: one "
+                         "eighth of the imputed genome per GPU (BASELINE.json configs[4]: M ~ 10M over 2.88 Gb, "
+                         "--ld-wind-kb 1000; --n-snp defaults to 1.25M per GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -131,6 +133,12 @@ def main():
 
     if args.workload == "c4":
         return whole_genome(args, world, rank, local, coll)
+    if args.workload == "c5":  # bp positions: 2.88 Gb / 10M SNPs = 288 bp per SNP, window 1000 kb
+        if args.n_snp == ap.get_default("n_snp"):
+            args.n_snp = 1_250_000
+        args.length_cm = 288.0 * args.n_snp
+        args.window_cm = 1.0e6
+        args.no_cpu = True
     N, M = args.n_org, args.n_snp
     flags = (_lib.FLAG_ADDITIVE_ONLY if args.additive_only else 0) | getattr(_lib, PATHS[args.path][0])
     t = time.perf_counter()
@@ -203,7 +211,7 @@ def main():
                     fp32_equivalent_frac_of_fp32_peak=fp32_equiv / FP32_MFMA_PEAK_TFLOPS)
         achieved = roof["achieved"]
         stages = {k: round(float(np.mean([x[k] for x in tims])), 3)
-                  for k in ("repack_ms", "stats_ms", "schedule_ms", "band_ms", "finalize_ms", "total_ms")}
+                  for k in ("count_ms", "stats_ms", "schedule_ms", "band_ms", "finalize_ms", "total_ms")}
         ws = out["l2_ws"]
         res = {
             "metric": METRIC,
@@ -219,10 +227,15 @@ def main():
             "dtype": dtype,
             "data": "synthetic (GPU-generated PLINK .bed, AR(1) haplotypes, 1% missing; one chromosome per GPU)",
             "config": {
-                "workload": ("C3 (BASELINE.json configs[2]): chr1-like N=315599 individuals, M=%d SNPs over %.0f cM, "
-                             "%s, --ld-wind-cm %g, maf %g, std-thr %g, rsq 1/M" %
-                             (M, args.length_cm, "additive only" if args.additive_only else "additive+dominance",
-                              w, args.maf, args.std_thr)),
+                "workload": (("C3 (BASELINE.json configs[2]): chr1-like N=%d individuals, M=%d SNPs over %.0f cM, "
+                              "%s, --ld-wind-cm %g, maf %g, std-thr %g, rsq 1/M" %
+                              (N, M, args.length_cm, "additive only" if args.additive_only else "additive+dominance",
+                               w, args.maf, args.std_thr)) if args.workload == "c3" else
+                             ("C5 slice (BASELINE.json configs[4]: imputed genome, M~10M over 2.88 Gb, --ld-wind-kb "
+                              "1000, 8 GPUs): per GPU N=%d individuals, M=%d SNPs over %.0f Mb (1/8 genome at M=1.25M), "
+                              "%s, window %g bp, maf %g, std-thr %g, rsq 1/M" %
+                              (N, M, args.length_cm / 1e6, "additive only" if args.additive_only else
+                               "additive+dominance", w, args.maf, args.std_thr))),
                 "n_org": N, "n_snp": M, "mean_window": float(ws[ws > 0].mean()),
                 "pairs_per_step_per_gpu": tims[-1]["pairs"],
                 "parallelism": f"position sharding, one chromosome unit per GPU x {world}",

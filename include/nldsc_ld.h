@@ -86,7 +86,9 @@ void nldsc_engine_destroy(nldsc_engine* e);
 
 /* Make a .bed image resident on the engine's device.  `bed` is the complete file content
  * (3 magic bytes + n_snp rows of ceil(n_org/4) bytes), in host memory (_host) or in device
- * memory of the engine's device (_device, e.g. a torch tensor's data pointer; copied). */
+ * memory of the engine's device (_device, e.g. a torch tensor's data pointer; copied).
+ * The rows are stored at a 64-byte-aligned pitch (pitched copies; padding read as missing), the
+ * layout every run reads in place. */
 int nldsc_engine_load_bed_file(nldsc_engine* e, const char* path, int32_t n_snp, int32_t n_org,
                                char* err, size_t errlen);
 int nldsc_engine_load_bed_host(nldsc_engine* e, const uint8_t* bed, size_t len, int32_t n_snp,
@@ -102,7 +104,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
                      nldsc_ld_result* r, char* err, size_t errlen);
 
 /* Per-stage device timings (milliseconds, HIP events on the engine stream) of the last run:
- * [0] repack+count, [1] per-SNP statistics, [2] window replay + schedule (host, incl. sync),
+ * [0] genotype count, [1] per-SNP statistics, [2] window replay + schedule (host time; overlaps [0]),
  * [3] band correlation kernel (all launches), [4] finalize, [5] total.
  * Also: algorithmic FLOPs (2N(1/2 sum WSA + sum WSD)), FLOPs issued to the matrix cores by the
  * band kernel (all 32x32 blocks of the schedule, padded sample slots included), SNP pairs
@@ -112,6 +114,13 @@ int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, d
 /* Path of the last run: 2 = exact Gram on fp4 MFMAs, 1 = exact Gram on int8 MFMAs, 0 = fp32;
  * *ops_alg_i8 = algorithmic ops of the exact formulation, 2N (2 sum WSA + 2 sum WSD). */
 int nldsc_engine_path(const nldsc_engine* e, int32_t* exact_i8, double* ops_alg_i8);
+
+/* Load SNP rows [snp_begin, snp_end) of a .bed file of n_snp_file SNPs as the engine's image
+ * (snp_end - snp_begin SNPs; the run then takes the positions of that slice).  Position sharding
+ * (SURVEY.md §8 e1): each GPU reads only its owned range plus the window halo around it.
+ * Same magic / size checks and messages as nldsc_engine_load_bed_file. */
+int nldsc_engine_load_bed_file_range(nldsc_engine* e, const char* path, int32_t n_snp_file, int32_t n_org,
+                                     int32_t snp_begin, int32_t snp_end, char* err, size_t errlen);
 
 /* Host-only plan of the band kernel (no GPU needed; the engine calls the same code):
  * replays the reference's sliding-window pointers (stream.h:131-155,182-197) from positions and

@@ -28,7 +28,7 @@ EXPORTED = (
     "nldsc_ld_calculate", "nldsc_version", "nldsc_device_count", "nldsc_engine_create",
     "nldsc_engine_destroy", "nldsc_engine_load_bed_file", "nldsc_engine_load_bed_host",
     "nldsc_engine_load_bed_device", "nldsc_engine_run", "nldsc_engine_timings",
-    "nldsc_synth_bed_device", "nldsc_engine_path", "nldsc_plan_band",
+    "nldsc_synth_bed_device", "nldsc_engine_path", "nldsc_plan_band", "nldsc_engine_load_bed_file_range",
 )
 
 
@@ -92,11 +92,15 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         L.nldsc_plan_band.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
                                       ctypes.c_int32, vp, vp, vp, ctypes.c_int32]
         L.nldsc_engine_path.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)]
+        # entry points newer builds add (an older build loaded for A/B timing may lack them)
+        if path == LIB_PATH or hasattr(L, "nldsc_engine_load_bed_file_range"):
+            L.nldsc_engine_load_bed_file_range.argtypes = [vp, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32,
+                                                           ctypes.c_int32, ctypes.c_int32] + c_err
         L.nldsc_synth_bed_device.argtypes = [ctypes.c_int32, vp, ctypes.c_int32, ctypes.c_int32,
                                              ctypes.POINTER(ctypes.c_float), ctypes.c_float, ctypes.c_float,
                                              ctypes.c_uint64] + c_err
         for name in EXPORTED:
-            if name not in ("nldsc_version", "nldsc_device_count", "nldsc_engine_destroy"):
+            if name not in ("nldsc_version", "nldsc_device_count", "nldsc_engine_destroy") and hasattr(L, name):
                 getattr(L, name).restype = ctypes.c_int
         _libs[path] = L
     return _libs[path]

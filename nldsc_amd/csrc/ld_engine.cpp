@@ -3,7 +3,8 @@
 // One engine = one HIP device + one stream + device buffers that persist across runs.
 // A run (nldsc_engine_run) is the whole hot path of bayarpark/nldsc's `calculate`
 // (nldsc/ldscore/_ldscore/ldscalc.h:8-65) over a .bed image already resident in HBM:
-//   repack+count -> per-SNP statistics -> window replay + tile schedule (host, O(M)) ->
+//   count (resident rows, kept at an aligned pitch by the loaders) -> per-SNP statistics ->
+//   window replay + tile schedule (host, O(M), overlapping the count) ->
 //   band correlation kernels -> finalize -> results to host.
 #include <hip/hip_runtime.h>
 
@@ -26,7 +27,18 @@ namespace {
 
 constexpr int BLK = 32;             // SNPs per MFMA block
 constexpr int CHUNK_BYTES = 32;     // one K-loop chunk of a 2-bit row (16 B per lane half)
-constexpr int ROW_ALIGN_BYTES = 64; // rows hold an even number of chunks (the fp4 loop takes two at a time)
+#ifndef NLDSC_F4_PF
+#define NLDSC_F4_PF 2
+#endif
+// resident row pitch: a multiple of the chunks the fp4 K loop takes per iteration (2 or 4 x 32 bytes)
+constexpr int ROW_ALIGN_BYTES = NLDSC_F4_PF == 4 ? 128 : 64;
+
+// resident layout of a .bed image: row j of ceil(N/4) bytes at j * row_bytes, n_rows = M rounded up to 32
+int row_pitch(int32_t n_org) {
+    const int nb = n_org / 4 + (n_org % 4 > 0);
+    return (nb + ROW_ALIGN_BYTES - 1) / ROW_ALIGN_BYTES * ROW_ALIGN_BYTES;
+}
+int padded_rows(int32_t n_snp) { return (n_snp + BLK - 1) / BLK * BLK; }
 
 // Message of BedStreamReader::check_plink_magic_number (stream.h:88-102), verbatim.
 const char* kBadMagic =
@@ -71,6 +83,24 @@ struct DevBuf {
     }
 };
 
+// page-locked host buffer (async H2D copies out of it do not block the calling thread)
+struct HostPinned {
+    uint8_t* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= n) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipHostMalloc((void**)&p, std::max<size_t>(want, 1));
+        if (e == hipSuccess) n = want;
+        return e;
+    }
+    ~HostPinned() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
 }  // namespace
 
 struct nldsc_engine {
@@ -79,10 +109,10 @@ struct nldsc_engine {
     hipEvent_t ev[6] = {};
     // resident .bed image
     DevBuf<uint8_t> bed;
-    size_t bed_len = 0;
+    DevBuf<uint8_t> lastb;  // each row's original last byte (the per-run count kernel masks a copy of it)
     int32_t n_snp = 0, n_org = 0;
     // work buffers
-    DevBuf<uint32_t> geno;
+
     DevBuf<int> counts, Lw, Rw, Aw, ws_acc, ws3;
     DevBuf<float2> lut;
     DevBuf<nldsc::SnpConst> cst;
@@ -93,6 +123,7 @@ struct nldsc_engine {
     std::vector<uint8_t> h_flags, h_all_pass;
     std::vector<int> h_L, h_R;
     std::vector<int4> h_items;
+    HostPinned h_stage;  // pinned upload staging of the plan (L, R, items)
     // timings of the last run
     double ms[6] = {0, 0, 0, 0, 0, 0};
     double flop_alg = 0, flop_issued = 0, pairs = 0, ops_alg_i8 = 0;
@@ -116,7 +147,7 @@ struct nldsc_engine {
 
     ~nldsc_engine() {
         (void)hipSetDevice(device);
-        bed.release(); geno.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
+        bed.release(); lastb.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
         ws3.release(); lut.release(); cst.release(); sflags.release(); pos.release(); maf.release(); rstd.release();
         l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
@@ -286,6 +317,27 @@ void plan_tiles(const std::vector<int4>& ones, int nblk, std::vector<int4>& out)
     }
 }
 
+// device buffers of a resident image of n_snp rows (all rows, pitch padding, saved last bytes)
+hipError_t alloc_image(nldsc_engine* e, int32_t n_snp, int32_t n_org) {
+    e->n_snp = e->n_org = 0;  // no valid image until finish_image
+    hipError_t he = e->bed.ensure((size_t)padded_rows(n_snp) * (size_t)row_pitch(n_org));
+    if (he == hipSuccess) he = e->lastb.ensure((size_t)n_snp);
+    return he;
+}
+
+// after the rows are copied in: save last bytes, pad, and mark the image valid
+hipError_t finish_image(nldsc_engine* e, int32_t n_snp, int32_t n_org) {
+    const int nb = n_org / 4 + (n_org % 4 > 0);
+    hipError_t he = nldsc::launch_pad_rows(e->bed.p, e->lastb.p, n_snp, padded_rows(n_snp), nb, row_pitch(n_org),
+                                           e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    if (he == hipSuccess) {
+        e->n_snp = n_snp;
+        e->n_org = n_org;
+    }
+    return he;
+}
+
 }  // namespace
 
 extern "C" {
@@ -344,13 +396,11 @@ int nldsc_engine_load_bed_host(nldsc_engine* e, const uint8_t* bed, size_t len, 
     rc = check_magic(bed, len, n_snp, n_org, err, errlen);
     if (rc) return rc;
     HIPCHK(hipSetDevice(e->device));
-    const size_t need = bed_bytes_needed(n_snp, n_org);
-    HIPCHK(e->bed.ensure(need));
-    HIPCHK(hipMemcpyAsync(e->bed.p, bed, need, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    e->bed_len = need;
-    e->n_snp = n_snp;
-    e->n_org = n_org;
+    const size_t nb = (size_t)(n_org / 4 + (n_org % 4 > 0));
+    HIPCHK(alloc_image(e, n_snp, n_org));
+    HIPCHK(hipMemcpy2DAsync(e->bed.p, (size_t)row_pitch(n_org), bed + 3, nb, nb, (size_t)n_snp, hipMemcpyHostToDevice,
+                            e->stream));
+    HIPCHK(finish_image(e, n_snp, n_org));
     return NLDSC_OK;
 }
 
@@ -368,12 +418,90 @@ int nldsc_engine_load_bed_device(nldsc_engine* e, const void* bed, size_t len, i
         return set_err(err, errlen, NLDSC_E_BAD_MAGIC, "%s", kBadMagic);
     if (len < need)
         return set_err(err, errlen, NLDSC_E_SIZE, "BED image too short: %zu bytes, expected at least %zu", len, need);
-    HIPCHK(e->bed.ensure(need));
-    HIPCHK(hipMemcpyAsync(e->bed.p, bed, need, hipMemcpyDeviceToDevice, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    e->bed_len = need;
-    e->n_snp = n_snp;
-    e->n_org = n_org;
+    const size_t nb = (size_t)(n_org / 4 + (n_org % 4 > 0));
+    HIPCHK(alloc_image(e, n_snp, n_org));
+    HIPCHK(hipMemcpy2DAsync(e->bed.p, (size_t)row_pitch(n_org), static_cast<const uint8_t*>(bed) + 3, nb, nb,
+                            (size_t)n_snp, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(finish_image(e, n_snp, n_org));
+    return NLDSC_OK;
+}
+
+int nldsc_engine_load_bed_file_range(nldsc_engine* e, const char* path, int32_t n_snp_file, int32_t n_org,
+                                     int32_t snp_begin, int32_t snp_end, char* err, size_t errlen) {
+    if (!e || !path) return set_err(err, errlen, NLDSC_E_ARG, "NULL engine or path");
+    int rc = check_dims(n_snp_file, n_org, err, errlen);
+    if (rc) return rc;
+    if (snp_begin < 0 || snp_end > n_snp_file || snp_begin >= snp_end)
+        return set_err(err, errlen, NLDSC_E_ARG, "SNP range [%d, %d) outside [0, %d) or empty", snp_begin, snp_end,
+                       n_snp_file);
+    FILE* f = std::fopen(path, "rb");
+    if (!f) {
+        // the reference's ifstream fails silently and then rejects the (unread) magic number
+        return set_err(err, errlen, NLDSC_E_BAD_MAGIC, "%s", kBadMagic);
+    }
+    uint8_t magic[3] = {0, 0, 0};
+    const size_t got = std::fread(magic, 1, 3, f);
+    if (got < 3 || magic[0] != 0x6c || magic[1] != 0x1b || magic[2] != 0x01) {
+        std::fclose(f);
+        return set_err(err, errlen, NLDSC_E_BAD_MAGIC, "%s", kBadMagic);
+    }
+    const size_t nb = (size_t)(n_org / 4 + (n_org % 4 > 0));
+    const size_t first = 3 + nb * (size_t)snp_begin, bytes = nb * (size_t)(snp_end - snp_begin);
+    const size_t need = first + bytes;  // file bytes the slice needs (the whole file for [0, n_snp_file))
+    auto too_short = [&](size_t have) {
+        std::fclose(f);
+        return set_err(err, errlen, NLDSC_E_SIZE,
+                       "BED file too short: %zu bytes, expected at least %zu for %d SNPs x %d individuals", have,
+                       need, snp_end, n_org);
+    };
+    if (fseeko(f, 0, SEEK_END) != 0) return too_short(3);
+    const off_t fsize = ftello(f);
+    if (fsize < 0 || (size_t)fsize < need) return too_short(fsize < 0 ? 0 : (size_t)fsize);
+    if (fseeko(f, (off_t)first, SEEK_SET) != 0) return too_short((size_t)fsize);
+    HIPCHK(hipSetDevice(e->device));
+    // rows stream through two pinned 64 MiB slots: the read into one slot overlaps the H2D copy out of
+    // the other (an event per slot marks its copy done)
+    const size_t pitch = (size_t)row_pitch(n_org);
+    const size_t rows_per = std::max<size_t>(1, (size_t(64) << 20) / nb), CH = rows_per * nb;  // ~64 MiB of rows
+    uint8_t* stage = nullptr;
+    hipEvent_t done[2] = {nullptr, nullptr};
+    if (hipHostMalloc((void**)&stage, 2 * CH) != hipSuccess) {
+        std::fclose(f);
+        return set_err(err, errlen, NLDSC_E_OOM, "cannot allocate pinned staging buffer");
+    }
+    hipError_t he = hipEventCreateWithFlags(&done[0], hipEventDisableTiming);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&done[1], hipEventDisableTiming);
+    const int32_t n_snp = snp_end - snp_begin;
+    if (he == hipSuccess) he = alloc_image(e, n_snp, n_org);
+    bool pending[2] = {false, false};
+    size_t off = 0, short_at = 0;
+    bool short_read = false;
+    for (int slot = 0; he == hipSuccess && off < bytes; slot ^= 1) {
+        const size_t n = std::min(CH, bytes - off);
+        uint8_t* buf = stage + (size_t)slot * CH;
+        if (pending[slot]) he = hipEventSynchronize(done[slot]);
+        if (he != hipSuccess) break;
+        const size_t r = std::fread(buf, 1, n, f);
+        if (r != n) {
+            short_read = true;
+            short_at = first + off + r;
+            break;
+        }
+        he = hipMemcpy2DAsync(e->bed.p + (off / nb) * pitch, pitch, buf, nb, nb, n / nb, hipMemcpyHostToDevice,
+                              e->stream);
+        if (he == hipSuccess) he = hipEventRecord(done[slot], e->stream);
+        pending[slot] = true;
+        off += n;
+    }
+    const hipError_t hs = hipStreamSynchronize(e->stream);
+    if (he == hipSuccess) he = hs;
+    for (hipEvent_t ev : done)
+        if (ev) (void)hipEventDestroy(ev);
+    (void)hipHostFree(stage);
+    if (short_read) return too_short(short_at);
+    std::fclose(f);
+    if (he != hipSuccess) return set_err(err, errlen, NLDSC_E_HIP, "HIP error %s loading BED", hipGetErrorString(he));
+    HIPCHK(finish_image(e, n_snp, n_org));
     return NLDSC_OK;
 }
 
@@ -382,58 +510,7 @@ int nldsc_engine_load_bed_file(nldsc_engine* e, const char* path, int32_t n_snp,
     if (!e || !path) return set_err(err, errlen, NLDSC_E_ARG, "NULL engine or path");
     int rc = check_dims(n_snp, n_org, err, errlen);
     if (rc) return rc;
-    FILE* f = std::fopen(path, "rb");
-    if (!f) {
-        // the reference's ifstream fails silently and then rejects the (unread) magic number
-        return set_err(err, errlen, NLDSC_E_BAD_MAGIC, "%s", kBadMagic);
-    }
-    const size_t need = bed_bytes_needed(n_snp, n_org);
-    uint8_t magic[3] = {0, 0, 0};
-    size_t got = std::fread(magic, 1, 3, f);
-    if (got < 3 || magic[0] != 0x6c || magic[1] != 0x1b || magic[2] != 0x01) {
-        std::fclose(f);
-        return set_err(err, errlen, NLDSC_E_BAD_MAGIC, "%s", kBadMagic);
-    }
-    HIPCHK(hipSetDevice(e->device));
-    // stream the rows through a pinned staging buffer (64 MiB double-buffered)
-    constexpr size_t CH = size_t(64) << 20;
-    uint8_t* stage = nullptr;
-    if (hipHostMalloc((void**)&stage, 2 * CH) != hipSuccess) {
-        std::fclose(f);
-        return set_err(err, errlen, NLDSC_E_OOM, "cannot allocate pinned staging buffer");
-    }
-    hipError_t he = e->bed.ensure(need);
-    size_t off = 3;
-    int slot = 0;
-    if (he == hipSuccess) he = hipMemcpyAsync(e->bed.p, magic, 3, hipMemcpyHostToDevice, e->stream);
-    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
-    while (he == hipSuccess && off < need) {
-        const size_t n = std::min(CH, need - off);
-        uint8_t* buf = stage + (size_t)slot * CH;
-        // the copy issued two chunks ago used this slot; wait for it before overwriting
-        he = hipStreamSynchronize(e->stream);
-        if (he != hipSuccess) break;
-        const size_t r = std::fread(buf, 1, n, f);
-        if (r != n) {
-            std::fclose(f);
-            (void)hipStreamSynchronize(e->stream);
-            (void)hipHostFree(stage);
-            return set_err(err, errlen, NLDSC_E_SIZE,
-                           "BED file too short: %zu bytes, expected at least %zu for %d SNPs x %d individuals",
-                           off + r, need, n_snp, n_org);
-        }
-        he = hipMemcpyAsync(e->bed.p + off, buf, n, hipMemcpyHostToDevice, e->stream);
-        off += n;
-        slot ^= 1;
-    }
-    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
-    std::fclose(f);
-    (void)hipHostFree(stage);
-    if (he != hipSuccess) return set_err(err, errlen, NLDSC_E_HIP, "HIP error %s loading BED", hipGetErrorString(he));
-    e->bed_len = need;
-    e->n_snp = n_snp;
-    e->n_org = n_org;
-    return NLDSC_OK;
+    return nldsc_engine_load_bed_file_range(e, path, n_snp, n_org, 0, n_snp, err, errlen);
 }
 
 int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32_t own_end,
@@ -462,7 +539,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     hipStream_t st = e->stream;
 
     const int nb = N / 4 + (N % 4 > 0);
-    const int row_bytes = (nb + ROW_ALIGN_BYTES - 1) / ROW_ALIGN_BYTES * ROW_ALIGN_BYTES;
+    const int row_bytes = row_pitch(N);
     const int pitch_words = row_bytes / 4;
     const int n_it = row_bytes / CHUNK_BYTES;
     const int nblk = (M + BLK - 1) / BLK;
@@ -473,7 +550,8 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     uint32_t tail_keep = 0xFFu;
     if (rem) tail_keep = strict ? (uint32_t)((1u << (2 * rem)) - 1u) : (uint32_t)(0xFFu << (8 - 2 * rem)) & 0xFFu;
 
-    HIPCHK(e->geno.ensure((size_t)Mpad * pitch_words));
+    // the band kernels read the resident rows (Mpad rows at row_bytes pitch) in place
+    const uint32_t* geno = reinterpret_cast<const uint32_t*>(e->bed.p);
     HIPCHK(e->counts.ensure((size_t)M * 4));
     HIPCHK(e->lut.ensure((size_t)Mpad * 4));
     HIPCHK(e->cst.ensure((size_t)Mpad));
@@ -493,8 +571,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     auto t_start = std::chrono::steady_clock::now();
     HIPCHK(hipEventRecord(e->ev[0], st));
     HIPCHK(hipMemcpyAsync(e->pos.p, p->positions, sizeof(double) * M, hipMemcpyHostToDevice, st));
-    if (Mpad > M) HIPCHK(hipMemsetAsync(e->geno.p + (size_t)M * pitch_words, 0x55, (size_t)(Mpad - M) * row_bytes, st));
-    HIPCHK(nldsc::launch_repack_count(e->bed.p + 3, e->geno.p, M, nb, pitch_words, tail_keep, e->counts.p, st));
+    HIPCHK(nldsc::launch_count_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, e->counts.p, st));
     HIPCHK(hipEventRecord(e->ev[1], st));
     HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->cst.p,
                                    e->sflags.p, e->maf.p, e->rstd.p, st));
@@ -509,7 +586,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         // Sorted positions: nothing waits for the GPU.  The right pointers and the all-pass left
         // pointers do not depend on the MAF flags, and SNPs failing MAF only shrink the set of needed
         // block pairs (their L_j grow, their rows and columns drop), so the all-pass schedule is a
-        // superset of the exact one; it is planned here while the GPU repacks, and the exact left
+        // superset of the exact one; it is planned here while the GPU counts, and the exact left
         // pointers come from the device flags (left_pointer_kernel).  The kernels mask every pair
         // with the exact pointers.
         e->h_all_pass.assign(M, 1);
@@ -541,16 +618,22 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
                                it.z, nblk);
     }
     HIPCHK(e->items.ensure(std::max<size_t>(e->h_items.size(), 1)));
+    // the plan goes up through pinned staging: a copy from pageable memory would block this thread
+    // until the stream drains (the count kernel), pinned copies are queued and return at once
+    const size_t bL = sizeof(int) * (size_t)M, bI = sizeof(int4) * e->h_items.size();
+    HIPCHK(e->h_stage.ensure(2 * bL + bI));
+    std::memcpy(e->h_stage.p, e->h_L.data(), bL);
+    std::memcpy(e->h_stage.p + bL, e->h_R.data(), bL);
+    if (bI) std::memcpy(e->h_stage.p + 2 * bL, e->h_items.data(), bI);
     if (sorted) {
         HIPCHK(e->Aw.ensure((size_t)M));
-        HIPCHK(hipMemcpyAsync(e->Aw.p, e->h_L.data(), sizeof(int) * M, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->Aw.p, e->h_stage.p, bL, hipMemcpyHostToDevice, st));
         HIPCHK(nldsc::launch_left_pointers(e->Aw.p, e->sflags.p, e->pos.p, M, e->Lw.p, st));
     } else {
-        HIPCHK(hipMemcpyAsync(e->Lw.p, e->h_L.data(), sizeof(int) * M, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->Lw.p, e->h_stage.p, bL, hipMemcpyHostToDevice, st));
     }
-    HIPCHK(hipMemcpyAsync(e->Rw.p, e->h_R.data(), sizeof(int) * M, hipMemcpyHostToDevice, st));
-    if (!e->h_items.empty())
-        HIPCHK(hipMemcpyAsync(e->items.p, e->h_items.data(), sizeof(int4) * e->h_items.size(), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(e->Rw.p, e->h_stage.p + bL, bL, hipMemcpyHostToDevice, st));
+    if (bI) HIPCHK(hipMemcpyAsync(e->items.p, e->h_stage.p + 2 * bL, bI, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(e->l2_acc.p, 0, sizeof(double) * M, st));
     HIPCHK(hipMemsetAsync(e->l2d_acc.p, 0, sizeof(double) * M, st));
     HIPCHK(hipMemsetAsync(e->ws_acc.p, 0, sizeof(int) * 3 * (size_t)M, st));
@@ -574,12 +657,12 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
             const int n_tiles = (int)e->h_items.size();
             const int per = e->band_round < 0 ? e->n_cu * 2 : e->band_round > 0 ? e->band_round : n_tiles;
             for (int off = 0; off < n_tiles; off += per)
-                HIPCHK(nldsc::launch_band_f4_grp(dom, e->f4_grp, std::min(per, n_tiles - off), e->geno.p, pitch_words,
+                HIPCHK(nldsc::launch_band_f4_grp(dom, e->f4_grp, std::min(per, n_tiles - off), geno, pitch_words,
                                                  n_it, nblk, e->cst.p, e->items.p + off, e->pos.p, e->Lw.p, e->Rw.p,
                                                  e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end,
                                                  e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, e->xcd, st));
         } else if (tiled)
-            HIPCHK(nldsc::launch_band_tile(dom, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, nblk, e->cst.p,
+            HIPCHK(nldsc::launch_band_tile(dom, (int)e->h_items.size(), geno, pitch_words, n_it, nblk, e->cst.p,
                                            e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
                                            (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                            e->ws_acc.p, e->xcd, st));
@@ -591,24 +674,25 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
                           : e->band_round > 0 ? e->band_round : n_items;
             for (int off = 0; off < n_items; off += per)
                 if (e->f4_ring > 0 && max_nc == 1)
-                    HIPCHK(nldsc::launch_band_f4_ring(dom, e->f4_ring, std::min(per, n_items - off), e->geno.p,
+                    HIPCHK(nldsc::launch_band_f4_ring(dom, e->f4_ring, std::min(per, n_items - off), geno,
                                                       pitch_words, n_it, e->cst.p, e->items.p + off, e->pos.p, e->Lw.p,
                                                       e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr,
                                                       own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p,
                                                       e->xcd, st));
                 else
-                HIPCHK(nldsc::launch_band_f4(dom, max_nc, std::min(per, n_items - off), e->geno.p, pitch_words, n_it,
+                HIPCHK(nldsc::launch_band_f4(dom, max_nc, std::min(per, n_items - off),
+                                             geno, pitch_words, n_it,
                                              e->cst.p, e->items.p + off, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
                                              p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p,
                                              e->l2d_acc.p, e->ws_acc.p, e->xcd, st));
         }
         else if (use_i8)
-            HIPCHK(nldsc::launch_band_i8(dom, max_nc, (int)e->h_items.size(), e->geno.p, pitch_words, n_it, e->cst.p,
+            HIPCHK(nldsc::launch_band_i8(dom, max_nc, (int)e->h_items.size(), geno, pitch_words, n_it, e->cst.p,
                                          e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
                                          (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                          e->ws_acc.p, e->xcd, st));
         else
-            HIPCHK(nldsc::launch_band(dom, e->band_wps, (int)e->h_items.size(), e->geno.p, pitch_words, n_it,
+            HIPCHK(nldsc::launch_band(dom, e->band_wps, (int)e->h_items.size(), geno, pitch_words, n_it,
                                       e->lut.p, e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
                                       (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                       e->ws_acc.p, st));

@@ -15,8 +15,12 @@ struct SnpConst {
     double X, H, Ob;
 };
 
-hipError_t launch_repack_count(const uint8_t* rows, uint32_t* geno, int n_snp, int nb, int pitch_words,
-                               uint32_t tail_keep, int* counts, hipStream_t st);
+// resident rows: after a load, save each row's last byte and fill the pitch padding (rows >= n_snp all 0x55)
+hipError_t launch_pad_rows(uint8_t* img, uint8_t* last, int n_snp, int n_rows, int nb, int row_bytes,
+                           hipStream_t st);
+// per run: genotype-code counts with the last byte set to this run's individuals (tail_keep mask)
+hipError_t launch_count_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
+                             int* counts, hipStream_t st);
 hipError_t launch_snp_stats(const int* counts, const double* pos, int n_snp, int n_snp_pad, int n_org, double maf_thr,
                             double std_thr, float2* lut, SnpConst* cst, uint8_t* sflags, double* maf_out,
                             double* rstd_out, hipStream_t st);

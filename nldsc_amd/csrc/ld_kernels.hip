@@ -1,9 +1,9 @@
 // ld_kernels.hip — gfx950 (MI355X, CDNA4) kernels of the LD-score engine.
 //
 // Pipeline for one `calculate` (reference: nldsc/ldscore/_ldscore/ldscalc.h:8-65):
-//   1. repack_count_kernel  .bed rows (unaligned, ceil(N/4) B) -> aligned 2-bit genotype rows in HBM,
-//                           the reference's last-byte rule applied (stream.h:55-66), plus per-SNP
-//                           genotype-code counts.  HBM-bound byte work.
+//   1. count_rows_kernel    per-SNP genotype-code counts over the resident .bed rows (kept at an aligned
+//                           pitch by the loaders), the reference's last-byte rule applied
+//                           (stream.h:55-66).  HBM-bound byte work.
 //   2. snp_stats_kernel     per-SNP MAF / filters / residual std and two 4-entry fp32 lookup tables
 //                           (standardised additive value and standardised dominance residual per
 //                           2-bit code), in closed form from the counts (encoder.h:91-133,
@@ -26,13 +26,15 @@ namespace nldsc {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // ------------------------------------------------------------------------------------------
-// 1. repack + count
+// 1. resident row layout + per-run count
 // ------------------------------------------------------------------------------------------
-// Output row j: pitch_words little-endian words.  Byte p of the row keeps the .bed byte
-// (4 samples, first sample in bits 7:6 per the reference's unpack order — any fixed slot order
-// is fine for dot products as long as every SNP uses the same one).  Bytes past the row and
-// the last byte's invalid bit pairs become 01 ("missing"), whose standardised value is exactly
-// 0 in both lookup tables, so they contribute nothing to any dot product.
+// The engine keeps the .bed rows in HBM at a pitch of row_bytes = ceil(nb / 64) * 64 (the loaders
+// place them there with pitched copies, so nothing is repacked per run).  Byte p of a row keeps the
+// .bed byte (4 samples, first sample in bits 7:6 per the reference's unpack order — any fixed slot
+// order is fine for dot products as long as every SNP uses the same one).  Bytes past the row are
+// 01 pairs ("missing"), and each run rewrites the last byte from its saved original so that only the
+// bit pairs that are individuals for that run's order (reference: high pairs first; PLINK: low
+// pairs) stay and the rest read as missing — which contributes nothing to any dot product.
 __device__ __forceinline__ void count_codes(uint32_t word, int& c0, int& c1, int& c2) {
     const uint32_t hi = (word >> 1) & 0x55555555u, lo = word & 0x55555555u;
     c0 += __popc(~hi & ~lo & 0x55555555u);  // 00 hom A1
@@ -40,49 +42,52 @@ __device__ __forceinline__ void count_codes(uint32_t word, int& c0, int& c1, int
     c2 += __popc(hi & lo);                  // 11 hom A2
 }
 
-// One workgroup per SNP row; each thread builds 16-byte output chunks.  Interior chunks come from
-// 4-byte aligned loads of the (unaligned) .bed row recombined with v_alignbyte; the chunk holding
-// the row's last byte and the padding is built byte by byte.
-__global__ void __launch_bounds__(256) repack_count_kernel(const uint8_t* __restrict__ rows, uint32_t* __restrict__ geno,
-                                                           int n_snp, int nb, int pitch_words, uint32_t tail_keep,
-                                                           int* __restrict__ counts) {
+// After a load: save every row's last byte and fill the padding bytes [nb, row_bytes) with 0x55;
+// rows [n_snp, n_rows) (the last 32-SNP block's padding SNPs) are all 0x55.  One thread per row.
+__global__ void pad_rows_kernel(uint8_t* __restrict__ img, uint8_t* __restrict__ last, int n_snp, int n_rows, int nb,
+                                int row_bytes) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_rows) return;
+    uint8_t* row = img + (size_t)j * (size_t)row_bytes;
+    if (j < n_snp) {
+        last[j] = row[nb - 1];
+        for (int p = nb; p < row_bytes; ++p) row[p] = 0x55;
+    } else {
+        for (int p = 0; p < row_bytes; ++p) row[p] = 0x55;
+    }
+}
+
+// Per run: genotype-code counts of every row (one workgroup per SNP, 16-byte loads) with the last
+// byte set to this run's individuals: (saved byte & keep) | (0x55 & ~keep).  HBM-bound read of the
+// image; the thread that owns the last byte's chunk counts the patched value and writes it back.
+__global__ void __launch_bounds__(256) count_rows_kernel(uint8_t* __restrict__ img, const uint8_t* __restrict__ last,
+                                                         int n_snp, int nb, int row_bytes, uint32_t tail_keep,
+                                                         int* __restrict__ counts) {
     const int j = blockIdx.x;
     if (j >= n_snp) return;
-    const uint8_t* src = rows + (size_t)j * (size_t)nb;
-    uint4* dst = reinterpret_cast<uint4*>(geno + (size_t)j * (size_t)pitch_words);
-    const int n_chunks = pitch_words / 4;
-    const uintptr_t sa = reinterpret_cast<uintptr_t>(src);
-    const uint32_t off = (uint32_t)(sa & 3u);
-    const uint32_t* base = reinterpret_cast<const uint32_t*>(sa - off);  // aligned, >= the buffer start
-    // chunk c reads aligned dwords base[4c .. 4c+4]; safe while they end before the row's last byte
-    const int fast_end = (int)(((long long)nb - 1 + off - 20) / 16) + 1;  // chunks c < fast_end are interior
+    uint8_t* row = img + (size_t)j * (size_t)row_bytes;
+    const uint4* src = reinterpret_cast<const uint4*>(row);
+    const int n_chunks = row_bytes / 16, c_last = (nb - 1) / 16;
     int c0 = 0, c1 = 0, c2 = 0;
-    for (int c = threadIdx.x; c < n_chunks; c += blockDim.x) {
-        uint4 o;
-        if (c < fast_end && 16 * c + 20 <= nb - 1 + (int)off) {
-            const uint32_t d0 = base[4 * c], d1 = base[4 * c + 1], d2 = base[4 * c + 2], d3 = base[4 * c + 3],
-                           d4 = base[4 * c + 4];
-            o.x = __builtin_amdgcn_alignbyte(d1, d0, off);
-            o.y = __builtin_amdgcn_alignbyte(d2, d1, off);
-            o.z = __builtin_amdgcn_alignbyte(d3, d2, off);
-            o.w = __builtin_amdgcn_alignbyte(d4, d3, off);
-        } else {
-            uint32_t wv[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                uint32_t word = 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int p = 16 * c + 4 * q + k;
-                    uint32_t b = p < nb ? (uint32_t)src[p] : 0x55u;
-                    if (p == nb - 1) b = (b & tail_keep) | (0x55u & ~tail_keep);
-                    word |= b << (8 * k);
-                }
-                wv[q] = word;
-            }
-            o = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+    const int T = blockDim.x;
+    int c = threadIdx.x;
+    for (; c + 3 * T < n_chunks; c += 4 * T) {  // 4 loads in flight; the last byte's chunk is left to the tail loop
+        if (c_last >= c && c_last - c < 4 * T && (c_last - c) % T == 0) break;
+        const uint4 a = src[c], b = src[c + T], d = src[c + 2 * T], f = src[c + 3 * T];
+        count_codes(a.x, c0, c1, c2); count_codes(a.y, c0, c1, c2); count_codes(a.z, c0, c1, c2); count_codes(a.w, c0, c1, c2);
+        count_codes(b.x, c0, c1, c2); count_codes(b.y, c0, c1, c2); count_codes(b.z, c0, c1, c2); count_codes(b.w, c0, c1, c2);
+        count_codes(d.x, c0, c1, c2); count_codes(d.y, c0, c1, c2); count_codes(d.z, c0, c1, c2); count_codes(d.w, c0, c1, c2);
+        count_codes(f.x, c0, c1, c2); count_codes(f.y, c0, c1, c2); count_codes(f.z, c0, c1, c2); count_codes(f.w, c0, c1, c2);
+    }
+    for (; c < n_chunks; c += T) {
+        uint4 o = src[c];
+        if (c == c_last) {
+            const uint32_t b = ((uint32_t)last[j] & tail_keep) | (0x55u & ~tail_keep);
+            const int q = ((nb - 1) & 15) >> 2, sh = 8 * ((nb - 1) & 3);
+            uint32_t* w = q == 0 ? &o.x : q == 1 ? &o.y : q == 2 ? &o.z : &o.w;
+            *w = (*w & ~(0xFFu << sh)) | (b << sh);
+            row[nb - 1] = (uint8_t)b;
         }
-        dst[c] = o;
         count_codes(o.x, c0, c1, c2);
         count_codes(o.y, c0, c1, c2);
         count_codes(o.z, c0, c1, c2);
@@ -673,6 +678,9 @@ constexpr int E8M0_ONE = 127;  // block scale 2^0
 #ifndef NLDSC_F4_VPM
 #define NLDSC_F4_VPM 5  // VALU instructions interleaved after each MFMA of a one-column-block item
 #endif
+#ifndef NLDSC_F4_PF
+#define NLDSC_F4_PF 2   // chunk buffers per strip in the fp4 K loop (4: deeper prefetch, rows padded to 128 B)
+#endif
 
 struct F4Frag {
     i32x4 x, h, o;
@@ -847,6 +855,72 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
             mfmas(a1, b1);  // K step 2t+1
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
+    } else if constexpr (NLDSC_F4_PF == 4 && SYNC == 0) {
+    // four chunk buffers per strip (rows padded to 128 bytes, n_it % 4 == 0): chunk t+4 is requested
+    // right after chunk t's first K step and decoded six K steps later
+    uint4 r0 = rowp[0], r1 = rowp[2], r2 = rowp[4], r3 = rowp[6], c0[NC], c1[NC], c2[NC], c3[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) { c0[c] = colp[c][0]; c1[c] = colp[c][2]; c2[c] = colp[c][4]; c3[c] = colp[c][6]; }
+    F4Frag a0 = decode_f4(r0.x, r0.y), a1, b0[NC], b1[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) b0[c] = decode_f4(c0[c].x, c0[c].y);
+    // one iteration = chunks t .. t+3 (8 K steps); `ld(p, k)` fetches chunk k of a strip into the
+    // buffer just drained, and the sched_barrier keeps the scheduler from sinking it toward its use
+    auto iter4 = [&](int t, auto ld) {
+        a1 = decode_f4(r0.z, r0.w);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) b1[c] = decode_f4(c0[c].z, c0[c].w);
+        mfmas(a0, b0);  // chunk t, words 0-1
+        r0 = ld(rowp, t + 4);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) c0[c] = ld(colp[c], t + 4);
+        __builtin_amdgcn_sched_barrier(0);
+        a0 = decode_f4(r1.x, r1.y);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) b0[c] = decode_f4(c1[c].x, c1[c].y);
+        mfmas(a1, b1);  // chunk t, words 2-3
+        a1 = decode_f4(r1.z, r1.w);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) b1[c] = decode_f4(c1[c].z, c1[c].w);
+        mfmas(a0, b0);  // chunk t+1, words 0-1
+        r1 = ld(rowp, t + 5);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) c1[c] = ld(colp[c], t + 5);
+        __builtin_amdgcn_sched_barrier(0);
+        a0 = decode_f4(r2.x, r2.y);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) b0[c] = decode_f4(c2[c].x, c2[c].y);
+        mfmas(a1, b1);  // chunk t+1, words 2-3
+        a1 = decode_f4(r2.z, r2.w);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) b1[c] = decode_f4(c2[c].z, c2[c].w);
+        mfmas(a0, b0);  // chunk t+2, words 0-1
+        r2 = ld(rowp, t + 6);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) c2[c] = ld(colp[c], t + 6);
+        __builtin_amdgcn_sched_barrier(0);
+        a0 = decode_f4(r3.x, r3.y);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) b0[c] = decode_f4(c3[c].x, c3[c].y);
+        mfmas(a1, b1);  // chunk t+2, words 2-3
+        a1 = decode_f4(r3.z, r3.w);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) b1[c] = decode_f4(c3[c].z, c3[c].w);
+        mfmas(a0, b0);  // chunk t+3, words 0-1
+        r3 = ld(rowp, t + 7);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) c3[c] = ld(colp[c], t + 7);
+        __builtin_amdgcn_sched_barrier(0);
+        a0 = decode_f4(r0.x, r0.y);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) b0[c] = decode_f4(c0[c].x, c0[c].y);
+        mfmas(a1, b1);  // chunk t+3, words 2-3
+    };
+    auto ld_in = [](const uint4* p, int k) -> uint4 { return p[2 * k]; };
+    auto ld_clamp = [last](const uint4* p, int k) -> uint4 { return p[2 * min(k, last)]; };
+    int t = 0;
+    for (; t + 8 < n_it; t += 4) iter4(t, ld_in);  // fetches chunks <= t + 7 < n_it
+    for (; t < n_it; t += 4) iter4(t, ld_clamp);   // last iteration: nothing left to fetch (clamped dummies)
     } else {
     uint4 pr = rowp[0], qr = rowp[2], pc[NC], qc[NC];
 #pragma unroll
@@ -1205,11 +1279,19 @@ __global__ void __launch_bounds__(256) synth_bed_kernel(uint8_t* __restrict__ ro
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
-hipError_t launch_repack_count(const uint8_t* rows, uint32_t* geno, int n_snp, int nb, int pitch_words,
-                               uint32_t tail_keep, int* counts, hipStream_t st) {
+hipError_t launch_pad_rows(uint8_t* img, uint8_t* last, int n_snp, int n_rows, int nb, int row_bytes,
+                           hipStream_t st) {
+    if (n_rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pad_rows_kernel, dim3((n_rows + 255) / 256), dim3(256), 0, st, img, last, n_snp, n_rows, nb,
+                       row_bytes);
+    return hipGetLastError();
+}
+
+hipError_t launch_count_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
+                             int* counts, hipStream_t st) {
     if (n_snp <= 0) return hipSuccess;
-    hipLaunchKernelGGL(repack_count_kernel, dim3(n_snp), dim3(256), 0, st, rows, geno, n_snp, nb, pitch_words,
-                       tail_keep, counts);
+    hipLaunchKernelGGL(count_rows_kernel, dim3(n_snp), dim3(256), 0, st, img, last, n_snp, nb, row_bytes, tail_keep,
+                       counts);
     return hipGetLastError();
 }
 

@@ -41,6 +41,32 @@ def shard_ranges(positions: np.ndarray, ld_wind: float, world: int) -> list[tupl
     return [(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:])]
 
 
+def halo_range(positions: np.ndarray, ld_wind: float, own: tuple[int, int]) -> tuple[int, int]:
+    """SNP rows [a, b) a GPU loads to compute its owned range [lo, hi): the owned SNPs plus every SNP
+    within one window of them.  Exact only when every position is non-negative and
+    sorted — then the reference's neighbours of SNP j are exactly the MAF-passing SNPs with
+    |pos_k - pos_j| <= w (its ChunkwiseReader pointers, stream.h:131-155,182-197, never lag or stop
+    early).  Anything else (unused SNPs with pos < 0, unsorted positions) needs the reference's
+    sequential pointer history: load the whole chromosome, (0, n)."""
+    pos = np.asarray(positions, dtype=np.float64)
+    n = len(pos)
+    lo, hi = own
+    if hi <= lo:
+        return lo, lo
+    if n == 0 or (pos < 0).any() or (np.diff(pos) < 0).any():
+        return 0, n
+    # a few ulps of slack: the kernels test |pos_k - pos_j| <= w, not pos_k >= pos_j - w (extra rows are harmless)
+    eps = 8.0 * np.finfo(np.float64).eps * (float(pos[-1]) + abs(ld_wind))
+    a = int(np.searchsorted(pos, pos[lo] - ld_wind - eps, side="left"))
+    b = int(np.searchsorted(pos, pos[hi - 1] + ld_wind + eps, side="right"))
+    return min(a, lo), max(b, hi)
+
+
+def empty_result(n_snp: int) -> dict:
+    return {k: (np.full(n_snp, np.nan) if k in RESULT_KEYS[:4] else np.full(n_snp, -1, np.int32))
+            for k in RESULT_KEYS}
+
+
 def assign_units(work: Sequence[float], world: int) -> list[list[int]]:
     """LPT: unit indices per rank, heaviest units first onto the least loaded rank."""
     load = np.zeros(world)
@@ -73,8 +99,7 @@ def gather_ranges(local: dict, own: tuple[int, int], n_snp: int, *, device=None)
     dist.all_gather(parts, t)
     if rank != 0:
         return None
-    full = {k: (np.full(n_snp, np.nan) if k in RESULT_KEYS[:4] else np.full(n_snp, -1, np.int32))
-            for k in RESULT_KEYS}
+    full = empty_result(n_snp)
     for s, part in zip(spans, parts):
         a, b = int(s[0]), int(s[1])
         arr = part.cpu().numpy()
@@ -96,10 +121,22 @@ def calculate_sharded(load_and_run: Callable[[tuple[int, int]], dict], positions
 
 def engine_runner(bed_path: str, n_snp: int, n_org: int, ld_wind: float, maf: float, std_thr: float,
                   rsq_thr: float, positions: np.ndarray, *, flags: int = 0, device: int = 0):
-    """`load_and_run` for calculate_sharded backed by this rank's GPU engine."""
+    """`load_and_run` for calculate_sharded backed by this rank's GPU engine: the rank reads only its
+    `halo_range` of the .bed (one window around its owned SNPs) and computes the owned SNPs on that
+    slice; rsq_thr stays the whole chromosome's (1/M)."""
+    pos = np.asarray(positions, dtype=np.float64)
+
     def run(own):
         from .engine import Engine
+        res = empty_result(n_snp)
+        lo, hi = own
+        if hi <= lo:
+            return res
+        a, b = halo_range(pos, ld_wind, own)
         with Engine(device) as e:
-            e.load_bed_file(bed_path, n_snp, n_org)
-            return e.run(ld_wind, maf, std_thr, rsq_thr, positions, own=own, flags=flags)
+            e.load_bed_file_range(bed_path, n_snp, n_org, a, b)
+            part = e.run(ld_wind, maf, std_thr, rsq_thr, pos[a:b], own=(lo - a, hi - a), flags=flags)
+        for k in RESULT_KEYS:
+            res[k][lo:hi] = part[k][lo - a:hi - a]
+        return res
     return run

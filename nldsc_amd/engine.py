@@ -46,6 +46,13 @@ class Engine:
         _lib.check(self._L.nldsc_engine_load_bed_file(self._h, path.encode(), n_snp, n_org, err, len(err)), err)
         self.n_snp, self.n_org = n_snp, n_org
 
+    def load_bed_file_range(self, path: str, n_snp_file: int, n_org: int, begin: int, end: int):
+        """Rows [begin, end) of a .bed file of n_snp_file SNPs (position sharding: own range + halo)."""
+        err = _lib.errbuf()
+        _lib.check(self._L.nldsc_engine_load_bed_file_range(self._h, path.encode(), n_snp_file, n_org, int(begin),
+                                                               int(end), err, len(err)), err)
+        self.n_snp, self.n_org = int(end) - int(begin), n_org
+
     def load_bed_bytes(self, bed, n_snp: int, n_org: int):
         """`bed`: the whole .bed content (bytes / uint8 numpy array), magic included."""
         buf = np.frombuffer(bed, dtype=np.uint8) if isinstance(bed, (bytes, bytearray)) else np.ascontiguousarray(bed, np.uint8)
@@ -86,7 +93,7 @@ class Engine:
         nl = ctypes.c_int32()
         self._L.nldsc_engine_timings(self._h, ms, ctypes.byref(flop), ctypes.byref(issued), ctypes.byref(pairs),
                                         ctypes.byref(nl))
-        keys = ("repack_ms", "stats_ms", "schedule_ms", "band_ms", "finalize_ms", "total_ms")
+        keys = ("count_ms", "stats_ms", "schedule_ms", "band_ms", "finalize_ms", "total_ms")
         d = {k: ms[i] for i, k in enumerate(keys)}
         d.update(flop_alg=flop.value, flop_issued=issued.value, pairs=pairs.value, band_items=nl.value)
         ex, ops = ctypes.c_int32(), ctypes.c_double()

@@ -264,3 +264,52 @@ def test_heavy_maf_failure_both_schedule_paths(engine, order):
         got = engine.run(1.0, 0.2, 1e-5, 0.01, pos, flags=MODES[mode])
         assert_ld_close(got, exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
                                            maf=(0.0, 0.0)), label=f"{order} {mode}")
+
+
+def test_resident_image_survives_alternating_orders(engine):
+    """The resident rows are counted in place and each run rewrites their last byte from the saved original
+    for its own sample order, so compat / strict / compat runs on one loaded image equal fresh loads."""
+    for name in ("n1001", "n1003"):
+        bed, pos, meta, orc, f64 = load_set(name)
+        args = (meta["ld_wind"], meta["maf"], meta["std_thr"], meta["rsq_thr"], pos)
+        engine.load_bed_bytes(bed, meta["n_snp"], meta["n_org"])
+        a = engine.run(*args)
+        s1 = engine.run(*args, flags=_lib_flag("FLAG_STRICT_PLINK_ORDER"))
+        b = engine.run(*args)
+        engine.load_bed_bytes(bed, meta["n_snp"], meta["n_org"])
+        s2 = engine.run(*args, flags=_lib_flag("FLAG_STRICT_PLINK_ORDER"))
+        same_gram(a, b, name)
+        same_gram(s1, s2, name + " strict")
+        assert not np.array_equal(a["l2_ws"], s1["l2_ws"]) or not np.allclose(a["l2"], s1["l2"], equal_nan=True)
+
+
+def _lib_flag(name):
+    from nldsc_amd import _lib
+    return getattr(_lib, name)
+
+
+def test_halo_loaded_shards_assemble_to_full(engine, tmp_path):
+    """Position sharding as the torchrun driver runs it: each rank loads only its halo range of the .bed
+    file (nldsc_engine_load_bed_file_range) and computes its owned SNPs; the assembled table equals the
+    single-GPU run on the whole file."""
+    from nldsc_amd import distributed as D
+    from nldsc_amd import synth
+    N, M = 1003, 900
+    spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=12.0, seed=44, missing=0.02)
+    synth.write_plink(str(tmp_path / "c"), spec)
+    pos = synth.positions_cm(spec)
+    args = (1.0, 0.01, 1e-5, 1.0 / M)
+    engine.load_bed_file(str(tmp_path / "c.bed"), M, N)
+    full = engine.run(*args, pos)
+    run = D.engine_runner(str(tmp_path / "c.bed"), M, N, *args, pos, device=0)
+    got = D.empty_result(M)
+    for own in D.shard_ranges(pos, 1.0, 4):
+        a, b = D.halo_range(pos, 1.0, own)
+        assert b - a < M
+        part = run(own)
+        for k in got:
+            got[k][own[0]:own[1]] = part[k][own[0]:own[1]]
+    for k in ("l2_ws", "l2d_ws", "l2d_wse", "maf", "residuals_std"):
+        np.testing.assert_array_equal(got[k], full[k], err_msg=k)
+    for k in ("l2", "l2d"):
+        np.testing.assert_allclose(got[k], full[k], rtol=1e-12, atol=1e-13, equal_nan=True, err_msg=k)

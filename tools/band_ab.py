@@ -9,7 +9,8 @@ ABI).  Tokens: wpsW, ncC (fp32 path), i8 (exact path), i8nc2, tile (exact path o
 xcd (XCD-contiguous item order), f4 (exact path on fp4 MFMAs), f4nc2 (fp4 items of two column
 blocks), roundR (R fp4 items per launch; round-1 = one launch per round of resident waves), grpS (fp4 on
 4-wave workgroups of skewed 2x2 tiles, a barrier every S chunk pairs; grp0: no barriers), ringD (fp4
-strips through a D-deep per-wave LDS ring filled by LDS-DMA).
+strips through a D-deep per-wave LDS ring filled by LDS-DMA), nodirect (fp4 path on the repacked copy instead
+of the .bed rows in place).
 """
 import argparse
 import json
@@ -65,6 +66,7 @@ def main():
         os.environ["NLDSC_BAND_F4_RING"] = ring[0] if ring else "0"
         rnd = [p[5:] for p in parts if p.startswith("round")]
         os.environ["NLDSC_BAND_ROUND"] = rnd[0] if rnd else "0"
+        os.environ["NLDSC_DIRECT"] = "0" if "nodirect" in parts else "1"
         e = Engine(0, lib_path=lib)
         v = label
         e.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
@@ -86,7 +88,10 @@ def main():
         band = [t["band_ms"] for t in ts]
         fa, fi = ts[-1]["flop_alg"], ts[-1]["flop_issued"]
         med = float(np.median(band))
-        summary[v] = dict(band_ms_median=med, band_ms_min=float(min(band)), alg_tflops=fa / med / 1e9,
+        summary[v] = dict(band_ms_median=med, band_ms_min=float(min(band)),
+                          total_ms_median=float(np.median([t["total_ms"] for t in ts])),
+                          count_ms_median=float(np.median([t["count_ms"] for t in ts])),
+                          alg_tflops=fa / med / 1e9,
                           issued_tflops=fi / med / 1e9, items=ts[-1]["band_items"],
                           alg_over_issued=fa / fi,
                           max_abs_l2_vs_first=float(np.nanmax(np.abs(outs[v]["l2"] - ref["l2"]))),
