@@ -27,11 +27,8 @@ namespace {
 
 constexpr int BLK = 32;             // SNPs per MFMA block
 constexpr int CHUNK_BYTES = 32;     // one K-loop chunk of a 2-bit row (16 B per lane half)
-#ifndef NLDSC_F4_PF
-#define NLDSC_F4_PF 2
-#endif
-// resident row pitch: a multiple of the chunks the fp4 K loop takes per iteration (2 or 4 x 32 bytes)
-constexpr int ROW_ALIGN_BYTES = NLDSC_F4_PF == 4 ? 128 : 64;
+// resident row pitch: an even number of 32-byte chunks (the fp4 K loop takes two per iteration)
+constexpr int ROW_ALIGN_BYTES = 64;
 
 // resident layout of a .bed image: row j of ceil(N/4) bytes at j * row_bytes, n_rows = M rounded up to 32
 int row_pitch(int32_t n_org) {
@@ -140,6 +137,7 @@ struct nldsc_engine {
     int f4_grp = -1;         // fp4 path on 4-wave workgroups of skewed 2x2 tiles (NLDSC_BAND_F4_GRP = barrier
                              // period in chunk pairs, 0: no barriers; -1: one wave per block pair)
     int f4_ring = 0;         // fp4 strips through a per-wave LDS ring of this depth (NLDSC_BAND_F4_RING, 0: registers)
+    int tile_r = 16, tile_c = 16;  // item order: tiles of R row blocks x C diagonal offsets (NLDSC_TILE_R/C; R <= 1: row-major)
     int band_round = 0;      // exact-path items per launch (NLDSC_BAND_ROUND; 0: one launch, -1: one
                              // launch per round of resident waves)
     int n_cu = 256;
@@ -294,6 +292,32 @@ void plan_items(const double* pos, const uint8_t* flags, int M, double w, const 
     out.insert(out.end(), ones.begin(), ones.end());
 }
 
+// Reorder single-block-pair items (row-major by I, then J) into tiles of R row blocks x C diagonal
+// offsets d = J - I: tile (I / R, d / C), then I, then J.  The launch hands each XCD a contiguous
+// run of the list, so the waves resident on one XCD at a time work on about R row strips and R + C
+// column strips, each reused ~R or ~C times from that XCD's L2.  Row-major order (R = 1) is as good
+// for narrow bands (C3: d <= 10) and poor for wide ones (C5: d <= ~220, a column strip is read by
+// ~2 resident waves): 16 x 16 tiles cut the C5 band kernel by 8.5 % (profiles/r01_ab_tiles_c5.json).
+void order_items_tiled(std::vector<int4>& items, int nblk, int R, int C, std::vector<int4>& scratch) {
+    if (R <= 1 || items.empty()) return;
+    std::vector<int> first(nblk + 1, 0);  // items of row block I: [first[I], first[I+1])
+    int dmax = 0;
+    for (const int4& it : items) {
+        ++first[it.x + 1];
+        dmax = std::max(dmax, it.y - it.x);
+    }
+    if (dmax < 2 * C) return;  // narrow band: row-major is as good (C3, profiles/r01_ab_tiles_c3.json)
+    for (int I = 0; I < nblk; ++I) first[I + 1] += first[I];
+    std::vector<int> cur(first.begin(), first.end() - 1);  // next unread item of each row block
+    scratch.clear();
+    scratch.reserve(items.size());
+    for (int t0 = 0; t0 < nblk; t0 += R)
+        for (int c0 = 0; c0 <= dmax; c0 += C)
+            for (int I = t0; I < std::min(nblk, t0 + R); ++I)
+                for (int& k = cur[I]; k < first[I + 1] && items[k].y - I < c0 + C; ++k) scratch.push_back(items[k]);
+    items.swap(scratch);
+}
+
 // Skewed 2x2 tiles of the exact path (band_tile_kernel) from the single-block-pair items: pair
 // (a, b), a <= b, goes to tile I = a & ~1, J = I + 2 * ((b - a) >> 1), wave 2 (a - I) + ((b - a) & 1)
 // (waves: (I, J), (I, J+1), (I+1, J+1), (I+1, J+2)).  Each pair lands in exactly one tile slot.
@@ -368,6 +392,8 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_BAND_TILE")) e->band_tile = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_XCD")) e->xcd = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_BAND_ROUND")) e->band_round = std::atoi(v);
+    if (const char* v = std::getenv("NLDSC_TILE_R")) e->tile_r = std::atoi(v);
+    if (const char* v = std::getenv("NLDSC_TILE_C")) e->tile_c = std::max(1, std::atoi(v));
     if (const char* v = std::getenv("NLDSC_BAND_F4_GRP")) e->f4_grp = std::atoi(v);
     if (const char* v = std::getenv("NLDSC_BAND_F4_RING")) e->f4_ring = std::atoi(v);
     {
@@ -609,6 +635,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         if (it.x < 0 || it.y < it.x || (it.z != 1 && it.z != 2) || it.y + it.z > nblk)
             return set_err(err, errlen, NLDSC_E_ARG, "internal: bad work item (%d, %d, %d) for %d blocks", it.x,
                            it.y, it.z, nblk);
+    if (max_nc == 1 && !tiled) order_items_tiled(e->h_items, nblk, e->tile_r, e->tile_c, e->h_ones);
     if (tiled) {
         e->h_ones.swap(e->h_items);
         plan_tiles(e->h_ones, nblk, e->h_items);

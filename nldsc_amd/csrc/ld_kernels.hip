@@ -678,9 +678,6 @@ constexpr int E8M0_ONE = 127;  // block scale 2^0
 #ifndef NLDSC_F4_VPM
 #define NLDSC_F4_VPM 5  // VALU instructions interleaved after each MFMA of a one-column-block item
 #endif
-#ifndef NLDSC_F4_PF
-#define NLDSC_F4_PF 2   // chunk buffers per strip in the fp4 K loop (4: deeper prefetch, rows padded to 128 B)
-#endif
 
 struct F4Frag {
     i32x4 x, h, o;
@@ -855,72 +852,6 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
             mfmas(a1, b1);  // K step 2t+1
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
-    } else if constexpr (NLDSC_F4_PF == 4 && SYNC == 0) {
-    // four chunk buffers per strip (rows padded to 128 bytes, n_it % 4 == 0): chunk t+4 is requested
-    // right after chunk t's first K step and decoded six K steps later
-    uint4 r0 = rowp[0], r1 = rowp[2], r2 = rowp[4], r3 = rowp[6], c0[NC], c1[NC], c2[NC], c3[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) { c0[c] = colp[c][0]; c1[c] = colp[c][2]; c2[c] = colp[c][4]; c3[c] = colp[c][6]; }
-    F4Frag a0 = decode_f4(r0.x, r0.y), a1, b0[NC], b1[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) b0[c] = decode_f4(c0[c].x, c0[c].y);
-    // one iteration = chunks t .. t+3 (8 K steps); `ld(p, k)` fetches chunk k of a strip into the
-    // buffer just drained, and the sched_barrier keeps the scheduler from sinking it toward its use
-    auto iter4 = [&](int t, auto ld) {
-        a1 = decode_f4(r0.z, r0.w);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) b1[c] = decode_f4(c0[c].z, c0[c].w);
-        mfmas(a0, b0);  // chunk t, words 0-1
-        r0 = ld(rowp, t + 4);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) c0[c] = ld(colp[c], t + 4);
-        __builtin_amdgcn_sched_barrier(0);
-        a0 = decode_f4(r1.x, r1.y);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) b0[c] = decode_f4(c1[c].x, c1[c].y);
-        mfmas(a1, b1);  // chunk t, words 2-3
-        a1 = decode_f4(r1.z, r1.w);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) b1[c] = decode_f4(c1[c].z, c1[c].w);
-        mfmas(a0, b0);  // chunk t+1, words 0-1
-        r1 = ld(rowp, t + 5);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) c1[c] = ld(colp[c], t + 5);
-        __builtin_amdgcn_sched_barrier(0);
-        a0 = decode_f4(r2.x, r2.y);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) b0[c] = decode_f4(c2[c].x, c2[c].y);
-        mfmas(a1, b1);  // chunk t+1, words 2-3
-        a1 = decode_f4(r2.z, r2.w);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) b1[c] = decode_f4(c2[c].z, c2[c].w);
-        mfmas(a0, b0);  // chunk t+2, words 0-1
-        r2 = ld(rowp, t + 6);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) c2[c] = ld(colp[c], t + 6);
-        __builtin_amdgcn_sched_barrier(0);
-        a0 = decode_f4(r3.x, r3.y);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) b0[c] = decode_f4(c3[c].x, c3[c].y);
-        mfmas(a1, b1);  // chunk t+2, words 2-3
-        a1 = decode_f4(r3.z, r3.w);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) b1[c] = decode_f4(c3[c].z, c3[c].w);
-        mfmas(a0, b0);  // chunk t+3, words 0-1
-        r3 = ld(rowp, t + 7);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) c3[c] = ld(colp[c], t + 7);
-        __builtin_amdgcn_sched_barrier(0);
-        a0 = decode_f4(r0.x, r0.y);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) b0[c] = decode_f4(c0[c].x, c0[c].y);
-        mfmas(a1, b1);  // chunk t+3, words 2-3
-    };
-    auto ld_in = [](const uint4* p, int k) -> uint4 { return p[2 * k]; };
-    auto ld_clamp = [last](const uint4* p, int k) -> uint4 { return p[2 * min(k, last)]; };
-    int t = 0;
-    for (; t + 8 < n_it; t += 4) iter4(t, ld_in);  // fetches chunks <= t + 7 < n_it
-    for (; t < n_it; t += 4) iter4(t, ld_clamp);   // last iteration: nothing left to fetch (clamped dummies)
     } else {
     uint4 pr = rowp[0], qr = rowp[2], pc[NC], qc[NC];
 #pragma unroll

@@ -9,8 +9,8 @@ ABI).  Tokens: wpsW, ncC (fp32 path), i8 (exact path), i8nc2, tile (exact path o
 xcd (XCD-contiguous item order), f4 (exact path on fp4 MFMAs), f4nc2 (fp4 items of two column
 blocks), roundR (R fp4 items per launch; round-1 = one launch per round of resident waves), grpS (fp4 on
 4-wave workgroups of skewed 2x2 tiles, a barrier every S chunk pairs; grp0: no barriers), ringD (fp4
-strips through a D-deep per-wave LDS ring filled by LDS-DMA), nodirect (fp4 path on the repacked copy instead
-of the .bed rows in place).
+strips through a D-deep per-wave LDS ring filled by LDS-DMA), trR / tcC (item order: tiles of R row blocks x C
+diagonal offsets; tr1 = row-major).
 """
 import argparse
 import json
@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--n-snp", type=int, default=20_000)
     ap.add_argument("--length-cm", type=float, default=70.0)
     ap.add_argument("--variants", default="wps1:nc2,wps2:nc2,wps2:nc1,wps1:nc1")
+    ap.add_argument("--window", type=float, default=1.0, help="window in position units (C5: 1e6 bp)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--major", action="store_true",
                     help="swap hom-A1/hom-A2 codes of every SNP (.bim A2 = the major allele, as in PLINK's usual "
@@ -66,7 +67,10 @@ def main():
         os.environ["NLDSC_BAND_F4_RING"] = ring[0] if ring else "0"
         rnd = [p[5:] for p in parts if p.startswith("round")]
         os.environ["NLDSC_BAND_ROUND"] = rnd[0] if rnd else "0"
-        os.environ["NLDSC_DIRECT"] = "0" if "nodirect" in parts else "1"
+        tr = [p[2:] for p in parts if p.startswith("tr")]
+        tc = [p[2:] for p in parts if p.startswith("tc")]
+        os.environ["NLDSC_TILE_R"] = tr[0] if tr else "16"
+        os.environ["NLDSC_TILE_C"] = tc[0] if tc else "16"
         e = Engine(0, lib_path=lib)
         v = label
         e.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
@@ -77,7 +81,7 @@ def main():
     outs = {}
     for r in range(args.rounds + 1):
         for v, e in engines.items():
-            o = e.run(1.0, 1e-4, 1e-5, 1.0 / M, pos)
+            o = e.run(args.window, 1e-4, 1e-5, 1.0 / M, pos)
             t = e.timings()
             if r > 0:
                 res[v].append(t)
