@@ -104,6 +104,7 @@ struct nldsc_engine {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[6] = {};
+    hipEvent_t ev_plan = nullptr;  // GPU plan counters landed in h_meta
     // resident .bed image
     DevBuf<uint8_t> bed;
     DevBuf<uint8_t> lastb;  // each row's original last byte (the per-run count kernel masks a copy of it)
@@ -121,6 +122,10 @@ struct nldsc_engine {
     std::vector<int> h_L, h_R;
     std::vector<int4> h_items;
     HostPinned h_stage;  // pinned upload staging of the plan (L, R, items)
+    HostPinned h_meta;   // GPU plan counters (items, diagonal items)
+    DevBuf<int> Ew, plan_counts, plan_meta;
+    DevBuf<int2> plan_rows;
+    bool gpu_plan = true;  // band schedule on the GPU for non-negative sorted positions (NLDSC_GPU_PLAN=0: host)
     // timings of the last run
     double ms[6] = {0, 0, 0, 0, 0, 0};
     double flop_alg = 0, flop_issued = 0, pairs = 0, ops_alg_i8 = 0;
@@ -149,6 +154,8 @@ struct nldsc_engine {
         ws3.release(); lut.release(); cst.release(); sflags.release(); pos.release(); maf.release(); rstd.release();
         l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+        if (ev_plan) (void)hipEventDestroy(ev_plan);
+        Ew.release(); plan_counts.release(); plan_meta.release(); plan_rows.release();
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -392,6 +399,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_BAND_TILE")) e->band_tile = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_XCD")) e->xcd = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_BAND_ROUND")) e->band_round = std::atoi(v);
+    if (const char* v = std::getenv("NLDSC_GPU_PLAN")) e->gpu_plan = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_TILE_R")) e->tile_r = std::atoi(v);
     if (const char* v = std::getenv("NLDSC_TILE_C")) e->tile_c = std::max(1, std::atoi(v));
     if (const char* v = std::getenv("NLDSC_BAND_F4_GRP")) e->f4_grp = std::atoi(v);
@@ -404,6 +412,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     for (auto& ev : e->ev)
         if (he == hipSuccess) he = hipEventCreate(&ev);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_plan, hipEventDisableTiming);
     if (he != hipSuccess) {
         delete e;
         return set_err(err, errlen, NLDSC_E_HIP, "HIP error %s creating stream/events", hipGetErrorString(he));
@@ -594,9 +603,30 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     HIPCHK(e->l2d.ensure((size_t)M));
     HIPCHK(e->ws3.ensure((size_t)M * 3));
 
+    // band schedule: on the GPU when every position is >= 0 and sorted (the kernels run ahead of the
+    // count and the host only waits for two counters), else the host replay of the reference's pointers
+    const bool sorted = positions_sorted(p->positions, M);
+    const bool gpu_plan = e->gpu_plan && sorted && max_nc == 1 && !tiled &&
+                          std::all_of(p->positions, p->positions + M, [](double x) { return x >= 0.0; });
+    if (gpu_plan) {
+        const size_t n_t = (size_t)(nblk + 15) / 16;
+        HIPCHK(e->Aw.ensure((size_t)M));
+        HIPCHK(e->Ew.ensure((size_t)M));
+        HIPCHK(e->plan_rows.ensure((size_t)nblk));
+        HIPCHK(e->plan_counts.ensure(n_t * n_t));
+        HIPCHK(e->plan_meta.ensure(4));
+        HIPCHK(e->h_meta.ensure(4 * sizeof(int)));
+    }
+
     auto t_start = std::chrono::steady_clock::now();
     HIPCHK(hipEventRecord(e->ev[0], st));
     HIPCHK(hipMemcpyAsync(e->pos.p, p->positions, sizeof(double) * M, hipMemcpyHostToDevice, st));
+    if (gpu_plan) {
+        HIPCHK(nldsc::launch_plan(e->pos.p, M, p->ld_wind, own_begin, own_end, e->Aw.p, e->Ew.p, e->Rw.p,
+                                  e->plan_rows.p, e->plan_counts.p, e->plan_meta.p, st));
+        HIPCHK(hipMemcpyAsync(e->h_meta.p, e->plan_meta.p, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(e->ev_plan, st));
+    }
     HIPCHK(nldsc::launch_count_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, e->counts.p, st));
     HIPCHK(hipEventRecord(e->ev[1], st));
     HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->cst.p,
@@ -605,9 +635,19 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
 
     // ---- window replay + schedule ----
     auto t_host0 = std::chrono::steady_clock::now();
+    int n_items = 0, n_diag = 0;
+    if (gpu_plan) {
+        HIPCHK(hipEventSynchronize(e->ev_plan));  // the count kernel is running meanwhile
+        const int* meta = reinterpret_cast<const int*>(e->h_meta.p);
+        n_items = meta[1];
+        n_diag = meta[2];
+        HIPCHK(e->items.ensure(std::max<size_t>((size_t)n_items, 1)));
+        if (n_items > 0)
+            HIPCHK(nldsc::launch_plan_emit(M, e->plan_rows.p, e->plan_meta.p, e->plan_counts.p, e->items.p, st));
+        HIPCHK(nldsc::launch_left_pointers(e->Aw.p, e->sflags.p, e->pos.p, M, e->Lw.p, st));
+    } else {
     e->h_L.resize(M);
     e->h_R.resize(M);
-    const bool sorted = positions_sorted(p->positions, M);
     if (sorted) {
         // Sorted positions: nothing waits for the GPU.  The right pointers and the all-pass left
         // pointers do not depend on the MAF flags, and SNPs failing MAF only shrink the set of needed
@@ -661,27 +701,29 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     }
     HIPCHK(hipMemcpyAsync(e->Rw.p, e->h_stage.p + bL, bL, hipMemcpyHostToDevice, st));
     if (bI) HIPCHK(hipMemcpyAsync(e->items.p, e->h_stage.p + 2 * bL, bI, hipMemcpyHostToDevice, st));
+    n_items = (int)e->h_items.size();
+    for (const int4& it : tiled ? e->h_ones : e->h_items) n_diag += it.x == it.y;
+    }
     HIPCHK(hipMemsetAsync(e->l2_acc.p, 0, sizeof(double) * M, st));
     HIPCHK(hipMemsetAsync(e->l2d_acc.p, 0, sizeof(double) * M, st));
     HIPCHK(hipMemsetAsync(e->ws_acc.p, 0, sizeof(int) * 3 * (size_t)M, st));
     auto t_host1 = std::chrono::steady_clock::now();
 
     HIPCHK(hipEventRecord(e->ev[3], st));
-    e->n_band_items = (int32_t)e->h_items.size();
+    e->n_band_items = n_items;
     {
-        double products = 0;  // 32x32 block products issued per sample slot
-        for (const int4& it : tiled ? e->h_ones : e->h_items) {
-            const bool dg = it.x == it.y;
-            if (use_i8)  // int8 Gram: xx, xo, ox, oo (+ xh, oh, and hx, ho off the diagonal) per column block
-                products += it.z * (dom ? 8.0 : 4.0) - ((dom && dg) ? 2.0 : 0.0);
-            else         // fp32: AA (+ AR, and RA off the diagonal)
-                products += it.z * (dom ? 3.0 : 1.0) - ((dom && dg) ? 1.0 : 0.0);
-        }
+        // 32x32 block products issued per sample slot: exact paths xx, xo, ox, oo (+ xh, oh, and hx, ho
+        // off the diagonal) per block pair; fp32 AA (+ AR, and RA off the diagonal)
+        double blocks = 0;
+        if (gpu_plan) blocks = n_items;
+        else for (const int4& it : tiled ? e->h_ones : e->h_items) blocks += it.z;
+        const double products = use_i8 ? blocks * (dom ? 8.0 : 4.0) - (dom ? 2.0 * n_diag : 0.0)
+                                        : blocks * (dom ? 3.0 : 1.0) - (dom ? 1.0 * n_diag : 0.0);
         e->flop_issued = products * 2.0 * BLK * BLK * (double)row_bytes * 4.0;
     }
-    if (!e->h_items.empty()) {
+    if (n_items > 0) {
         if (f4_grp) {
-            const int n_tiles = (int)e->h_items.size();
+            const int n_tiles = n_items;
             const int per = e->band_round < 0 ? e->n_cu * 2 : e->band_round > 0 ? e->band_round : n_tiles;
             for (int off = 0; off < n_tiles; off += per)
                 HIPCHK(nldsc::launch_band_f4_grp(dom, e->f4_grp, std::min(per, n_tiles - off), geno, pitch_words,
@@ -689,14 +731,13 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
                                                  e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end,
                                                  e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, e->xcd, st));
         } else if (tiled)
-            HIPCHK(nldsc::launch_band_tile(dom, (int)e->h_items.size(), geno, pitch_words, n_it, nblk, e->cst.p,
+            HIPCHK(nldsc::launch_band_tile(dom, n_items, geno, pitch_words, n_it, nblk, e->cst.p,
                                            e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
                                            (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                            e->ws_acc.p, e->xcd, st));
         else if (use_f4) {
             // Items of one launch start together and stream through the samples in near lockstep, so
             // the strips they share stay in their XCD's L2; a round = the waves resident at once.
-            const int n_items = (int)e->h_items.size();
             const int per = e->band_round < 0 ? e->n_cu * 4 * (max_nc == 2 ? 1 : 2)
                           : e->band_round > 0 ? e->band_round : n_items;
             for (int off = 0; off < n_items; off += per)
@@ -714,12 +755,12 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
                                              e->l2d_acc.p, e->ws_acc.p, e->xcd, st));
         }
         else if (use_i8)
-            HIPCHK(nldsc::launch_band_i8(dom, max_nc, (int)e->h_items.size(), geno, pitch_words, n_it, e->cst.p,
+            HIPCHK(nldsc::launch_band_i8(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p,
                                          e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
                                          (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                          e->ws_acc.p, e->xcd, st));
         else
-            HIPCHK(nldsc::launch_band(dom, e->band_wps, (int)e->h_items.size(), geno, pitch_words, n_it,
+            HIPCHK(nldsc::launch_band(dom, e->band_wps, n_items, geno, pitch_words, n_it,
                                       e->lut.p, e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
                                       (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                       e->ws_acc.p, st));

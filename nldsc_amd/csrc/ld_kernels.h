@@ -26,6 +26,13 @@ hipError_t launch_snp_stats(const int* counts, const double* pos, int n_snp, int
                             double* rstd_out, hipStream_t st);
 // exact left pointers L from the all-pass replay's A and the device MAF flags (sorted positions)
 hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const double* pos, int n, int* L, hipStream_t st);
+// band schedule on the GPU for non-negative sorted positions: all-pass left pointers A, window edges E,
+// right pointers R, per-row-block offset ranges `rows` (nblk), tile item offsets `counts` (capacity
+// ceil(nblk/16) * ceil(nblk/16)); meta[1] = items, meta[2] = diagonal items (read after the stream
+// reaches it), then plan_emit writes the items (16 row blocks x 16 offsets tile order)
+hipError_t launch_plan(const double* pos, int n, double w, int own_lo, int own_hi, int* A, int* E, int* R,
+                       int2* rows, int* counts, int* meta, hipStream_t st);
+hipError_t launch_plan_emit(int n, const int2* rows, const int* meta, const int* offsets, int4* items, hipStream_t st);
 hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                        const float2* lut, const int4* items, const double* pos, const int* Lw, const int* Rw,
                        const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,

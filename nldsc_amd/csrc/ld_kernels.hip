@@ -18,6 +18,8 @@
 //   (+) synth_bed_kernel    deterministic synthetic .bed image for benchmarks.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <climits>
+#include <algorithm>
 
 #include "ld_kernels.h"
 
@@ -202,6 +204,134 @@ __global__ void left_pointer_kernel(const int* __restrict__ A, const uint8_t* __
         while (l < j && !((sflags[l] & 1) && pos[l] >= 0.0)) ++l;
     }
     L[j] = l;
+}
+
+// ---- band schedule on the GPU (every position >= 0 and sorted; ld_engine.cpp plan_items is the host
+// reference for any positions).  With all SNPs used, ChunkwiseReader's pointers reduce to window edges
+// (stream.h:142-155,182-197): the all-pass left pointer A_j = first k with pos_j - pos_k <= w, and the
+// right pointer R_j = min(n - 1, max(R_{j-1} + 1, E_j)) with E_j = first k > j with pos_k - pos_j > w
+// (its extend_cache advances at least one SNP per SNP), i.e. R_j = min(n - 1, j + max_{k<=j}(E_k - k)).
+// Row block I needs columns up to E_{i_end} - 1 (its last row's window edge; every later SNP whose
+// window reaches back into I lies before it too).  Items are emitted in tiles of PLAN_R row blocks x
+// PLAN_C diagonal offsets (see order_items_tiled), each tile's items row by row.
+constexpr int PLAN_R = 16, PLAN_C = 16;
+
+__global__ void plan_edges_kernel(const double* __restrict__ pos, int n, double w, int* __restrict__ A,
+                                  int* __restrict__ E) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const double pj = pos[j];
+    int lo = j + 1, hi = n;  // first k in (j, n] with pos_k - pos_j > w (n: none)
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (pos[mid] - pj > w) hi = mid; else lo = mid + 1;
+    }
+    E[j] = lo;
+    lo = 0; hi = j;  // first k in [0, j] with pos_j - pos_k <= w
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (pj - pos[mid] <= w) hi = mid; else lo = mid + 1;
+    }
+    A[j] = lo;
+}
+
+// one workgroup of 1024: R_j = min(n - 1, j + running max of (E_k - k))
+__global__ void __launch_bounds__(1024) plan_right_kernel(const int* __restrict__ E, int n, int* __restrict__ R) {
+    __shared__ int part[1024];
+    const int t = threadIdx.x, per = (n + 1023) / 1024;
+    const int b = min(n, t * per), e = min(n, b + per);
+    int m = INT_MIN;
+    for (int k = b; k < e; ++k) m = max(m, E[k] - k);
+    part[t] = m;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // inclusive max-scan of the chunk maxima
+        const int v = t >= o ? part[t - o] : INT_MIN;
+        __syncthreads();
+        part[t] = max(part[t], v);
+        __syncthreads();
+    }
+    int run = t > 0 ? part[t - 1] : INT_MIN;
+    for (int k = b; k < e; ++k) {
+        run = max(run, E[k] - k);
+        R[k] = min(n - 1, k + run);
+    }
+}
+
+// per row block I: useful column offsets d = J - I, [d0, d1] (empty: d0 > d1); meta[0] = max d1 + 1,
+// meta[2] = diagonal items
+__global__ void plan_rows_kernel(const int* __restrict__ E, const int* __restrict__ A, int n, int nblk, int own_lo,
+                                 int own_hi, int2* __restrict__ rows, int* __restrict__ meta) {
+    const int I = blockIdx.x * blockDim.x + threadIdx.x;
+    if (I >= nblk) return;
+    int2 r = make_int2(1, 0);
+    if (I >= A[own_lo] / 32 && I * 32 < own_hi) {
+        const int i_end = min(n, 32 * I + 32) - 1;
+        const int Jmax = min(nblk - 1, (E[i_end] - 1) / 32);
+        const int ob0 = own_lo / 32, ob1 = (own_hi - 1) / 32;
+        const bool own_row = I >= ob0 && I <= ob1;
+        const int J0 = own_row ? I : max(I, ob0), J1 = own_row ? Jmax : min(Jmax, ob1);
+        r = make_int2(J0 - I, J1 - I);
+    }
+    rows[I] = r;
+    if (r.x <= r.y) {
+        atomicMax(&meta[0], r.y + 1);
+        if (r.x == 0) atomicAdd(&meta[2], 1);
+    }
+}
+
+__device__ __forceinline__ int plan_n_c(const int* meta) { return (meta[0] + PLAN_C - 1) / PLAN_C; }
+
+// per tile (T, c) of PLAN_R row blocks x PLAN_C offsets, in (T, c) order: its item count
+__global__ void plan_count_kernel(const int2* __restrict__ rows, int nblk, const int* __restrict__ meta,
+                                  int* __restrict__ counts) {
+    const int n_t = (nblk + PLAN_R - 1) / PLAN_R, n_c = plan_n_c(meta);
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n_t * n_c; k += gridDim.x * blockDim.x) {
+        const int T = k / n_c, c = k % n_c;
+        int cnt = 0;
+        for (int I = T * PLAN_R; I < min(nblk, T * PLAN_R + PLAN_R); ++I) {
+            const int a = max(rows[I].x, c * PLAN_C), b = min(rows[I].y, c * PLAN_C + PLAN_C - 1);
+            if (a <= b) cnt += b - a + 1;
+        }
+        counts[k] = cnt;
+    }
+}
+
+// one workgroup of 1024: exclusive scan of the tile counts in place; meta[1] = total items
+__global__ void __launch_bounds__(1024) plan_scan_kernel(int* __restrict__ counts, int nblk, int* __restrict__ meta) {
+    __shared__ int part[1024];
+    const int n = (nblk + PLAN_R - 1) / PLAN_R * plan_n_c(meta);
+    const int t = threadIdx.x, per = (n + 1023) / 1024;
+    const int b = min(n, t * per), e = min(n, b + per);
+    int sum = 0;
+    for (int k = b; k < e; ++k) sum += counts[k];
+    part[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int run = t > 0 ? part[t - 1] : 0;
+    for (int k = b; k < e; ++k) {
+        const int c = counts[k];
+        counts[k] = run;
+        run += c;
+    }
+    if (t == 1023) meta[1] = part[1023];
+}
+
+__global__ void plan_emit_kernel(const int2* __restrict__ rows, int nblk, const int* __restrict__ meta,
+                                 const int* __restrict__ offsets, int4* __restrict__ items) {
+    const int n_t = (nblk + PLAN_R - 1) / PLAN_R, n_c = plan_n_c(meta);
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n_t * n_c; k += gridDim.x * blockDim.x) {
+        const int T = k / n_c, c = k % n_c;
+        int o = offsets[k];
+        for (int I = T * PLAN_R; I < min(nblk, T * PLAN_R + PLAN_R); ++I) {
+            const int a = max(rows[I].x, c * PLAN_C), b = min(rows[I].y, c * PLAN_C + PLAN_C - 1);
+            for (int d = a; d <= b; ++d) items[o++] = make_int4(I, I + d, 1, 0);
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1238,6 +1368,27 @@ hipError_t launch_snp_stats(const int* counts, const double* pos, int n_snp, int
 hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const double* pos, int n, int* L, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(left_pointer_kernel, dim3((n + 255) / 256), dim3(256), 0, st, A, sflags, pos, n, L);
+    return hipGetLastError();
+}
+
+hipError_t launch_plan(const double* pos, int n, double w, int own_lo, int own_hi, int* A, int* E, int* R,
+                       int2* rows, int* counts, int* meta, hipStream_t st) {
+    const int nblk = (n + 31) / 32;
+    hipError_t e = hipMemsetAsync(meta, 0, 4 * sizeof(int), st);
+    if (e != hipSuccess || n <= 0 || own_hi <= own_lo) return e;
+    hipLaunchKernelGGL(plan_edges_kernel, dim3((n + 255) / 256), dim3(256), 0, st, pos, n, w, A, E);
+    hipLaunchKernelGGL(plan_right_kernel, dim3(1), dim3(1024), 0, st, E, n, R);
+    hipLaunchKernelGGL(plan_rows_kernel, dim3((nblk + 255) / 256), dim3(256), 0, st, E, A, n, nblk, own_lo, own_hi,
+                       rows, meta);
+    hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, counts);
+    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts, nblk, meta);
+    return hipGetLastError();
+}
+
+hipError_t launch_plan_emit(int n, const int2* rows, const int* meta, const int* offsets, int4* items, hipStream_t st) {
+    const int nblk = (n + 31) / 32;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, offsets, items);
     return hipGetLastError();
 }
 

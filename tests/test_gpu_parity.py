@@ -313,3 +313,46 @@ def test_halo_loaded_shards_assemble_to_full(engine, tmp_path):
         np.testing.assert_array_equal(got[k], full[k], err_msg=k)
     for k in ("l2", "l2d"):
         np.testing.assert_allclose(got[k], full[k], rtol=1e-12, atol=1e-13, equal_nan=True, err_msg=k)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_gpu_schedule_matches_host_schedule(engine, seed):
+    """Non-negative sorted positions take the GPU schedule (window edges by binary search, the drifting
+    right pointer as a prefix max, tile-ordered items by a prefix sum); NLDSC_GPU_PLAN=0 forces the host
+    replay.  Same block pairs, same scores, for whole runs and owned sub-ranges, narrow and wide bands."""
+    import os
+
+    from nldsc_amd import synth
+    from nldsc_amd.engine import Engine
+    rng = np.random.default_rng(500 + seed)
+    N = int(rng.choice([64, 301, 1003]))
+    M = int(rng.integers(50, 1500))
+    spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=float(rng.uniform(1.0, 40.0)), seed=seed, missing=0.02)
+    rows = synth.pack_bed_rows(synth.genotypes(spec))
+    pos = synth.positions_cm(spec)
+    if seed % 3 == 0:
+        pos = np.round(pos, 1)  # duplicate positions and exact window ties
+    w = float(rng.choice([0.5, 1.0, 5.0]))
+    args = (w, 0.01, 1e-5, 1.0 / M, pos)
+    owns = [(0, M), (M // 3, 2 * M // 3), (M - 1, M), (0, 1)]
+    old = os.environ.get("NLDSC_GPU_PLAN")
+    out = {}
+    try:
+        for g in ("1", "0"):
+            os.environ["NLDSC_GPU_PLAN"] = g
+            with Engine(0) as e:
+                e.load_bed_bytes(synth.bed_bytes(rows), M, N)
+                out[g] = [(e.run(*args, own=o, flags=MODES["f4"]), e.timings()["band_items"]) for o in owns]
+    finally:
+        if old is None:
+            os.environ.pop("NLDSC_GPU_PLAN", None)
+        else:
+            os.environ["NLDSC_GPU_PLAN"] = old
+    for o, (a, na), (b, nb) in zip(owns, out["1"], out["0"]):
+        assert na == nb, (o, na, nb)
+        sub = {k: v[o[0]:o[1]] for k, v in a.items()}
+        ref = {k: v[o[0]:o[1]] for k, v in b.items()}
+        same_gram(sub, ref, f"own {o}")
+    exp = O.run_f64(rows, N, *args)
+    assert_ld_close(out["1"][0][0], exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
+                                                   maf=(0.0, 0.0)), label=f"gpu plan seed {seed}")
