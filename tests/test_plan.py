@@ -157,3 +157,46 @@ def test_left_pointers_from_all_pass_replay(seed):
     A, Ra = O.replay_windows(pos, np.ones(n, bool), w)
     np.testing.assert_array_equal(L, left_pointers_from_all_pass(pos, passed, A))
     np.testing.assert_array_equal(R[L >= 0], Ra[L >= 0])
+
+
+def gpu_schedule_restated(pos, w, own):
+    """numpy restatement of the GPU schedule kernels (ld_kernels.hip plan_*): window edges E by the exact
+    predicate, all-pass left pointers A, right pointers R = min(n-1, j + running max(E_k - k)), and the
+    per-row-block useful offset ranges -> the set of block pairs."""
+    n = len(pos)
+    E = np.array([next((k for k in range(j + 1, n) if pos[k] - pos[j] > w), n) for j in range(n)])
+    A = np.array([next(k for k in range(j + 1) if pos[j] - pos[k] <= w) for j in range(n)])
+    R = np.minimum(n - 1, np.arange(n) + np.maximum.accumulate(E - np.arange(n)))
+    nblk = (n + 31) // 32
+    ob0, ob1 = own[0] // 32, (own[1] - 1) // 32
+    pairs = set()
+    for I in range(A[own[0]] // 32, nblk):
+        if I * 32 >= own[1]:
+            break
+        jmax = min(nblk - 1, (E[min(n, 32 * I + 32) - 1] - 1) // 32)
+        own_row = ob0 <= I <= ob1
+        J0, J1 = (I, jmax) if own_row else (max(I, ob0), min(jmax, ob1))
+        pairs |= {(I, J) for J in range(J0, J1 + 1)}
+    return A, R, pairs
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_gpu_schedule_formulas_match_host_replay(seed):
+    """The closed forms the GPU schedule uses for non-negative sorted positions reproduce the host replay of
+    ChunkwiseReader (all-pass left/right pointers) and cover every needed block pair; the host plan's own
+    items are a subset of them (the GPU bound uses the exact |dpos| <= w predicate)."""
+    from nldsc_amd import _lib
+    rng = np.random.default_rng(900 + seed)
+    n = int(rng.integers(40, 700))
+    pos = np.cumsum(rng.exponential(0.02, n))
+    if seed % 2:
+        pos = np.round(pos, 2)  # ties
+    w = float(rng.choice([0.1, 0.25, 1.0]))
+    passed = np.ones(n, bool)
+    for own in ((0, n), (n // 4, n // 2), (n - 1, n)):
+        A, R, pairs = gpu_schedule_restated(pos, w, own)
+        L, Rh, items = _lib.plan_band(pos, passed.astype(np.uint8), w, own=own, max_nc=1)
+        np.testing.assert_array_equal(A, L)
+        np.testing.assert_array_equal(R, Rh)
+        assert covered(items) <= pairs
+        assert not (needed_blocks(pos, passed, w, L, Rh, own) - pairs)
