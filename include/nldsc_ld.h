@@ -133,6 +133,15 @@ int nldsc_engine_load_bed_file_range(nldsc_engine* e, const char* path, int32_t 
 int nldsc_plan_band(const double* positions, const uint8_t* flags, int32_t n_snp, double ld_wind, int32_t own_begin,
                     int32_t own_end, int32_t max_nc, int32_t* L, int32_t* R, int32_t* items, int32_t cap);
 
+/* The score table as the reference writes it (make_output + DataFrame.to_csv(sep="\t", index=False,
+ * float_format="%.5f"), nldsc/ldscore/routine.py:94-101), without the header line: row i = prefix line i
+ * (the caller's "CHR\tSNP\tBP" text, lines separated by '\n'), then L2, L2D [, MAF, WSA, WSD, WSDE,
+ * RSTD when extra]; floats "%.5f", NaN as an empty field.  Host-only, no GPU.  Returns the bytes
+ * written to `out`, or NLDSC_E_OOM when `cap` is too small, NLDSC_E_ARG on bad arguments. */
+int64_t nldsc_format_scores(const char* prefix, int64_t prefix_len, int32_t n, const double* l2, const double* l2d,
+                            const double* maf, const int32_t* l2_ws, const int32_t* l2d_ws, const int32_t* l2d_wse,
+                            const double* rstd, int32_t extra, char* out, int64_t cap);
+
 /* Deterministic synthetic PLINK .bed on the device (benchmarks / full-size tests):
  * writes the complete file image (magic + rows) to `bed_dev` (len >= 3 + n_snp*ceil(n_org/4)).
  * Model as nldsc_amd/synth.py: latent AR(1) haplotypes, thr[j] = Phi^-1(p_j), `missing` rate. */

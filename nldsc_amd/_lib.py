@@ -29,6 +29,7 @@ EXPORTED = (
     "nldsc_engine_destroy", "nldsc_engine_load_bed_file", "nldsc_engine_load_bed_host",
     "nldsc_engine_load_bed_device", "nldsc_engine_run", "nldsc_engine_timings",
     "nldsc_synth_bed_device", "nldsc_engine_path", "nldsc_plan_band", "nldsc_engine_load_bed_file_range",
+    "nldsc_format_scores",
 )
 
 
@@ -102,6 +103,10 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         for name in EXPORTED:
             if name not in ("nldsc_version", "nldsc_device_count", "nldsc_engine_destroy") and hasattr(L, name):
                 getattr(L, name).restype = ctypes.c_int
+        if hasattr(L, "nldsc_format_scores"):
+            L.nldsc_format_scores.restype = ctypes.c_int64
+            L.nldsc_format_scores.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_int32] + [vp] * 7 + \
+                [ctypes.c_int32, vp, ctypes.c_int64]  # out: any writable buffer address
         _libs[path] = L
     return _libs[path]
 

@@ -19,7 +19,7 @@ import numpy as np
 from ..core.common import NLDSCParameterError, elapsed_time
 from ..core.logger import log
 from .common import FAMFile, BIMFile, LDWindow, MAF, ResidualsSTDThreshold, RSQThreshold
-from .routine import m_values, make_output, write_m_file
+from .routine import m_values, make_output, write_m_file, write_scores
 
 CHROMS = [str(c) for c in range(1, 23)] + ["X", "Y", "XY", "MT"]
 
@@ -75,7 +75,8 @@ def estimate_lds_genome(bfile: str, ld_wind: float, wind_metric: str, maf_thr: f
                         std_thr: float = 1e-5, rsq_thr: float | None = None, *, out: str | None = None,
                         extra: bool = False, write_m: bool = False, flags: int = 0, device: int | None = None,
                         runner=None, rank: int | None = None, world: int | None = None) -> dict:
-    """Returns {chromosome: output DataFrame} for the chromosomes this rank processed."""
+    """Returns {chromosome: output DataFrame (None when written to `out`)} for the chromosomes this rank
+    processed."""
     units = expand_bfile(bfile)
     if out is not None and "@" not in out:
         raise NLDSCParameterError("a whole-genome run needs '@' in --out (one output per chromosome)")
@@ -108,10 +109,10 @@ def estimate_lds_genome(bfile: str, ld_wind: float, wind_metric: str, maf_thr: f
         t0 = time.perf_counter()
         res, tim = runner(bed, n_snp, m["n_org"], ld_wind_.data, maf_thr_.data, std_thr_.data, rsq, m["pos"], flags)
         ld = _Res(res)
-        df = make_output(m["bim"], ld, extra=extra)
+        df = make_output(m["bim"], ld, extra=extra) if out is None else None
         if out is not None:
             path = out.replace("@", m["chrom"])
-            df.to_csv(path, sep="\t", index=False, float_format="%.5f")
+            write_scores(path, m["bim"], ld, extra=extra)
             if write_m:
                 mm, md = m_values(m["bim"], ld)
                 write_m_file(str(Path(path).with_suffix(".M")), mm, md)

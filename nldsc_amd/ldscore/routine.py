@@ -18,7 +18,7 @@ from ..core.logger import log
 from . import _ldscore as lds
 from .common import BIMFile, LDWindow, MAF, PLINKFile, ResidualsSTDThreshold, RSQThreshold
 
-__all__ = ["estimate_lds", "make_output", "show_summary", "m_values", "write_m_file"]
+__all__ = ["estimate_lds", "make_output", "format_scores", "write_scores", "show_summary", "m_values", "write_m_file"]
 
 
 def show_summary(ld) -> None:
@@ -42,6 +42,52 @@ def make_output(bim: BIMFile, ld, *, extra: bool = False) -> pd.DataFrame:
         cols.update(MAF=pd.Series(list(ld.maf)), WSA=pd.Series(list(ld.l2_ws)), WSD=pd.Series(list(ld.l2d_ws)),
                     WSDE=pd.Series(list(ld.l2d_wse)), RSTD=pd.Series(list(ld.residuals_std)))
     return pd.DataFrame(cols)
+
+
+HEADER = ("CHR", "SNP", "BP", "L2", "L2D")
+HEADER_EXTRA = ("MAF", "WSA", "WSD", "WSDE", "RSTD")
+
+
+def format_scores(bim: BIMFile, ld, *, extra: bool = False) -> bytes:
+    """The bytes `make_output(bim, ld, extra=extra).to_csv(path, sep="\t", index=False, float_format="%.5f")`
+    writes (routine.py:94-101 of the reference), formatted by the native writer (nldsc_format_scores):
+    ~20x faster than pandas on the float columns.  CHR / SNP / BP are printed as pandas prints the parsed
+    .bim columns (int64 -> decimal, object -> the text); any other column type goes through pandas."""
+    import ctypes
+
+    from .. import _lib
+    cols = (bim.chr.reset_index(drop=True), bim.snp.reset_index(drop=True), bim.bp.reset_index(drop=True))
+    n = len(cols[0])
+    if any(c.dtype.kind not in "iuO" for c in cols) or len(ld.l2) != n:
+        buf = make_output(bim, ld, extra=extra).to_csv(sep="\t", index=False, float_format="%.5f")
+        return buf.encode()
+    text = [list(map(str, c.tolist())) for c in cols]  # what pandas prints for int64 / object cells
+    f64 = lambda v: np.ascontiguousarray(v, dtype=np.float64)  # noqa: E731
+    i32 = lambda v: np.ascontiguousarray(v, dtype=np.int32)  # noqa: E731
+    arrs = [f64(ld.l2), f64(ld.l2d)]
+    if extra:
+        arrs += [f64(ld.maf), i32(ld.l2_ws), i32(ld.l2d_ws), i32(ld.l2d_wse), f64(ld.residuals_std)]
+    lib, parts, chunk = _lib.lib(), [], 16384
+    out = np.empty(0, np.uint8)
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        prefix = "\n".join(map("\t".join, zip(text[0][a:b], text[1][a:b], text[2][a:b]))).encode()
+        need = len(prefix) + (b - a) * (16 + 7 * 400) + 1  # worst case of the numeric fields
+        if out.size < need:
+            out = np.empty(need, np.uint8)
+        ptrs = [v[a:].ctypes.data for v in arrs] + [None] * (7 - len(arrs))
+        got = lib.nldsc_format_scores(prefix, len(prefix), b - a, *ptrs, int(bool(extra)), out.ctypes.data,
+                                      out.size)
+        if got < 0:
+            raise RuntimeError(f"nldsc_format_scores failed ({got})")
+        parts.append(out[:got].tobytes())
+    head = "\t".join(HEADER + (HEADER_EXTRA if extra else ())) + "\n"
+    return head.encode() + b"".join(parts)
+
+
+def write_scores(path: str, bim: BIMFile, ld, *, extra: bool = False) -> None:
+    with open(path, "wb") as fh:
+        fh.write(format_scores(bim, ld, extra=extra))
 
 
 def m_values(bim: BIMFile, ld) -> tuple[int, int]:
@@ -125,13 +171,12 @@ def estimate_lds(bfile: str, ld_wind: float, wind_metric: str, maf_thr: float = 
 
     if summary:
         show_summary(ld)
-    out_df = make_output(bim_, ld, extra=extra)
     if out:
         log.info("Writing data to disk...")
-        out_df.to_csv(out, sep="\t", index=False, float_format="%.5f")
+        write_scores(out, bim_, ld, extra=extra)
         if write_m:
             m, md = m_values(bim_, ld)
             write_m_file(str(Path(out).with_suffix(".M")), m, md)
         log.info(f"Completed. File: {out}")
         return None
-    return out_df
+    return make_output(bim_, ld, extra=extra)

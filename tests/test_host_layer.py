@@ -103,3 +103,35 @@ def test_cli_requires_exactly_one_window():
                         "-maf", "0.01"], cwd=REPO, capture_output=True, text=True, timeout=120)
     assert "Please, specify exactly one --ld-wind option" in r.stderr
     assert "The program crashed with RuntimeError" in r.stderr
+
+
+def test_native_tsv_writer_is_byte_identical_to_pandas(tmp_path):
+    """nldsc_format_scores (the CLI's writer) against make_output(...).to_csv(sep="\\t", float_format="%.5f")
+    on awkward values: NaN, -0.0, rounding ties at the 5th decimal, huge and tiny magnitudes, inf, -1
+    window sizes, string and integer chromosome columns."""
+    import pandas as pd
+
+    from nldsc_amd.ldscore.common import BIMFile
+    from nldsc_amd.ldscore.routine import format_scores, make_output
+    rng = np.random.default_rng(3)
+    n = 5000
+    for chrom in ("7", "X"):
+        path = tmp_path / f"t{chrom}.bim"
+        with open(path, "w") as fh:
+            for i in range(n):
+                fh.write(f"{chrom}\trs{i}\t{i * 0.001:.6f}\t{1000 + 37 * i}\tA\tG\n")
+        bim = BIMFile(str(path))
+
+        class LD:
+            pass
+        ld = LD()
+        vals = rng.normal(0, 50, (4, n))
+        special = np.array([np.nan, -0.0, 0.0, 1.000005, 2.500005, -1e-7, 1e300, -1e300, np.inf, 0.123455,
+                            1234567.891234, 5e-6, -5e-6, 4.9999999e-6])
+        vals[:, :len(special)] = special
+        ld.l2, ld.l2d, ld.maf, ld.residuals_std = (list(v) for v in vals)
+        ws = rng.integers(-1, 700, (3, n)).astype(np.int32)
+        ld.l2_ws, ld.l2d_ws, ld.l2d_wse = (list(int(x) for x in w) for w in ws)
+        for extra in (False, True):
+            ref = make_output(bim, ld, extra=extra).to_csv(sep="\t", index=False, float_format="%.5f").encode()
+            assert format_scores(bim, ld, extra=extra) == ref, (chrom, extra)
