@@ -135,3 +135,27 @@ def test_native_tsv_writer_is_byte_identical_to_pandas(tmp_path):
         for extra in (False, True):
             ref = make_output(bim, ld, extra=extra).to_csv(sep="\t", index=False, float_format="%.5f").encode()
             assert format_scores(bim, ld, extra=extra) == ref, (chrom, extra)
+
+
+def test_native_f5_matches_python_formatting():
+    """The writer's integer-arithmetic "%.5f" against Python's correctly rounded formatting on 300k values:
+    random magnitudes 1e-15 .. 1e15, random bit patterns, values next to rounding boundaries."""
+    import ctypes
+
+    from nldsc_amd import _lib
+    rng = np.random.default_rng(11)
+    n = 100_000
+    x = np.concatenate([rng.uniform(-1, 1, n) * 10.0 ** rng.integers(-15, 15, n),
+                        rng.integers(0, 2**63, n, dtype=np.uint64).view(np.float64),
+                        np.round(rng.uniform(-100, 100, n), 5) + rng.choice([-5e-6, 5e-6, 4.9999e-6], n)])
+    x = x[~np.isnan(x)]
+    zeros = np.zeros(len(x))
+    prefix = b"\n".join(b"p" for _ in range(len(x)))
+    out = np.empty(len(prefix) + len(x) * 900, np.uint8)
+    got = _lib.lib().nldsc_format_scores(prefix, len(prefix), len(x), x.ctypes.data, zeros.ctypes.data, None, None,
+                                         None, None, None, 0, out.ctypes.data, out.size)
+    assert got > 0
+    lines = out[:got].tobytes().decode().splitlines()
+    exp = ["p\t%.5f\t0.00000" % v for v in x]
+    bad = [(v, a, b) for v, a, b in zip(x, lines, exp) if a != b]
+    assert not bad, bad[:5]
