@@ -108,6 +108,9 @@ struct nldsc_engine {
     // resident .bed image
     DevBuf<uint8_t> bed;
     DevBuf<uint8_t> lastb;  // each row's original last byte (the per-run count kernel masks a copy of it)
+    DevBuf<uint8_t> flip;   // per SNP: resident row stores the swapped (00 <-> 11) coding
+    bool orient = true;     // store rows minor-homozygote-as-00 at load (NLDSC_ORIENT=0: file coding)
+    bool oriented = false;  // the resident image was oriented
     int32_t n_snp = 0, n_org = 0;
     // work buffers
 
@@ -150,7 +153,7 @@ struct nldsc_engine {
 
     ~nldsc_engine() {
         (void)hipSetDevice(device);
-        bed.release(); lastb.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
+        bed.release(); lastb.release(); flip.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
         ws3.release(); lut.release(); cst.release(); sflags.release(); pos.release(); maf.release(); rstd.release();
         l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
@@ -353,6 +356,7 @@ hipError_t alloc_image(nldsc_engine* e, int32_t n_snp, int32_t n_org) {
     e->n_snp = e->n_org = 0;  // no valid image until finish_image
     hipError_t he = e->bed.ensure((size_t)padded_rows(n_snp) * (size_t)row_pitch(n_org));
     if (he == hipSuccess) he = e->lastb.ensure((size_t)n_snp);
+    if (he == hipSuccess) he = e->flip.ensure((size_t)n_snp);
     return he;
 }
 
@@ -361,6 +365,9 @@ hipError_t finish_image(nldsc_engine* e, int32_t n_snp, int32_t n_org) {
     const int nb = n_org / 4 + (n_org % 4 > 0);
     hipError_t he = nldsc::launch_pad_rows(e->bed.p, e->lastb.p, n_snp, padded_rows(n_snp), nb, row_pitch(n_org),
                                            e->stream);
+    e->oriented = e->orient;
+    if (he == hipSuccess && e->oriented)
+        he = nldsc::launch_orient_rows(e->bed.p, e->lastb.p, n_snp, row_pitch(n_org), e->flip.p, e->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
     if (he == hipSuccess) {
         e->n_snp = n_snp;
@@ -400,6 +407,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_XCD")) e->xcd = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_BAND_ROUND")) e->band_round = std::atoi(v);
     if (const char* v = std::getenv("NLDSC_GPU_PLAN")) e->gpu_plan = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_ORIENT")) e->orient = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_TILE_R")) e->tile_r = std::atoi(v);
     if (const char* v = std::getenv("NLDSC_TILE_C")) e->tile_c = std::max(1, std::atoi(v));
     if (const char* v = std::getenv("NLDSC_BAND_F4_GRP")) e->f4_grp = std::atoi(v);
@@ -629,7 +637,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     }
     HIPCHK(nldsc::launch_count_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, e->counts.p, st));
     HIPCHK(hipEventRecord(e->ev[1], st));
-    HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->cst.p,
+    HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->oriented ? e->flip.p : nullptr, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->cst.p,
                                    e->sflags.p, e->maf.p, e->rstd.p, st));
     HIPCHK(hipEventRecord(e->ev[2], st));
 

@@ -21,9 +21,12 @@ hipError_t launch_pad_rows(uint8_t* img, uint8_t* last, int n_snp, int n_rows, i
 // per run: genotype-code counts with the last byte set to this run's individuals (tail_keep mask)
 hipError_t launch_count_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
                              int* counts, hipStream_t st);
-hipError_t launch_snp_stats(const int* counts, const double* pos, int n_snp, int n_snp_pad, int n_org, double maf_thr,
-                            double std_thr, float2* lut, SnpConst* cst, uint8_t* sflags, double* maf_out,
-                            double* rstd_out, hipStream_t st);
+// flip: per-SNP stored-orientation flags (nullptr: none flipped)
+hipError_t launch_snp_stats(const int* counts, const uint8_t* flip, const double* pos, int n_snp, int n_snp_pad,
+                            int n_org, double maf_thr, double std_thr, float2* lut, SnpConst* cst, uint8_t* sflags,
+                            double* maf_out, double* rstd_out, hipStream_t st);
+// after a load: swap 00 <-> 11 in rows (and saved last bytes) with more hom-A2 than hom-A1 calls; flip[j] = 1
+hipError_t launch_orient_rows(uint8_t* img, uint8_t* last, int n_snp, int row_bytes, uint8_t* flip, hipStream_t st);
 // exact left pointers L from the all-pass replay's A and the device MAF flags (sorted positions)
 hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const double* pos, int n, int* L, hipStream_t st);
 // band schedule on the GPU for non-negative sorted positions: all-pass left pointers A, window edges E,

@@ -59,6 +59,46 @@ __global__ void pad_rows_kernel(uint8_t* __restrict__ img, uint8_t* __restrict__
     }
 }
 
+// After a load (after pad_rows_kernel): store every SNP in its minor-homozygote-is-00 orientation.
+// Rows with more hom-A2 (11) than hom-A1 (00) calls get 00 <-> 11 swapped in place (het 10 and
+// missing 01 unchanged; the saved last byte too) and flip[j] = 1.  The exact kernels' operands are then
+// mostly zero whatever the file's allele order (PLINK usually writes A1 = minor, so A2 = major), which
+// keeps the matrix cores' power, and the chip's clock, where the synthetic A2-minor data has it.
+__global__ void __launch_bounds__(256) orient_rows_kernel(uint8_t* __restrict__ img, uint8_t* __restrict__ last,
+                                                          int n_snp, int row_bytes, uint8_t* __restrict__ flip) {
+    const int j = blockIdx.x;
+    if (j >= n_snp) return;
+    uint32_t* row = reinterpret_cast<uint32_t*>(img + (size_t)j * (size_t)row_bytes);
+    const int n_words = row_bytes / 4;
+    int c0 = 0, c1 = 0, c2 = 0;
+    for (int w = threadIdx.x; w < n_words; w += blockDim.x) count_codes(row[w], c0, c1, c2);
+    for (int o = 32; o > 0; o >>= 1) {
+        c0 += __shfl_down(c0, o, 64);
+        c2 += __shfl_down(c2, o, 64);
+    }
+    __shared__ int red[2][4];
+    __shared__ int swap;
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][wv] = c0; red[1][wv] = c2; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int a = 0, b = 0;
+        for (int q = 0; q < (int)(blockDim.x >> 6); ++q) { a += red[0][q]; b += red[1][q]; }
+        swap = b > a;
+        flip[j] = (uint8_t)swap;
+        if (swap) {
+            const uint32_t lb = last[j], t = ~(lb ^ (lb >> 1)) & 0x55u;
+            last[j] = (uint8_t)(lb ^ (t | (t << 1)));
+        }
+    }
+    __syncthreads();
+    if (!swap) return;
+    for (int w = threadIdx.x; w < n_words; w += blockDim.x) {
+        const uint32_t v = row[w], t = ~(v ^ (v >> 1)) & 0x55555555u;  // pairs 00 or 11
+        row[w] = v ^ (t | (t << 1));
+    }
+}
+
 // Per run: genotype-code counts of every row (one workgroup per SNP, 16-byte loads) with the last
 // byte set to this run's individuals: (saved byte & keep) | (0x55 & ~keep).  HBM-bound read of the
 // image; the thread that owns the last byte's chunk counts the patched value and writes it back.
@@ -118,10 +158,40 @@ __global__ void __launch_bounds__(256) count_rows_kernel(uint8_t* __restrict__ i
 // Closed form of SNPInMemory::decode + standardise (encoder.h:91-133, tools.h:54-85) from the
 // genotype counts c0 (hom A1), c1 (het), c2 (hom A2) over the n_org individuals the reference
 // reads.  Missing calls are mean-imputed by the reference, so their centred value is exactly 0.
-__global__ void snp_stats_kernel(const int* __restrict__ counts, const double* __restrict__ pos, int n_snp,
-                                 int n_snp_pad, int n_org, double maf_thr, double std_thr,
-                                 float2* __restrict__ lut, SnpConst* __restrict__ cst, uint8_t* __restrict__ sflags,
-                                 double* __restrict__ maf_out, double* __restrict__ rstd_out) {
+// Moments of one coding from its genotype counts (c0 hom A1, c1 het, c2 hom A2; N = n_org slots).
+struct Coding {
+    double abar, dbar, beta, sd_a, rstd, da[3], r[3];
+};
+__device__ __forceinline__ Coding coding_moments(double c0, double c1, double c2, double N) {
+    Coding m;
+    const double n_obs = c0 + c1 + c2;
+    m.abar = (c1 + 2.0 * c2) / n_obs;
+    m.dbar = 2.0 * (c1 + c2) / n_obs;
+    m.da[0] = -m.abar; m.da[1] = 1.0 - m.abar; m.da[2] = 2.0 - m.abar;
+    const double dd0 = -m.dbar, dd1 = 2.0 - m.dbar, dd2 = 2.0 - m.dbar;
+    const double var_a = (c0 * m.da[0] * m.da[0] + c1 * m.da[1] * m.da[1] + c2 * m.da[2] * m.da[2]) / N;
+    const double cov = (c0 * m.da[0] * dd0 + c1 * m.da[1] * dd1 + c2 * m.da[2] * dd2) / N;
+    m.beta = cov / var_a;  // Math::regression_residuals slope
+    m.r[0] = dd0 - m.beta * m.da[0]; m.r[1] = dd1 - m.beta * m.da[1]; m.r[2] = dd2 - m.beta * m.da[2];
+    const int distinct = (c0 > 0) + (c1 > 0) + (c2 > 0);
+    // <= 2 observed genotypes: the dominance coding is affine in the additive one, the residual is
+    // exactly constant, its std exactly 0.
+    const double var_r = distinct <= 2 ? 0.0 : (c0 * m.r[0] * m.r[0] + c1 * m.r[1] * m.r[1] + c2 * m.r[2] * m.r[2]) / N;
+    m.sd_a = sqrt(var_a);
+    m.rstd = sqrt(var_r);
+    return m;
+}
+
+// flip[j]: the resident row of SNP j stores the swapped coding (00 <-> 11, see orient_rows_kernel).
+// MAF, residual std and the filters come from the file's coding (the reference's); the constants of
+// the exact epilogue and the fp32 lookup table describe the stored coding the band kernels read.
+// Swapping the alleles negates A and leaves R unchanged (the residual of [x >= 1] and of [x <= 1] on
+// span{1, x} is the same vector), so every r^2 is the same.
+__global__ void snp_stats_kernel(const int* __restrict__ counts, const uint8_t* __restrict__ flip,
+                                 const double* __restrict__ pos, int n_snp, int n_snp_pad, int n_org, double maf_thr,
+                                 double std_thr, float2* __restrict__ lut, SnpConst* __restrict__ cst,
+                                 uint8_t* __restrict__ sflags, double* __restrict__ maf_out,
+                                 double* __restrict__ rstd_out) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_snp_pad) return;
     float2 L[4] = {make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
@@ -129,14 +199,15 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const double* _
     uint8_t fl = 0;
     double sX = 0.0, sH = 0.0, sOb = 0.0;
     if (j < n_snp) {
-        const int* cj = counts + 4 * (size_t)j;
-        sX = (double)cj[1] + 2.0 * cj[2];
-        sH = (double)cj[1] + cj[2];
-        sOb = (double)cj[0] + cj[1] + cj[2];
+        const double s0 = counts[4 * (size_t)j], c1 = counts[4 * (size_t)j + 1], s2 = counts[4 * (size_t)j + 2];
+        const bool fj = flip != nullptr && flip[j];
+        const double c0 = fj ? s2 : s0, c2 = fj ? s0 : s2;  // the file's coding
+        sX = c1 + 2.0 * s2;  // sums over the stored coding's indicators
+        sH = c1 + s2;
+        sOb = s0 + c1 + s2;
         const double qnan = __builtin_nan("");
         double maf_d = qnan, rstd_d = qnan;
         if (pos[j] >= 0.0) {  // SNPFilter::is_used (tools.h:15-23)
-            const double c0 = counts[4 * (size_t)j], c1 = counts[4 * (size_t)j + 1], c2 = counts[4 * (size_t)j + 2];
             const double n_obs = c0 + c1 + c2;
             const double N = (double)n_org;
             // MAF exactly as encoder.h:114-118 (fp64 mean of integers cast to fp32)
@@ -152,31 +223,22 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const double* _
                     for (int c = 0; c < 4; ++c) L[c] = make_float2(qnan, 0.f);
                     K = SnpConst{qnan, qnan, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
                 } else {
-                    const double abar = (c1 + 2.0 * c2) / n_obs, dbar = 2.0 * (c1 + c2) / n_obs;
-                    const double da0 = -abar, da1 = 1.0 - abar, da2 = 2.0 - abar;
-                    const double dd0 = -dbar, dd1 = 2.0 - dbar, dd2 = 2.0 - dbar;
-                    const double var_a = (c0 * da0 * da0 + c1 * da1 * da1 + c2 * da2 * da2) / N;
-                    const double cov = (c0 * da0 * dd0 + c1 * da1 * dd1 + c2 * da2 * dd2) / N;
-                    const double beta = cov / var_a;  // Math::regression_residuals slope
-                    const double r0 = dd0 - beta * da0, r1 = dd1 - beta * da1, r2 = dd2 - beta * da2;
-                    const int distinct = (c0 > 0) + (c1 > 0) + (c2 > 0);
-                    // <= 2 observed genotypes: the dominance coding is affine in the additive one,
-                    // the residual is exactly constant, its std exactly 0.
-                    const double var_r = distinct <= 2 ? 0.0 : (c0 * r0 * r0 + c1 * r1 * r1 + c2 * r2 * r2) / N;
-                    const double sd_a = sqrt(var_a);
-                    rstd_d = sqrt(var_r);
+                    const Coding f = coding_moments(c0, c1, c2, N);
+                    rstd_d = f.rstd;
                     const bool rpass = rstd_d > std_thr;  // SNPFilter::residuals_std (tools.h:40-43)
                     if (rpass) fl |= 2;
-                    const float ia = (float)(da0 / sd_a), ib = (float)(da1 / sd_a), ic = (float)(da2 / sd_a);
+                    const Coding m = fj ? coding_moments(s0, c1, s2, N) : f;  // the stored coding
+                    const float ia = (float)(m.da[0] / m.sd_a), ib = (float)(m.da[1] / m.sd_a),
+                                ic = (float)(m.da[2] / m.sd_a);
                     float ra = 0.f, rb = 0.f, rc = 0.f;
-                    if (rpass) { ra = (float)(r0 / rstd_d); rb = (float)(r1 / rstd_d); rc = (float)(r2 / rstd_d); }
-                    L[0] = make_float2(ia, ra);   // code 00 hom A1
+                    if (rpass) { ra = (float)(m.r[0] / m.rstd); rb = (float)(m.r[1] / m.rstd); rc = (float)(m.r[2] / m.rstd); }
+                    L[0] = make_float2(ia, ra);   // stored code 00 (hom A1, or hom A2 when flipped)
                     L[1] = make_float2(0.f, 0.f); // code 01 missing (imputed -> centred 0)
                     L[2] = make_float2(ib, rb);   // code 10 het
-                    L[3] = make_float2(ic, rc);   // code 11 hom A2
+                    L[3] = make_float2(ic, rc);   // stored code 11
                     // exact path: A = (x - mu o) / sa,  R = (2h - beta x - c o) / s   (x, h, o integer)
-                    K = SnpConst{abar, sd_a, rpass ? dbar - beta * abar : 0.0, rpass ? beta : 0.0,
-                                 rpass ? rstd_d : 0.0, 0.0, 0.0, 0.0};
+                    K = SnpConst{m.abar, m.sd_a, rpass ? m.dbar - m.beta * m.abar : 0.0, rpass ? m.beta : 0.0,
+                                 rpass ? m.rstd : 0.0, 0.0, 0.0, 0.0};
                 }
             }
         }
@@ -1356,12 +1418,18 @@ hipError_t launch_count_rows(uint8_t* img, const uint8_t* last, int n_snp, int n
     return hipGetLastError();
 }
 
-hipError_t launch_snp_stats(const int* counts, const double* pos, int n_snp, int n_snp_pad, int n_org, double maf_thr,
-                            double std_thr, float2* lut, SnpConst* cst, uint8_t* sflags, double* maf_out,
-                            double* rstd_out, hipStream_t st) {
+hipError_t launch_snp_stats(const int* counts, const uint8_t* flip, const double* pos, int n_snp, int n_snp_pad,
+                            int n_org, double maf_thr, double std_thr, float2* lut, SnpConst* cst, uint8_t* sflags,
+                            double* maf_out, double* rstd_out, hipStream_t st) {
     const int blocks = (n_snp_pad + 255) / 256;
-    hipLaunchKernelGGL(snp_stats_kernel, dim3(blocks), dim3(256), 0, st, counts, pos, n_snp, n_snp_pad, n_org, maf_thr,
-                       std_thr, lut, cst, sflags, maf_out, rstd_out);
+    hipLaunchKernelGGL(snp_stats_kernel, dim3(blocks), dim3(256), 0, st, counts, flip, pos, n_snp, n_snp_pad, n_org,
+                       maf_thr, std_thr, lut, cst, sflags, maf_out, rstd_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_orient_rows(uint8_t* img, uint8_t* last, int n_snp, int row_bytes, uint8_t* flip, hipStream_t st) {
+    if (n_snp <= 0) return hipSuccess;
+    hipLaunchKernelGGL(orient_rows_kernel, dim3(n_snp), dim3(256), 0, st, img, last, n_snp, row_bytes, flip);
     return hipGetLastError();
 }
 

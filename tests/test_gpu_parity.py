@@ -356,3 +356,49 @@ def test_gpu_schedule_matches_host_schedule(engine, seed):
     exp = O.run_f64(rows, N, *args)
     assert_ld_close(out["1"][0][0], exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
                                                    maf=(0.0, 0.0)), label=f"gpu plan seed {seed}")
+
+
+def _swap_alleles(rows, which):
+    """Swap hom-A1 (00) and hom-A2 (11) codes of the SNPs in `which` (as if .bim A1/A2 were exchanged)."""
+    rows = rows.copy()
+    sub = rows[which].astype(np.uint32)
+    t = ~(sub ^ (sub >> 1)) & 0x55
+    rows[which] = (sub ^ (t | (t << 1))).astype(np.uint8)
+    return rows
+
+
+@pytest.mark.parametrize("name", ["n1001", "n1003", "allmiss"])
+def test_allele_orientation_is_invisible(name):
+    """The engine stores every SNP minor-homozygote-as-00 (rows with more 11 than 00 calls are swapped at
+    load).  On a file whose alleles are swapped for half of the SNPs (A2 = major, PLINK's usual order), the
+    scores equal the fp64 truth of that file, and equal a run that keeps the file coding (NLDSC_ORIENT=0)."""
+    import os
+
+    import torch
+    torch.cuda.init()
+    from nldsc_amd.engine import Engine
+    bed, pos, meta, _, _ = load_set(name)
+    N, M = meta["n_org"], meta["n_snp"]
+    rows = np.frombuffer(bed, np.uint8, offset=3).reshape(M, -1)
+    swapped = _swap_alleles(rows, np.arange(0, M, 2))
+    args = (meta["ld_wind"], meta["maf"], meta["std_thr"], meta["rsq_thr"], pos)
+    exp = O.run_f64(swapped, N, *args)
+    old = os.environ.get("NLDSC_ORIENT")
+    out = {}
+    try:
+        for o in ("1", "0"):
+            os.environ["NLDSC_ORIENT"] = o
+            for mode in ("f4", "i8", "f32"):
+                with Engine(0) as e:
+                    e.load_bed_bytes(b"\x6c\x1b\x01" + swapped.tobytes(), M, N)
+                    out[o, mode] = e.run(*args, flags=MODES[mode])
+    finally:
+        if old is None:
+            os.environ.pop("NLDSC_ORIENT", None)
+        else:
+            os.environ["NLDSC_ORIENT"] = old
+    exact = dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10), maf=(0.0, 0.0))
+    for mode in ("f4", "i8"):
+        assert_ld_close(out["1", mode], exp, tol=exact, label=f"{name} oriented {mode}")
+        same_gram(out["1", mode], out["0", mode], f"{name} {mode}")
+    assert_ld_close(out["1", "f32"], exp, label=f"{name} oriented f32")
