@@ -103,6 +103,8 @@ struct HostPinned {
 struct nldsc_engine {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t plan_stream = nullptr;  // the GPU schedule runs here, beside the count kernel
+    hipEvent_t ev_pos = nullptr;        // positions uploaded (the schedule's only input)
     hipEvent_t ev[6] = {};
     hipEvent_t ev_plan = nullptr;  // GPU plan counters landed in h_meta
     // resident .bed image
@@ -160,6 +162,8 @@ struct nldsc_engine {
         if (ev_plan) (void)hipEventDestroy(ev_plan);
         Ew.release(); plan_counts.release(); plan_meta.release(); plan_rows.release();
         if (stream) (void)hipStreamDestroy(stream);
+        if (plan_stream) (void)hipStreamDestroy(plan_stream);
+        if (ev_pos) (void)hipEventDestroy(ev_pos);
     }
 };
 
@@ -418,6 +422,8 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
             e->n_cu = prop.multiProcessorCount;
     }
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->plan_stream, hipStreamNonBlocking);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_pos, hipEventDisableTiming);
     for (auto& ev : e->ev)
         if (he == hipSuccess) he = hipEventCreate(&ev);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_plan, hipEventDisableTiming);
@@ -630,10 +636,13 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     HIPCHK(hipEventRecord(e->ev[0], st));
     HIPCHK(hipMemcpyAsync(e->pos.p, p->positions, sizeof(double) * M, hipMemcpyHostToDevice, st));
     if (gpu_plan) {
+        // the schedule depends only on the positions: it runs on a second stream beside the count kernel
+        HIPCHK(hipEventRecord(e->ev_pos, st));
+        HIPCHK(hipStreamWaitEvent(e->plan_stream, e->ev_pos, 0));
         HIPCHK(nldsc::launch_plan(e->pos.p, M, p->ld_wind, own_begin, own_end, e->Aw.p, e->Ew.p, e->Rw.p,
-                                  e->plan_rows.p, e->plan_counts.p, e->plan_meta.p, st));
-        HIPCHK(hipMemcpyAsync(e->h_meta.p, e->plan_meta.p, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipEventRecord(e->ev_plan, st));
+                                  e->plan_rows.p, e->plan_counts.p, e->plan_meta.p, e->plan_stream));
+        HIPCHK(hipMemcpyAsync(e->h_meta.p, e->plan_meta.p, 4 * sizeof(int), hipMemcpyDeviceToHost, e->plan_stream));
+        HIPCHK(hipEventRecord(e->ev_plan, e->plan_stream));
     }
     HIPCHK(nldsc::launch_count_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, e->counts.p, st));
     HIPCHK(hipEventRecord(e->ev[1], st));
@@ -646,6 +655,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     int n_items = 0, n_diag = 0;
     if (gpu_plan) {
         HIPCHK(hipEventSynchronize(e->ev_plan));  // the count kernel is running meanwhile
+        HIPCHK(hipStreamWaitEvent(st, e->ev_plan, 0));  // emit / left pointers / band read the schedule
         const int* meta = reinterpret_cast<const int*>(e->h_meta.p);
         n_items = meta[1];
         n_diag = meta[2];

@@ -99,42 +99,37 @@ __global__ void __launch_bounds__(256) orient_rows_kernel(uint8_t* __restrict__ 
     }
 }
 
-// Per run: genotype-code counts of every row (one workgroup per SNP, 16-byte loads) with the last
-// byte set to this run's individuals: (saved byte & keep) | (0x55 & ~keep).  HBM-bound read of the
-// image; the thread that owns the last byte's chunk counts the patched value and writes it back.
+// Per run: genotype-code counts of every row (one workgroup per SNP, 16-byte non-temporal loads, 8 in
+// flight per thread) with the last byte set to this run's individuals: (saved byte & keep) | (0x55 &
+// ~keep).  HBM-bound read of the image.  The rows are counted as they stand, then one thread swaps the
+// last byte's old codes for the new ones in the counts and writes the byte (after the barrier, so no
+// thread of the loop saw a half-updated row).
+typedef uint32_t u32x4nt __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void count_chunk(const u32x4nt o, int& c0, int& c1, int& c2) {
+    count_codes(o.x, c0, c1, c2);
+    count_codes(o.y, c0, c1, c2);
+    count_codes(o.z, c0, c1, c2);
+    count_codes(o.w, c0, c1, c2);
+}
+
 __global__ void __launch_bounds__(256) count_rows_kernel(uint8_t* __restrict__ img, const uint8_t* __restrict__ last,
                                                          int n_snp, int nb, int row_bytes, uint32_t tail_keep,
                                                          int* __restrict__ counts) {
     const int j = blockIdx.x;
     if (j >= n_snp) return;
     uint8_t* row = img + (size_t)j * (size_t)row_bytes;
-    const uint4* src = reinterpret_cast<const uint4*>(row);
-    const int n_chunks = row_bytes / 16, c_last = (nb - 1) / 16;
+    const u32x4nt* src = reinterpret_cast<const u32x4nt*>(row);
+    const int n_chunks = row_bytes / 16, T = blockDim.x;
     int c0 = 0, c1 = 0, c2 = 0;
-    const int T = blockDim.x;
     int c = threadIdx.x;
-    for (; c + 3 * T < n_chunks; c += 4 * T) {  // 4 loads in flight; the last byte's chunk is left to the tail loop
-        if (c_last >= c && c_last - c < 4 * T && (c_last - c) % T == 0) break;
-        const uint4 a = src[c], b = src[c + T], d = src[c + 2 * T], f = src[c + 3 * T];
-        count_codes(a.x, c0, c1, c2); count_codes(a.y, c0, c1, c2); count_codes(a.z, c0, c1, c2); count_codes(a.w, c0, c1, c2);
-        count_codes(b.x, c0, c1, c2); count_codes(b.y, c0, c1, c2); count_codes(b.z, c0, c1, c2); count_codes(b.w, c0, c1, c2);
-        count_codes(d.x, c0, c1, c2); count_codes(d.y, c0, c1, c2); count_codes(d.z, c0, c1, c2); count_codes(d.w, c0, c1, c2);
-        count_codes(f.x, c0, c1, c2); count_codes(f.y, c0, c1, c2); count_codes(f.z, c0, c1, c2); count_codes(f.w, c0, c1, c2);
+    for (; c + 7 * T < n_chunks; c += 8 * T) {
+        u32x4nt v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(src + c + u * T);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) count_chunk(v[u], c0, c1, c2);
     }
-    for (; c < n_chunks; c += T) {
-        uint4 o = src[c];
-        if (c == c_last) {
-            const uint32_t b = ((uint32_t)last[j] & tail_keep) | (0x55u & ~tail_keep);
-            const int q = ((nb - 1) & 15) >> 2, sh = 8 * ((nb - 1) & 3);
-            uint32_t* w = q == 0 ? &o.x : q == 1 ? &o.y : q == 2 ? &o.z : &o.w;
-            *w = (*w & ~(0xFFu << sh)) | (b << sh);
-            row[nb - 1] = (uint8_t)b;
-        }
-        count_codes(o.x, c0, c1, c2);
-        count_codes(o.y, c0, c1, c2);
-        count_codes(o.z, c0, c1, c2);
-        count_codes(o.w, c0, c1, c2);
-    }
+    for (; c < n_chunks; c += T) count_chunk(__builtin_nontemporal_load(src + c), c0, c1, c2);
     // block reduction (4 waves of 64)
     for (int o = 32; o > 0; o >>= 1) {
         c0 += __shfl_down(c0, o, 64);
@@ -145,10 +140,18 @@ __global__ void __launch_bounds__(256) count_rows_kernel(uint8_t* __restrict__ i
     const int wv = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) { red[0][wv] = c0; red[1][wv] = c1; red[2][wv] = c2; }
     __syncthreads();
-    if (threadIdx.x < 3) {
-        int s = 0;
-        for (int q = 0; q < (int)(blockDim.x >> 6); ++q) s += red[threadIdx.x][q];
-        counts[(size_t)j * 4 + threadIdx.x] = s;
+    if (threadIdx.x == 0) {
+        int s[3] = {0, 0, 0};
+        for (int q = 0; q < (int)(blockDim.x >> 6); ++q)
+            for (int k = 0; k < 3; ++k) s[k] += red[k][q];
+        const uint32_t old_b = row[nb - 1], new_b = ((uint32_t)last[j] & tail_keep) | (0x55u & ~tail_keep);
+        int o0 = 0, o1 = 0, o2 = 0, n0 = 0, n1 = 0, n2 = 0;
+        count_codes(old_b | 0x55555500u, o0, o1, o2);  // the byte's 4 pairs; the rest of the word reads as missing
+        count_codes(new_b | 0x55555500u, n0, n1, n2);
+        row[nb - 1] = (uint8_t)new_b;
+        counts[(size_t)j * 4 + 0] = s[0] - o0 + n0;
+        counts[(size_t)j * 4 + 1] = s[1] - o1 + n1;
+        counts[(size_t)j * 4 + 2] = s[2] - o2 + n2;
     }
 }
 
