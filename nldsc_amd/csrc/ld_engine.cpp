@@ -735,8 +735,11 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         double blocks = 0;
         if (gpu_plan) blocks = n_items;
         else for (const int4& it : tiled ? e->h_ones : e->h_items) blocks += it.z;
+        // (the default fp4 kernel also skips m.x on diagonal blocks: the transpose of x.m)
+        const bool f4_diag_tr = use_f4 && !tiled && !(e->f4_ring > 0 && max_nc == 1);
         const double products = use_i8 ? blocks * (dom ? 8.0 : 4.0) - (dom ? 2.0 * n_diag : 0.0)
-                                        : blocks * (dom ? 3.0 : 1.0) - (dom ? 1.0 * n_diag : 0.0);
+                                         - (f4_diag_tr ? 1.0 * n_diag : 0.0)
+                                       : blocks * (dom ? 3.0 : 1.0) - (dom ? 1.0 * n_diag : 0.0);
         e->flop_issued = products * 2.0 * BLK * BLK * (double)row_bytes * 4.0;
     }
     if (n_items > 0) {

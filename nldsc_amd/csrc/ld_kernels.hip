@@ -941,7 +941,9 @@ __device__ __forceinline__ void ring_read(uint32_t row_addr, uint32_t col_addr, 
 // SYNC > 0 (workgroups of several waves, band_f4_grp_kernel): a workgroup barrier every SYNC
 // chunk pairs keeps the waves that share strips at the same samples, so the strips they share are
 // served from the CU's L1 / the XCD's L2; an inactive wave (!active) only keeps the barrier count.
-template <bool DOM, int NC, bool DIAG0, int SYNC = 0, int RING = 0>
+// tr (32 x 33 floats of LDS, or nullptr): on a diagonal block, m.x is the transpose of x.m, so its MFMAs
+// are skipped and the epilogue reads x.m transposed through tr.
+template <bool DOM, int NC, bool DIAG0, int SYNC = 0, int RING = 0, bool TR = false>
 __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const uint32_t* __restrict__ geno,
                                              int pitch_words, int n_it, const SnpConst* __restrict__ cst,
                                              const double* __restrict__ pos, const int* __restrict__ Lw,
@@ -949,7 +951,7 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
                                              int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                                              int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
                                              int* __restrict__ ws_acc, bool active = true,
-                                             uint4* ring = nullptr) {
+                                             uint4* ring = nullptr, float* tr = nullptr) {
     constexpr int NS = 32 * (1 + NC);
     const int lane = threadIdx.x & 63;
     const int i = lane & 31, h = lane >> 5;
@@ -1002,7 +1004,7 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         for (int c = 0; c < NC; ++c) {
             gxx[c] = mfma_f4(a.x, b[c].x, gxx[c]);
             gxo[c] = mfma_f4(a.x, b[c].o, gxo[c]);
-            gox[c] = mfma_f4(a.o, b[c].x, gox[c]);
+            if (!(TR && DIAG0 && c == 0)) gox[c] = mfma_f4(a.o, b[c].x, gox[c]);
             goo[c] = mfma_f4(a.o, b[c].o, goo[c]);
             if (DOM) {
                 gxh[c] = mfma_f4(a.x, b[c].h, gxh[c]);
@@ -1082,6 +1084,13 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         mfmas(a1, b1);  // K step 2t+3 (chunk t+1, words 2-3)
     }
     }
+    if constexpr (TR && DIAG0) {  // m.x(a, b) = x.m(b, a): lane (i, h) register r holds (row si(r), column i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tr[((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + i] = gxo[0][r];
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) gox[0][r] = tr[i * 33 + (r & 3) + 8 * (r >> 2) + 4 * h];
+    }
 #pragma unroll
     for (int c = 0; c < NC; ++c)
         pair_epilogue<DOM, f32x16v, true>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * c,
@@ -1156,10 +1165,12 @@ __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __rest
                                                         int own_lo, int own_hi, double* __restrict__ l2_acc,
                                                         double* __restrict__ l2d_acc, int* __restrict__ ws_acc, int xcd) {
     __shared__ BandI8Lds sh;
+    __shared__ float tr[32 * 33];
     const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
 #define NLDSC_BODY(NC_, DIAG_)                                                                                        \
-    band_f4_body<DOM, NC_, DIAG_>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,  \
-                                  rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc)
+    band_f4_body<DOM, NC_, DIAG_, 0, 0, true>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp,      \
+                                              ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, true, \
+                                              nullptr, tr)
     const bool diag = it.y == it.x;
     if (WPS == 1 && it.z == 2) { if (diag) NLDSC_BODY(2, true); else NLDSC_BODY(2, false); }
     else { if (diag) NLDSC_BODY(1, true); else NLDSC_BODY(1, false); }
