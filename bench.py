@@ -98,6 +98,8 @@ def main():
     ap.add_argument("--maf", type=float, default=1e-4)
     ap.add_argument("--std-thr", type=float, default=1e-5)
     ap.add_argument("--additive-only", action="store_true")
+    ap.add_argument("--missing", type=float, default=None,
+                    help="missing-call rate of the synthetic genotypes (default 0.01; C5: 0, imputed hard calls)")
     ap.add_argument("--path", choices=tuple(PATHS), default="f4",
                     help="correlation path: exact Gram on fp4 MFMAs (default), on int8 MFMAs, or fp32 "
                          "standardised values")
@@ -139,10 +141,14 @@ def main():
         args.length_cm = 288.0 * args.n_snp
         args.window_cm = 1.0e6
         args.no_cpu = True
+        if args.missing is None:
+            args.missing = 0.0  # imputed genotypes (hard calls) have no missing calls
+    if args.missing is None:
+        args.missing = 0.01
     N, M = args.n_org, args.n_snp
     flags = (_lib.FLAG_ADDITIVE_ONLY if args.additive_only else 0) | getattr(_lib, PATHS[args.path][0])
     t = time.perf_counter()
-    buf, pos = synth.device_bed(M, N, seed=7 + rank, length_cm=args.length_cm, device=local)
+    buf, pos = synth.device_bed(M, N, seed=7 + rank, length_cm=args.length_cm, missing=args.missing, device=local)
     eng = Engine(local)
     eng.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
     bed_host = None
@@ -225,7 +231,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": dtype,
-            "data": "synthetic (GPU-generated PLINK .bed, AR(1) haplotypes, 1% missing; one chromosome per GPU)",
+            "data": "synthetic (GPU-generated PLINK .bed, AR(1) haplotypes, %g%% missing calls; one chromosome per GPU)"
+                    % (100 * args.missing),
             "config": {
                 "workload": (("C3 (BASELINE.json configs[2]): chr1-like N=%d individuals, M=%d SNPs over %.0f cM, "
                               "%s, --ld-wind-cm %g, maf %g, std-thr %g, rsq 1/M" %

@@ -18,9 +18,11 @@ struct SnpConst {
 // resident rows: after a load, save each row's last byte and fill the pitch padding (rows >= n_snp all 0x55)
 hipError_t launch_pad_rows(uint8_t* img, uint8_t* last, int n_snp, int n_rows, int nb, int row_bytes,
                            hipStream_t st);
-// per run: genotype-code counts with the last byte set to this run's individuals (tail_keep mask)
+// per run: set each row's non-individual slots (last byte outside tail_keep, pitch padding) to `pad`
+// (0x55 missing, or 0x00 for the fp4 kernel) and count genotype codes; n_pad00 = 00-coded non-individual
+// slots per row (discounted from hom-A1)
 hipError_t launch_count_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
-                             int* counts, hipStream_t st);
+                             uint32_t pad, int n_pad00, int* counts, hipStream_t st);
 // flip: per-SNP stored-orientation flags (nullptr: none flipped)
 hipError_t launch_snp_stats(const int* counts, const uint8_t* flip, const double* pos, int n_snp, int n_snp_pad,
                             int n_org, double maf_thr, double std_thr, float2* lut, SnpConst* cst, uint8_t* sflags,

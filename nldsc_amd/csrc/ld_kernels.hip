@@ -20,6 +20,7 @@
 #include <stdint.h>
 #include <climits>
 #include <algorithm>
+#include <type_traits>
 
 #include "ld_kernels.h"
 
@@ -100,10 +101,13 @@ __global__ void __launch_bounds__(256) orient_rows_kernel(uint8_t* __restrict__ 
 }
 
 // Per run: genotype-code counts of every row (one workgroup per SNP, 16-byte non-temporal loads, 8 in
-// flight per thread) with the last byte set to this run's individuals: (saved byte & keep) | (0x55 &
-// ~keep).  HBM-bound read of the image.  The rows are counted as they stand, then one thread swaps the
-// last byte's old codes for the new ones in the counts and writes the byte (after the barrier, so no
-// thread of the loop saw a half-updated row).
+// flight per thread) after setting the row's non-individual slots — the last byte's bit pairs that are
+// not individuals for this run's sample order, (saved byte & keep) | (pad & ~keep), and the pitch padding
+// — to this run's pad code: 0x55 ("missing": x = h = o = 0 for the int8 / fp32 kernels) or 0x00 for the
+// fp4 kernel, whose missing-indicator plane m must be 0 there so that SNPs without missing calls have
+// an all-zero m plane (their m products are skipped); its epilogue counts o = 1 - m over the n_org
+// individual slots only.  The chunks before the last byte's are counted in the loop; after the barrier
+// one thread rebuilds, writes and counts the tail chunks, discounting 00-coded padding (n_pad00 slots).
 typedef uint32_t u32x4nt __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void count_chunk(const u32x4nt o, int& c0, int& c1, int& c2) {
     count_codes(o.x, c0, c1, c2);
@@ -114,22 +118,22 @@ __device__ __forceinline__ void count_chunk(const u32x4nt o, int& c0, int& c1, i
 
 __global__ void __launch_bounds__(256) count_rows_kernel(uint8_t* __restrict__ img, const uint8_t* __restrict__ last,
                                                          int n_snp, int nb, int row_bytes, uint32_t tail_keep,
-                                                         int* __restrict__ counts) {
+                                                         uint32_t pad, int n_pad00, int* __restrict__ counts) {
     const int j = blockIdx.x;
     if (j >= n_snp) return;
     uint8_t* row = img + (size_t)j * (size_t)row_bytes;
     const u32x4nt* src = reinterpret_cast<const u32x4nt*>(row);
-    const int n_chunks = row_bytes / 16, T = blockDim.x;
+    const int c_last = (nb - 1) / 16, T = blockDim.x;
     int c0 = 0, c1 = 0, c2 = 0;
     int c = threadIdx.x;
-    for (; c + 7 * T < n_chunks; c += 8 * T) {
+    for (; c + 7 * T < c_last; c += 8 * T) {
         u32x4nt v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(src + c + u * T);
 #pragma unroll
         for (int u = 0; u < 8; ++u) count_chunk(v[u], c0, c1, c2);
     }
-    for (; c < n_chunks; c += T) count_chunk(__builtin_nontemporal_load(src + c), c0, c1, c2);
+    for (; c < c_last; c += T) count_chunk(__builtin_nontemporal_load(src + c), c0, c1, c2);
     // block reduction (4 waves of 64)
     for (int o = 32; o > 0; o >>= 1) {
         c0 += __shfl_down(c0, o, 64);
@@ -141,17 +145,23 @@ __global__ void __launch_bounds__(256) count_rows_kernel(uint8_t* __restrict__ i
     if ((threadIdx.x & 63) == 0) { red[0][wv] = c0; red[1][wv] = c1; red[2][wv] = c2; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        int s[3] = {0, 0, 0};
-        for (int q = 0; q < (int)(blockDim.x >> 6); ++q)
-            for (int k = 0; k < 3; ++k) s[k] += red[k][q];
-        const uint32_t old_b = row[nb - 1], new_b = ((uint32_t)last[j] & tail_keep) | (0x55u & ~tail_keep);
-        int o0 = 0, o1 = 0, o2 = 0, n0 = 0, n1 = 0, n2 = 0;
-        count_codes(old_b | 0x55555500u, o0, o1, o2);  // the byte's 4 pairs; the rest of the word reads as missing
-        count_codes(new_b | 0x55555500u, n0, n1, n2);
-        row[nb - 1] = (uint8_t)new_b;
-        counts[(size_t)j * 4 + 0] = s[0] - o0 + n0;
-        counts[(size_t)j * 4 + 1] = s[1] - o1 + n1;
-        counts[(size_t)j * 4 + 2] = s[2] - o2 + n2;
+        int s0 = 0, s1 = 0, s2 = 0;
+        for (int q = 0; q < (int)(blockDim.x >> 6); ++q) { s0 += red[0][q]; s1 += red[1][q]; s2 += red[2][q]; }
+        const uint32_t lb = ((uint32_t)last[j] & tail_keep) | (pad & ~tail_keep & 0xFFu);
+        uint32_t* w = reinterpret_cast<uint32_t*>(row);
+        for (int q = 4 * c_last; q < row_bytes / 4; ++q) {  // the tail chunks, word by word
+            uint32_t v = 0;
+            for (int k = 0; k < 4; ++k) {
+                const int p = 4 * q + k;
+                const uint32_t byte = p < nb - 1 ? row[p] : p == nb - 1 ? lb : (pad & 0xFFu);
+                v |= byte << (8 * k);
+            }
+            w[q] = v;
+            count_codes(v, s0, s1, s2);
+        }
+        counts[(size_t)j * 4 + 0] = s0 - n_pad00;
+        counts[(size_t)j * 4 + 1] = s1;
+        counts[(size_t)j * 4 + 2] = s2;
     }
 }
 
@@ -245,6 +255,7 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const uint8_t* 
                 }
             }
         }
+        if (s0 + c1 + s2 < (double)n_org) fl |= 4;  // some individual's call is missing (m plane not all zero)
         maf_out[j] = maf_d;
         rstd_out[j] = (fl & 1) ? rstd_d : qnan;
     }
@@ -660,7 +671,8 @@ __device__ __forceinline__ int xcd_slot(int b, int n) {
 // standardised dots from the 8 integer Gram entries in fp64, r2adj, window/pointer masks, and
 // per-SNP sums (ldscalc.h:33-55).  diag: the pair is a diagonal block (row block == column block).
 // MB: the Gram is in the missing basis {x, h, m} (fp4 path): gxo holds x.m, gox m.x, goo m.m, goh m.h,
-// gho h.m, and `kslots` is the number of sample slots; o = 1 - m over every slot.
+// gho h.m, and `kslots` is the number of individual slots (n_org; the other slots are all-zero in every
+// plane); o = 1 - m over the individual slots.
 template <bool DOM, class Acc, bool MB = false>
 __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpConst* cst, double* s_l2, double* s_l2d,
                                               int* s_wsa, int* s_wsd, int* s_wse, int rb, int cb, bool diag, int i,
@@ -999,27 +1011,43 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     // ones; each is reloaded right after its last word is decoded and read again two K steps
     // later, with no register copies of loads in flight (those would force vmcnt(0)).
     const int last = n_it - 1;
-    auto mfmas = [&](const F4Frag& a, const F4Frag (&b)[NC]) {
+    // RM / CM: the row / column block holds missing calls.  A block without any has an all-zero m plane,
+    // so the products with it are skipped (imputed hard calls: 3 of the 8 MFMAs remain).
+    auto mfmas_v = [&](const F4Frag& a, const F4Frag (&b)[NC], auto RMc, auto CMc) {
+        constexpr bool RM = decltype(RMc)::value, CM = decltype(CMc)::value;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             gxx[c] = mfma_f4(a.x, b[c].x, gxx[c]);
-            gxo[c] = mfma_f4(a.x, b[c].o, gxo[c]);
-            if (!(TR && DIAG0 && c == 0)) gox[c] = mfma_f4(a.o, b[c].x, gox[c]);
-            goo[c] = mfma_f4(a.o, b[c].o, goo[c]);
+            if (CM) gxo[c] = mfma_f4(a.x, b[c].o, gxo[c]);
+            if (RM && !(TR && DIAG0 && c == 0)) gox[c] = mfma_f4(a.o, b[c].x, gox[c]);
+            if (RM && CM) goo[c] = mfma_f4(a.o, b[c].o, goo[c]);
             if (DOM) {
                 gxh[c] = mfma_f4(a.x, b[c].h, gxh[c]);
-                goh[c] = mfma_f4(a.o, b[c].h, goh[c]);
+                if (RM) goh[c] = mfma_f4(a.o, b[c].h, goh[c]);
                 if (!(DIAG0 && c == 0)) {  // on a diagonal block R_i . A_j is the transposed A_j . R_i
                     ghx[c] = mfma_f4(a.h, b[c].x, ghx[c]);
-                    gho[c] = mfma_f4(a.h, b[c].o, gho[c]);
+                    if (CM) gho[c] = mfma_f4(a.h, b[c].o, gho[c]);
                 }
             }
         }
+        if constexpr (RM && CM) {
 #pragma unroll
-        for (int m = 0; m < 8 * NC; ++m) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, NC == 1 ? NLDSC_F4_VPM : 4, 0);
+            for (int m = 0; m < 8 * NC; ++m) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, NC == 1 ? NLDSC_F4_VPM : 4, 0);
+            }
+        } else {  // fewer MFMAs for the same decode: spread the VALU evenly over them
+            constexpr int n_mfma = NC * (1 + CM + RM + (RM && CM) + (DOM ? 2 + RM + CM : 0));
+            constexpr int n_valu = NC * (RM ? 11 : 9) * 2 + NC * (CM ? 11 : 9) * 2;
+#pragma unroll
+            for (int m = 0; m < n_mfma; ++m) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, (n_valu + n_mfma - 1) / n_mfma, 0);
+            }
         }
+    };
+    auto mfmas = [&](const F4Frag& a, const F4Frag (&b)[NC]) {
+        mfmas_v(a, b, std::true_type{}, std::true_type{});
     };
     if constexpr (RING > 0 && NC == 1) {
         // ring slot k: row chunk at [k][0][lane], column chunk at [k][1][lane] (uint4 ring[RING][2][64])
@@ -1050,6 +1078,7 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
     } else {
+    auto kloop = [&](auto RMc, auto CMc) {
     uint4 pr = rowp[0], qr = rowp[2], pc[NC], qc[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) { pc[c] = colp[c][0]; qc[c] = colp[c][2]; }
@@ -1063,25 +1092,37 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         a1 = decode_f4(pr.z, pr.w);
 #pragma unroll
         for (int c = 0; c < NC; ++c) b1[c] = decode_f4(pc[c].z, pc[c].w);
-        mfmas(a0, b0);  // K step 2t   (chunk t, words 0-1)
+        mfmas_v(a0, b0, RMc, CMc);  // K step 2t   (chunk t, words 0-1)
         pr = rowp[2 * min(t + 2, last)];
 #pragma unroll
         for (int c = 0; c < NC; ++c) pc[c] = colp[c][2 * min(t + 2, last)];
         a0 = decode_f4(qr.x, qr.y);
 #pragma unroll
         for (int c = 0; c < NC; ++c) b0[c] = decode_f4(qc[c].x, qc[c].y);
-        mfmas(a1, b1);  // K step 2t+1 (chunk t, words 2-3)
+        mfmas_v(a1, b1, RMc, CMc);  // K step 2t+1 (chunk t, words 2-3)
         a1 = decode_f4(qr.z, qr.w);
 #pragma unroll
         for (int c = 0; c < NC; ++c) b1[c] = decode_f4(qc[c].z, qc[c].w);
-        mfmas(a0, b0);  // K step 2t+2 (chunk t+1, words 0-1)
+        mfmas_v(a0, b0, RMc, CMc);  // K step 2t+2 (chunk t+1, words 0-1)
         qr = rowp[2 * min(t + 3, last)];
 #pragma unroll
         for (int c = 0; c < NC; ++c) qc[c] = colp[c][2 * min(t + 3, last)];
         a0 = decode_f4(pr.x, pr.y);
 #pragma unroll
         for (int c = 0; c < NC; ++c) b0[c] = decode_f4(pc[c].x, pc[c].y);
-        mfmas(a1, b1);  // K step 2t+3 (chunk t+1, words 2-3)
+        mfmas_v(a1, b1, RMc, CMc);  // K step 2t+3 (chunk t+1, words 2-3)
+    }
+    };
+    if constexpr (SYNC > 0) {
+        kloop(std::true_type{}, std::true_type{});
+    } else {
+        // wave-uniform: does the row block / do the column blocks hold a missing call (flag bit 2)?
+        const bool rm = __any(lane < 32 && (sh.info[lane].fl & 4));
+        const bool cm = __any(32 + lane < NS && (sh.info[32 + lane].fl & 4));
+        if (rm && cm) kloop(std::true_type{}, std::true_type{});
+        else if (rm) kloop(std::true_type{}, std::false_type{});
+        else if (cm) kloop(std::false_type{}, std::true_type{});
+        else kloop(std::false_type{}, std::false_type{});
     }
     }
     if constexpr (TR && DIAG0) {  // m.x(a, b) = x.m(b, a): lane (i, h) register r holds (row si(r), column i)
@@ -1095,7 +1136,7 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     for (int c = 0; c < NC; ++c)
         pair_epilogue<DOM, f32x16v, true>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * c,
                                           DIAG0 && c == 0, i, h, gxx[c], gxo[c], gox[c], goo[c], gxh[c], goh[c],
-                                          ghx[c], gho[c], ld_wind, n_org, rsq_thr, 128.0 * n_it);
+                                          ghx[c], gho[c], ld_wind, n_org, rsq_thr, n_org);
     __syncthreads();
     for (int s = lane; s < NS; s += 64) {
         const int g = sh.info[s].g;
@@ -1425,10 +1466,10 @@ hipError_t launch_pad_rows(uint8_t* img, uint8_t* last, int n_snp, int n_rows, i
 }
 
 hipError_t launch_count_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
-                             int* counts, hipStream_t st) {
+                             uint32_t pad, int n_pad00, int* counts, hipStream_t st) {
     if (n_snp <= 0) return hipSuccess;
     hipLaunchKernelGGL(count_rows_kernel, dim3(n_snp), dim3(256), 0, st, img, last, n_snp, nb, row_bytes, tail_keep,
-                       counts);
+                       pad, n_pad00, counts);
     return hipGetLastError();
 }
 

@@ -402,3 +402,31 @@ def test_allele_orientation_is_invisible(name):
         assert_ld_close(out["1", mode], exp, tol=exact, label=f"{name} oriented {mode}")
         same_gram(out["1", mode], out["0", mode], f"{name} {mode}")
     assert_ld_close(out["1", "f32"], exp, label=f"{name} oriented f32")
+
+
+@pytest.mark.parametrize("N", [301, 1003, 4096])
+def test_missing_free_blocks_skip_m_products(engine, N):
+    """32-SNP blocks without any missing call have an all-zero missing-indicator plane, and the fp4 kernel
+    skips every product with it (3 of 8 MFMAs left when both blocks are missing-free, 5 when one is).
+    Blocks alternate between no missing calls, 2 % missing and a single missing call; results equal the
+    int8 kernel (which always computes all 8 products) and the fp64 truth."""
+    from nldsc_amd import synth
+    M = 600
+    spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=8.0, seed=N, missing=0.02)
+    g = synth.genotypes(spec)
+    clean = synth.genotypes(synth.SynthSpec(n_org=N, n_snp=M, length_cm=8.0, seed=N, missing=0.0))
+    blk = np.arange(M) // 32
+    g[blk % 3 == 0] = clean[blk % 3 == 0]       # missing-free blocks
+    one = (blk % 3 == 1) & (np.arange(M) % 32 == 5)
+    g[blk % 3 == 1] = clean[blk % 3 == 1]
+    g[one, N // 2] = -1                           # blocks with a single missing call
+    rows = synth.pack_bed_rows(g)
+    pos = synth.positions_cm(spec)
+    args = (1.0, 0.01, 1e-5, 1.0 / M, pos)
+    engine.load_bed_bytes(synth.bed_bytes(rows), M, N)
+    f4 = engine.run(*args, flags=MODES["f4"])
+    i8 = engine.run(*args, flags=MODES["i8"])
+    same_gram(f4, i8, f"N={N}")
+    exp = O.run_f64(rows, N, *args)
+    assert_ld_close(f4, exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
+                                      maf=(0.0, 0.0)), label=f"missing-free blocks N={N}")
