@@ -141,7 +141,7 @@ struct nldsc_engine {
     int band_i8_nc = 1;    // column blocks per int8-path item (NLDSC_BAND_I8_NC)
     int band_f4_nc = 1;    // column blocks per fp4-path item (NLDSC_BAND_F4_NC)
     int band_mode = 2;     // default correlation path (NLDSC_BAND_MODE=f32|i8|f4): exact fp4
-                           // (int8 above N = 2^22)
+                           // (int8 from N = 2^20)
     bool band_tile = false;  // exact path on skewed 2x2 tiles sharing decoded strips (NLDSC_BAND_TILE)
     bool xcd = true;         // XCD-contiguous workgroup -> item order (NLDSC_XCD=0 disables)
     int f4_grp = -1;         // fp4 path on 4-wave workgroups of skewed 2x2 tiles (NLDSC_BAND_F4_GRP = barrier
@@ -579,7 +579,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     const bool strict = (p->flags & NLDSC_FLAG_STRICT_PLINK_ORDER) != 0;
     int path = (p->flags & NLDSC_FLAG_EXACT_F4) ? 2 : (p->flags & NLDSC_FLAG_EXACT_I8) ? 1
              : (p->flags & NLDSC_FLAG_FP32) ? 0 : e->band_mode;
-    if (path == 2 && N >= (1 << 22)) path = 1;  // fp32 accumulators are exact integers only below 2^24 >= 4N
+    if (path == 2 && N >= (1 << 20)) path = 1;  // fp32 accumulators are exact integers only below 2^24 >= 16N
     const bool use_i8 = path != 0, use_f4 = path == 2;
     const bool f4_grp = use_f4 && e->f4_grp >= 0;
     const bool tiled = (path == 1 && e->band_tile) || f4_grp;

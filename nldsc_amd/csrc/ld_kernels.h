@@ -46,7 +46,7 @@ hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st);
-// exact path on fp4 MFMAs (N < 2^22), items (I, J0, nc <= max_nc, 0)
+// exact path on fp4 MFMAs (N < 2^20), items (I, J0, nc <= max_nc, 0)
 hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,

@@ -694,17 +694,21 @@ __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpCons
         const bool nji = !diag && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
         if (nij || nji) {
             const SnpConst ki = cst[si];
-            const double xx = (double)gxx[r];
-            const double xo = MB ? ki.X - (double)gxo[r] : (double)gxo[r];
-            const double ox = MB ? kj.X - (double)gox[r] : (double)gox[r];
-            const double oo = MB ? ki.Ob + kj.Ob - kslots + (double)goo[r] : (double)goo[r];
+            // MB: the fp4 Gram is over v = m + 2x (the raw 2-bit code placed as an e2m1 value), h and m:
+            // x.x = (v.v - v.m - m.v + m.m) / 4, x.m = (v.m - m.m) / 2, m.x = (m.v - m.m) / 2 (exact)
+            const double mm = (double)goo[r];
+            const double xx = MB ? 0.25 * ((double)gxx[r] - (double)gxo[r] - (double)gox[r] + mm) : (double)gxx[r];
+            const double xo = MB ? ki.X - 0.5 * ((double)gxo[r] - mm) : (double)gxo[r];
+            const double ox = MB ? kj.X - 0.5 * ((double)gox[r] - mm) : (double)gox[r];
+            const double oo = MB ? ki.Ob + kj.Ob - kslots + mm : mm;
             const double aa = (xx - kj.mu * xo - ki.mu * (ox - kj.mu * oo)) / (ki.sa * kj.sa);
             const double r2 = r2_adjusted(aa, n_org);
             if (nij) { atomicAdd(&s_l2[si], r2); atomicAdd(&s_wsa[si], 1); }
             if (nji) { atomicAdd(&s_l2[sj], r2); atomicAdd(&s_wsa[sj], 1); }
             if (DOM) {
                 if (nij && rpj) {  // A_i . R_j -> L2D_i (ldscalc.h:40-46)
-                    const double xh = (double)gxh[r], oh = MB ? kj.H - (double)goh[r] : (double)goh[r];
+                    const double xh = MB ? 0.5 * ((double)gxh[r] - (double)goh[r]) : (double)gxh[r];
+                    const double oh = MB ? kj.H - (double)goh[r] : (double)goh[r];
                     const double ar = (2.0 * xh - kj.beta * xx - kj.c * xo -
                                        ki.mu * (2.0 * oh - kj.beta * ox - kj.c * oo)) / (ki.sa * kj.s);
                     const double rd = r2_adjusted(ar, n_org);
@@ -712,7 +716,8 @@ __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpCons
                     if (rd > rsq_thr) atomicAdd(&s_wse[si], 1);
                 }
                 if (!diag && nji && rpi) {  // R_i . A_j -> L2D_j
-                    const double hx = (double)ghx[r], ho = MB ? ki.H - (double)gho[r] : (double)gho[r];
+                    const double hx = MB ? 0.5 * ((double)ghx[r] - (double)gho[r]) : (double)ghx[r];
+                    const double ho = MB ? ki.H - (double)gho[r] : (double)gho[r];
                     const double ra = (2.0 * hx - ki.beta * xx - ki.c * ox -
                                        kj.mu * (2.0 * ho - ki.beta * xo - ki.c * oo)) / (ki.s * kj.sa);
                     const double rd = r2_adjusted(ra, n_org);
@@ -868,13 +873,13 @@ __global__ void __launch_bounds__(64, WPS) band_i8_kernel(const uint32_t* __rest
 }
 
 // ---- exact path on fp4 MFMAs: v_mfma_scale_f32_32x32x64_f8f6f4 with e2m1 operands ----
-// x in {0, 1, 2} and h, o in {0, 1} are exact e2m1 values (0000, 0010 = 1.0, 0100 = 2.0) and every
-// product is an integer in {0, 1, 2, 4}, so the fp32 accumulators hold exact integer Gram entries
-// as long as they stay below 2^24: entries are <= 4N, so the engine uses this path for N < 2^22.
-// One K step = 64 sample slots = two 16-code words per lane (twice the int8 step, same 32-cycle
-// MFMA), and the 2-bit -> 4-bit spread needs no shuffles because any fixed slot permutation is
-// fine: even code pairs go to the nibbles of one dword, odd pairs to another (11 VALU per word
-// against 27 for the int8 byte spread).
+// v = m + 2x in {0, 1, 2, 4} and h, m in {0, 1} are exact e2m1 values (0000, 0010 = 1.0, 0100 = 2.0,
+// 0110 = 4.0) and every product is an integer <= 16, so the fp32 accumulators hold exact integer Gram
+// entries as long as they stay below 2^24: entries are <= 16N, so the engine uses this path for
+// N < 2^20 (the int8 kernel above).  One K step = 64 sample slots = two 16-code words per lane (twice
+// the int8 step, same 32-cycle MFMA), and the 2-bit -> 4-bit spread needs no shuffles because any fixed
+// slot permutation is fine: even code pairs go to the nibbles of one dword, odd pairs to another (9
+// VALU per word for v, h, m against 27 for the int8 byte spread).
 // The third plane is the missing indicator m = [code 01] (missing call or padding slot) rather than
 // o = 1 - m: genotypes are mostly observed, so o is mostly ones while m is mostly zeros, and an MFMA
 // on mostly-zero operands draws less power (the chip holds a higher clock under this load).  The
@@ -883,22 +888,28 @@ typedef float f32x16v __attribute__((ext_vector_type(16)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 constexpr int E8M0_ONE = 127;  // block scale 2^0
 #ifndef NLDSC_F4_VPM
-#define NLDSC_F4_VPM 5  // VALU instructions interleaved after each MFMA of a one-column-block item
+#define NLDSC_F4_VPM 4  // VALU instructions interleaved after each MFMA of a one-column-block item (3, 5, 6
+                        // and alternating 4/5 measured slower: profiles/r01_ab_vpm.json)
 #endif
 
 struct F4Frag {
     i32x4 x, h, o;
 };
 
+// 16 two-bit codes (b1 b0) -> three e2m1 planes, even code pairs into the nibbles of the *0 dword, odd
+// pairs into the *1 dword (any fixed slot permutation is fine: both operands use it).  The first plane is
+// the code itself moved to nibble bits 2:1 — v = 0 (00 hom A1), 1.0 (01 missing), 2.0 (10 het), 4.0
+// (11 hom A2) = m + 2x — which costs two VALU ops per dword instead of the three of x itself; the
+// epilogue recovers the x products exactly.  h = [b1] and m = [b0 & ~b1] land on bit 1 (1.0).
 __device__ __forceinline__ void decode_f4_word(uint32_t w, int& x0, int& x1, int& h0, int& h1, int& o0, int& o1) {
-    constexpr uint32_t M = 0x22222222u;  // bit 1 of every nibble
-    const uint32_t t0 = w << 1, w2 = w >> 2, t1 = w >> 1;  // lo of even pairs / hi, lo of odd pairs -> bit 1
+    constexpr uint32_t M = 0x22222222u, K6 = 0x66666666u;  // bit 1 / bits 2:1 of every nibble
+    const uint32_t s1 = w << 1, s2 = w >> 1, w2 = w >> 2;
+    x0 = (int)(s1 & K6);       // even (b1, b0) at bits (1, 0) -> (2, 1)
+    x1 = (int)(s2 & K6);       // odd  (b1, b0) at bits (3, 2) -> (2, 1)
     h0 = (int)(w & M);
-    o0 = (int)(t0 & ~w & M);               // m: 01 (missing / padding) -> 0010 (1.0), else 0
-    x0 = (int)((w & M) + (w & t0 & M));    // 10 -> 0010 (1.0), 11 -> 0100 (2.0)
     h1 = (int)(w2 & M);
-    o1 = (int)(t1 & ~w2 & M);
-    x1 = (int)((w2 & M) + (w2 & t1 & M));
+    o0 = (int)(s1 & ~w & M);   // m: code 01 -> 0010 (1.0), else 0
+    o1 = (int)(s2 & ~w2 & M);
 }
 
 __device__ __forceinline__ F4Frag decode_f4(uint32_t wa, uint32_t wb) {
@@ -1038,7 +1049,7 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
             }
         } else {  // fewer MFMAs for the same decode: spread the VALU evenly over them
             constexpr int n_mfma = NC * (1 + CM + RM + (RM && CM) + (DOM ? 2 + RM + CM : 0));
-            constexpr int n_valu = NC * (RM ? 11 : 9) * 2 + NC * (CM ? 11 : 9) * 2;
+            constexpr int n_valu = NC * (RM ? 9 : 7) * 2 + NC * (CM ? 9 : 7) * 2;
 #pragma unroll
             for (int m = 0; m < n_mfma; ++m) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);

@@ -209,7 +209,7 @@ def test_full_size_spot_check_vs_oracle(engine, mode):
 
 def test_f4_gram_is_bitwise_the_int8_gram(engine):
     """The fp4 path's fp32 accumulators hold the same exact integers as the int8 path's int32 ones
-    (N < 2^22), and the fp64 epilogue is the same code: integer outputs, MAF and residual std are
+    (N < 2^20), and the fp64 epilogue is the same code: integer outputs, MAF and residual std are
     identical, and L2 / L2D differ only by the order of the fp64 atomic sums (two runs of one path
     differ the same way; one wrong Gram entry would move r2 by ~1e-6) — at N = 315 599 and on ragged
     small cases (tiny K, padding slots, missing calls)."""
