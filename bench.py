@@ -65,18 +65,22 @@ def cpu_baseline(bed_host: bytes, n_snp, n_org, w, maf, std_thr, rsq, pos, targe
     """Time the C port of the reference CPU path on the first K SNPs (K sized for ~target_s)."""
     from oracle import oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    # two short runs give the fixed window-fill cost and the marginal cost per SNP; then size K
+    # the cost per SNP grows while the first window fills, so K is sized from the marginal cost
+    # between two prefixes grown geometrically until they take a quarter of the target
     def timed(k):
         t = time.perf_counter()
         r = O.run_c(bed_host, n_snp, n_org, w, maf, std_thr, rsq, pos, end=k, threads=threads)
         return r, time.perf_counter() - t
-    k0, k1 = min(n_snp, 16), min(n_snp, 48)
-    _, t_a = timed(k0)
-    r0, t0 = timed(k1)
-    k = k1
-    marginal = max((t0 - t_a) / max(k1 - k0, 1), 1e-4)
-    if t0 < target_s and k1 < n_snp:
-        k = int(min(n_snp, k1 + (target_s - t0) / marginal))
+    k_prev, t_prev = 0, 0.0
+    k = min(n_snp, 16)
+    r0, t0 = timed(k)
+    while t0 < target_s / 4 and k < n_snp:
+        k_prev, t_prev = k, t0
+        k = min(n_snp, 3 * k)
+        r0, t0 = timed(k)
+    if t0 < 0.6 * target_s and k < n_snp:
+        marginal = max((t0 - t_prev) / max(k - k_prev, 1), 1e-6)
+        k = int(min(n_snp, k + (target_s - t0) / marginal))
         r0, t0 = timed(k)
     ws = r0["l2_ws"][:k]
     pairs = float(ws[ws > 0].sum())

@@ -121,7 +121,7 @@ struct nldsc_engine {
     DevBuf<nldsc::SnpConst> cst;
     DevBuf<uint8_t> sflags;
     DevBuf<double> pos, maf, rstd, l2_acc, l2d_acc, l2, l2d;
-    DevBuf<int4> items;
+    DevBuf<int4> items, items2;
     // host scratch
     std::vector<uint8_t> h_flags, h_all_pass;
     std::vector<int> h_L, h_R;
@@ -151,13 +151,14 @@ struct nldsc_engine {
     int band_round = 0;      // exact-path items per launch (NLDSC_BAND_ROUND; 0: one launch, -1: one
                              // launch per round of resident waves)
     int n_cu = 256;
+    bool diag_last = false;  // diagonal block pairs at the end of each XCD run (NLDSC_DIAG_LAST)
     std::vector<int4> h_ones;
 
     ~nldsc_engine() {
         (void)hipSetDevice(device);
         bed.release(); lastb.release(); flip.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
         ws3.release(); lut.release(); cst.release(); sflags.release(); pos.release(); maf.release(); rstd.release();
-        l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release();
+        l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release(); items2.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         if (ev_plan) (void)hipEventDestroy(ev_plan);
         Ew.release(); plan_counts.release(); plan_meta.release(); plan_rows.release();
@@ -416,6 +417,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_TILE_C")) e->tile_c = std::max(1, std::atoi(v));
     if (const char* v = std::getenv("NLDSC_BAND_F4_GRP")) e->f4_grp = std::atoi(v);
     if (const char* v = std::getenv("NLDSC_BAND_F4_RING")) e->f4_ring = std::atoi(v);
+    if (const char* v = std::getenv("NLDSC_DIAG_LAST")) e->diag_last = std::atoi(v) != 0;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
@@ -724,6 +726,13 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     if (bI) HIPCHK(hipMemcpyAsync(e->items.p, e->h_stage.p + 2 * bL, bI, hipMemcpyHostToDevice, st));
     n_items = (int)e->h_items.size();
     for (const int4& it : tiled ? e->h_ones : e->h_items) n_diag += it.x == it.y;
+    }
+    // single-block-pair items in one launch (exact paths): the diagonal items end every XCD run
+    if (e->diag_last && use_i8 && max_nc == 1 && !tiled && (!use_f4 || (e->band_round == 0 && e->f4_ring == 0)) &&
+        n_items > 0) {
+        HIPCHK(e->items2.ensure((size_t)n_items));
+        HIPCHK(nldsc::launch_diag_last(e->items.p, e->items2.p, n_items, e->xcd ? 8 : 1, st));
+        std::swap(e->items, e->items2);
     }
     HIPCHK(hipMemsetAsync(e->l2_acc.p, 0, sizeof(double) * M, st));
     HIPCHK(hipMemsetAsync(e->l2d_acc.p, 0, sizeof(double) * M, st));

@@ -38,6 +38,9 @@ hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const doubl
 hipError_t launch_plan(const double* pos, int n, double w, int own_lo, int own_hi, int* A, int* E, int* R,
                        int2* rows, int* counts, int* meta, hipStream_t st);
 hipError_t launch_plan_emit(int n, const int2* rows, const int* meta, const int* offsets, int4* items, hipStream_t st);
+// stable partition of each of `runs` contiguous runs of the item list (xcd_slot's XCD runs): off-diagonal
+// items first, diagonal ones last, written to `out`
+hipError_t launch_diag_last(const int4* in, int4* out, int n, int runs, hipStream_t st);
 hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                        const float2* lut, const int4* items, const double* pos, const int* Lw, const int* Rw,
                        const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,

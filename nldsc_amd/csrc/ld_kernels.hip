@@ -1526,6 +1526,57 @@ hipError_t launch_plan_emit(int n, const int2* rows, const int* meta, const int*
     return hipGetLastError();
 }
 
+// One workgroup per run of the item list (the XCD runs of xcd_slot, or the whole list): a stable partition
+// of the run into its off-diagonal items, then its diagonal items.  The diagonal block pairs issue 6 of the
+// 8 MFMAs per K step, so a run whose last items are diagonal drains its XCD's slots sooner.
+__global__ void __launch_bounds__(1024) diag_last_kernel(const int4* __restrict__ in, int4* __restrict__ out, int n,
+                                                         int runs) {
+    __shared__ int wave_off[16], total;
+    const int x = blockIdx.x, per = n / runs, rem = n % runs;
+    const int s0 = x * per + min(x, rem), len = per + (x < rem ? 1 : 0);
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    if (t == 0) total = 0;
+    __syncthreads();
+    int cnt = 0;  // pass 1: off-diagonal items of the run (coalesced 16-byte reads)
+    for (int k = t; k < len; k += 1024) cnt += in[s0 + k].x != in[s0 + k].y;
+    atomicAdd(&total, cnt);
+    __syncthreads();
+    const int n_off = total;
+    // pass 2: rounds of 1024 consecutive items; rank within the round from wave ballots
+    int base_off = 0, base_diag = n_off;
+    for (int r = 0; r < len; r += 1024) {
+        const int k = r + t;
+        int4 it = make_int4(0, 0, 0, 0);
+        if (k < len) it = in[s0 + k];
+        const bool off = k < len && it.x != it.y, diag = k < len && it.x == it.y;
+        const uint64_t bo = __ballot(off);
+        const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+        if (lane == 0) wave_off[w] = __popcll(bo);
+        __syncthreads();
+        int pre = 0, all = 0;
+        for (int v = 0; v < 16; ++v) {
+            const int c = wave_off[v];
+            pre += v < w ? c : 0;
+            all += c;
+        }
+        const int n_round = min(1024, len - r);
+        const int wave_base = w * 64;  // items of this wave before it in the round
+        const int in_wave_off = __popcll(bo & below);
+        if (off) out[s0 + base_off + pre + in_wave_off] = it;
+        if (diag) out[s0 + base_diag + (wave_base - pre) + (lane - in_wave_off)] = it;
+        base_off += all;
+        base_diag += n_round - all;
+        __syncthreads();
+    }
+}
+
+hipError_t launch_diag_last(const int4* in, int4* out, int n, int runs, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    runs = max(1, min(runs, n));
+    hipLaunchKernelGGL(diag_last_kernel, dim3(runs), dim3(1024), 0, st, in, out, n, runs);
+    return hipGetLastError();
+}
+
 hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                        const float2* lut, const int4* items, const double* pos, const int* Lw, const int* Rw,
                        const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
