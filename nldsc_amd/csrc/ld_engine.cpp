@@ -151,7 +151,8 @@ struct nldsc_engine {
     int band_round = 0;      // exact-path items per launch (NLDSC_BAND_ROUND; 0: one launch, -1: one
                              // launch per round of resident waves)
     int n_cu = 256;
-    bool diag_last = false;  // diagonal block pairs at the end of each XCD run (NLDSC_DIAG_LAST)
+    int diag_last = 0;  // NLDSC_DIAG_LAST: 1 = diagonal block pairs at the end of each XCD run; 2 = diagonal
+                        // items in a launch of their own before the off-diagonal ones (fp4, timing study)
     std::vector<int4> h_ones;
 
     ~nldsc_engine() {
@@ -417,7 +418,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_TILE_C")) e->tile_c = std::max(1, std::atoi(v));
     if (const char* v = std::getenv("NLDSC_BAND_F4_GRP")) e->f4_grp = std::atoi(v);
     if (const char* v = std::getenv("NLDSC_BAND_F4_RING")) e->f4_ring = std::atoi(v);
-    if (const char* v = std::getenv("NLDSC_DIAG_LAST")) e->diag_last = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_DIAG_LAST")) e->diag_last = std::atoi(v);
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
@@ -731,7 +732,8 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     if (e->diag_last && use_i8 && max_nc == 1 && !tiled && (!use_f4 || (e->band_round == 0 && e->f4_ring == 0)) &&
         n_items > 0) {
         HIPCHK(e->items2.ensure((size_t)n_items));
-        HIPCHK(nldsc::launch_diag_last(e->items.p, e->items2.p, n_items, e->xcd ? 8 : 1, st));
+        HIPCHK(nldsc::launch_diag_last(e->items.p, e->items2.p, n_items,
+                                         e->diag_last == 2 ? 1 : e->xcd ? 8 : 1, st));
         std::swap(e->items, e->items2);
     }
     HIPCHK(hipMemsetAsync(e->l2_acc.p, 0, sizeof(double) * M, st));
@@ -773,7 +775,18 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
             // the strips they share stay in their XCD's L2; a round = the waves resident at once.
             const int per = e->band_round < 0 ? e->n_cu * 4 * (max_nc == 2 ? 1 : 2)
                           : e->band_round > 0 ? e->band_round : n_items;
-            for (int off = 0; off < n_items; off += per)
+            const bool split = e->diag_last == 2 && max_nc == 1 && per == n_items && e->f4_ring == 0 && n_diag > 0;
+            if (split) {  // the diagonal items (the partition's tail) first, in a launch of their own
+                HIPCHK(nldsc::launch_band_f4(dom, 1, n_diag, geno, pitch_words, n_it, e->cst.p,
+                                             e->items.p + (n_items - n_diag), e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p,
+                                             M, p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p,
+                                             e->l2d_acc.p, e->ws_acc.p, e->xcd, st));
+                HIPCHK(nldsc::launch_band_f4(dom, 1, n_items - n_diag, geno, pitch_words, n_it, e->cst.p,
+                                             e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
+                                             (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
+                                             e->ws_acc.p, e->xcd, st));
+            }
+            for (int off = 0; off < n_items && !split; off += per)
                 if (e->f4_ring > 0 && max_nc == 1)
                     HIPCHK(nldsc::launch_band_f4_ring(dom, e->f4_ring, std::min(per, n_items - off), geno,
                                                       pitch_words, n_it, e->cst.p, e->items.p + off, e->pos.p, e->Lw.p,

@@ -11,7 +11,7 @@ blocks), roundR (R fp4 items per launch; round-1 = one launch per round of resid
 4-wave workgroups of skewed 2x2 tiles, a barrier every S chunk pairs; grp0: no barriers), ringD (fp4
 strips through a D-deep per-wave LDS ring filled by LDS-DMA), trR / tcC (item order: tiles of R row blocks x C
 diagonal offsets; tr1 = row-major), noori (keep the file's allele coding instead of minor-homozygote-as-00), dl (diagonal items last in
-every XCD run).
+every XCD run), dsplit (diagonal items in a launch of their own first).
 """
 import argparse
 import json
@@ -73,7 +73,7 @@ def main():
         os.environ["NLDSC_TILE_R"] = tr[0] if tr else "16"
         os.environ["NLDSC_TILE_C"] = tc[0] if tc else "16"
         os.environ["NLDSC_ORIENT"] = "0" if "noori" in parts else "1"
-        os.environ["NLDSC_DIAG_LAST"] = "1" if "dl" in parts else "0"
+        os.environ["NLDSC_DIAG_LAST"] = "2" if "dsplit" in parts else "1" if "dl" in parts else "0"
         e = Engine(0, lib_path=lib)
         v = label
         e.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
