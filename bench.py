@@ -116,6 +116,8 @@ def main():
                          "whole genome (sum M ~ 600k, BASELINE.json configs[3]) spread over the GPUs by LPT; c5: one "
                          "eighth of the imputed genome per GPU (BASELINE.json configs[4]: M ~ 10M over 2.88 Gb, "
                          "--ld-wind-kb 1000; --n-snp defaults to 1.25M per GPU)")
+    ap.add_argument("--concurrent", type=int, default=3,
+                    help="c4: chromosomes computed at once per GPU (host threads, one engine stream each)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -297,12 +299,20 @@ def whole_genome(args, world, rank, local, coll):
     torch.cuda.empty_cache()
     log(f"[rank {rank}] {len(units)} chromosomes resident ({int(Mc[mine].sum())} SNPs) in {time.perf_counter() - t:.1f} s")
 
+    # chromosomes run from `--concurrent` host threads (each engine has its own streams; the ctypes
+    # calls release the GIL), so one chromosome's count, schedule and band tail overlap another's band
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(max_workers=max(1, args.concurrent))
+
+    def one(unit):
+        u, e, pos = unit
+        e.run(args.window_cm, args.maf, args.std_thr, 1.0 / int(Mc[u]), pos, flags=flags)
+        return e.timings()["pairs"]
+
     def step():
-        pairs = 0.0
-        for u, e, pos in units:
-            e.run(args.window_cm, args.maf, args.std_thr, 1.0 / int(Mc[u]), pos, flags=flags)
-            pairs += e.timings()["pairs"]
-        return pairs
+        if args.concurrent <= 1:
+            return sum(one(x) for x in units)
+        return sum(pool.map(one, units))
 
     for _ in range(args.warmup):
         step()
@@ -329,9 +339,10 @@ def whole_genome(args, world, rank, local, coll):
             "data": "synthetic (GPU-generated PLINK .bed per autosome)",
             "config": {"workload": "C4 (BASELINE.json configs[3]): 22 autosomes, sum M=%d (M_c proportional to cM "
                                    "length), N=%d, --ld-wind-cm %g, additive+dominance, chromosome units over GPUs "
-                                   "by LPT" % (int(Mc.sum()), N, args.window_cm),
+                                   "by LPT, %d at once per GPU" % (int(Mc.sum()), N, args.window_cm, args.concurrent),
                        "whole_genome_seconds": t_max / args.steps},
         }), flush=True)
+    pool.shutdown()
     for _, e, _ in units:
         e.close()
     if world > 1:
