@@ -128,6 +128,8 @@ struct nldsc_engine {
     std::vector<int4> h_items;
     HostPinned h_stage;  // pinned upload staging of the plan (L, R, items)
     HostPinned h_meta;   // GPU plan counters (items, diagonal items)
+    HostPinned h_pos;    // pinned copy of the positions (the upload does not stall this thread)
+    HostPinned h_res;    // pinned landing buffer of the result copies (DMA, then host copies out)
     DevBuf<int> Ew, plan_counts, plan_meta;
     DevBuf<int2> plan_rows;
     bool gpu_plan = true;  // band schedule on the GPU for non-negative sorted positions (NLDSC_GPU_PLAN=0: host)
@@ -637,7 +639,9 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
 
     auto t_start = std::chrono::steady_clock::now();
     HIPCHK(hipEventRecord(e->ev[0], st));
-    HIPCHK(hipMemcpyAsync(e->pos.p, p->positions, sizeof(double) * M, hipMemcpyHostToDevice, st));
+    HIPCHK(e->h_pos.ensure(sizeof(double) * (size_t)M));
+    std::memcpy(e->h_pos.p, p->positions, sizeof(double) * (size_t)M);
+    HIPCHK(hipMemcpyAsync(e->pos.p, e->h_pos.p, sizeof(double) * M, hipMemcpyHostToDevice, st));
     if (gpu_plan) {
         // the schedule depends only on the positions: it runs on a second stream beside the count kernel
         HIPCHK(hipEventRecord(e->ev_pos, st));
@@ -816,19 +820,26 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     HIPCHK(nldsc::launch_finalize(e->Lw.p, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, own_begin, own_end, dom,
                                   e->l2.p, e->l2d.p, e->ws3.p, st));
     HIPCHK(hipEventRecord(e->ev[5], st));
+    // the owned slices land in pinned memory by DMA (pageable copies are staged by the runtime, slower),
+    // then go to the caller's arrays
     const int n_own = own_end - own_begin;
+    const size_t o = own_begin, b8 = sizeof(double) * (size_t)std::max(n_own, 0), b4 = sizeof(int) * (size_t)std::max(n_own, 0);
+    double* const dsrc[4] = {e->l2.p + o, e->l2d.p + o, e->maf.p + o, e->rstd.p + o};
+    double* const ddst[4] = {r->l2 + o, r->l2d + o, r->maf + o, r->residuals_std + o};
+    int* const isrc[3] = {e->ws3.p + o, e->ws3.p + M + o, e->ws3.p + 2 * (size_t)M + o};
+    int32_t* const idst[3] = {r->l2_ws + o, r->l2d_ws + o, r->l2d_wse + o};
     if (n_own > 0) {
-        const size_t o = own_begin;
-        HIPCHK(hipMemcpyAsync(r->l2 + o, e->l2.p + o, sizeof(double) * n_own, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(r->l2d + o, e->l2d.p + o, sizeof(double) * n_own, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(r->maf + o, e->maf.p + o, sizeof(double) * n_own, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(r->residuals_std + o, e->rstd.p + o, sizeof(double) * n_own, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(r->l2_ws + o, e->ws3.p + o, sizeof(int) * n_own, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(r->l2d_ws + o, e->ws3.p + M + o, sizeof(int) * n_own, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(r->l2d_wse + o, e->ws3.p + 2 * (size_t)M + o, sizeof(int) * n_own, hipMemcpyDeviceToHost,
-                              st));
+        HIPCHK(e->h_res.ensure(4 * b8 + 3 * b4));
+        for (int k = 0; k < 4; ++k)
+            HIPCHK(hipMemcpyAsync(e->h_res.p + k * b8, dsrc[k], b8, hipMemcpyDeviceToHost, st));
+        for (int k = 0; k < 3; ++k)
+            HIPCHK(hipMemcpyAsync(e->h_res.p + 4 * b8 + k * b4, isrc[k], b4, hipMemcpyDeviceToHost, st));
     }
     HIPCHK(hipStreamSynchronize(st));
+    if (n_own > 0) {
+        for (int k = 0; k < 4; ++k) std::memcpy(ddst[k], e->h_res.p + k * b8, b8);
+        for (int k = 0; k < 3; ++k) std::memcpy(idst[k], e->h_res.p + 4 * b8 + k * b4, b4);
+    }
     auto t_end = std::chrono::steady_clock::now();
 
     float f = 0;
