@@ -1026,6 +1026,9 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     // so the products with it are skipped (imputed hard calls: 3 of the 8 MFMAs remain).
     auto mfmas_v = [&](const F4Frag& a, const F4Frag (&b)[NC], auto RMc, auto CMc) {
         constexpr bool RM = decltype(RMc)::value, CM = decltype(CMc)::value;
+#ifdef NLDSC_F4_PRIO  // study build: raised wave priority over each MFMA group
+        __builtin_amdgcn_s_setprio(NLDSC_F4_PRIO);
+#endif
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             gxx[c] = mfma_f4(a.x, b[c].x, gxx[c]);
@@ -1056,6 +1059,9 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
                 __builtin_amdgcn_sched_group_barrier(0x002, (n_valu + n_mfma - 1) / n_mfma, 0);
             }
         }
+#ifdef NLDSC_F4_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
     };
     auto mfmas = [&](const F4Frag& a, const F4Frag (&b)[NC]) {
         mfmas_v(a, b, std::true_type{}, std::true_type{});
