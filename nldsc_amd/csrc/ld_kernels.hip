@@ -930,6 +930,10 @@ __device__ __forceinline__ F4Frag decode_f4(uint32_t wa, uint32_t wb) {
     return f;
 }
 
+#ifndef NLDSC_F4_PERM
+#define NLDSC_F4_PERM 1426357  // 01426357: xx, xo, xh, ox, hx, oo, oh, ho (band_f4_body)
+#endif
+
 __device__ __forceinline__ f32x16v mfma_f4(const i32x4& a, const i32x4& b, const f32x16v& c) {
     const i32x8 A = {a[0], a[1], a[2], a[3], 0, 0, 0, 0}, B = {b[0], b[1], b[2], b[3], 0, 0, 0, 0};
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, c, 4, 4, 0, E8M0_ONE, 0, E8M0_ONE);
@@ -1029,18 +1033,27 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
 #ifdef NLDSC_F4_PRIO  // study build: raised wave priority over each MFMA group
         __builtin_amdgcn_s_setprio(NLDSC_F4_PRIO);
 #endif
+        // Issue order of the 8 products = the digits of NLDSC_F4_PERM (0 xx, 1 xo, 2 ox, 3 oo, 4 xh, 5 oh,
+        // 6 hx, 7 ho).  The order alone moves the band kernel by up to 12 % (decode interleave, register
+        // assignment); the default xx, xo, xh, ox, hx, oo, oh, ho measured best of 18 orders, -1.2 % vs
+        // 0..7 (profiles/r01_ab_perm*.json).  On a diagonal block m.x and h.x are the transposes of x.m
+        // and x.h (skipped).
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-            gxx[c] = mfma_f4(a.x, b[c].x, gxx[c]);
-            if (CM) gxo[c] = mfma_f4(a.x, b[c].o, gxo[c]);
-            if (RM && !(TR && DIAG0 && c == 0)) gox[c] = mfma_f4(a.o, b[c].x, gox[c]);
-            if (RM && CM) goo[c] = mfma_f4(a.o, b[c].o, goo[c]);
-            if (DOM) {
-                gxh[c] = mfma_f4(a.x, b[c].h, gxh[c]);
-                if (RM) goh[c] = mfma_f4(a.o, b[c].h, goh[c]);
-                if (!(DIAG0 && c == 0)) {  // on a diagonal block R_i . A_j is the transposed A_j . R_i
-                    ghx[c] = mfma_f4(a.h, b[c].x, ghx[c]);
-                    if (CM) gho[c] = mfma_f4(a.h, b[c].o, gho[c]);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                constexpr long long perm = NLDSC_F4_PERM;
+                long long d = perm;
+                for (int u = 0; u < 7 - q; ++u) d /= 10;
+                switch ((int)(d % 10)) {
+                    case 0: gxx[c] = mfma_f4(a.x, b[c].x, gxx[c]); break;
+                    case 1: if (CM) gxo[c] = mfma_f4(a.x, b[c].o, gxo[c]); break;
+                    case 2: if (RM && !(TR && DIAG0 && c == 0)) gox[c] = mfma_f4(a.o, b[c].x, gox[c]); break;
+                    case 3: if (RM && CM) goo[c] = mfma_f4(a.o, b[c].o, goo[c]); break;
+                    case 4: if (DOM) gxh[c] = mfma_f4(a.x, b[c].h, gxh[c]); break;
+                    case 5: if (DOM && RM) goh[c] = mfma_f4(a.o, b[c].h, goh[c]); break;
+                    case 6: if (DOM && !(DIAG0 && c == 0)) ghx[c] = mfma_f4(a.h, b[c].x, ghx[c]); break;
+                    default: if (DOM && CM && !(DIAG0 && c == 0)) gho[c] = mfma_f4(a.h, b[c].o, gho[c]); break;
                 }
             }
         }
