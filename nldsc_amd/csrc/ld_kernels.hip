@@ -1126,6 +1126,9 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         pr = rowp[2 * min(t + 2, last)];
 #pragma unroll
         for (int c = 0; c < NC; ++c) pc[c] = colp[c][2 * min(t + 2, last)];
+#ifdef NLDSC_F4_LDPIN  // study build: keep the prefetch loads where they are issued (no sinking)
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         a0 = decode_f4(qr.x, qr.y);
 #pragma unroll
         for (int c = 0; c < NC; ++c) b0[c] = decode_f4(qc[c].x, qc[c].y);
@@ -1137,6 +1140,9 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         qr = rowp[2 * min(t + 3, last)];
 #pragma unroll
         for (int c = 0; c < NC; ++c) qc[c] = colp[c][2 * min(t + 3, last)];
+#ifdef NLDSC_F4_LDPIN
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         a0 = decode_f4(pr.x, pr.y);
 #pragma unroll
         for (int c = 0; c < NC; ++c) b0[c] = decode_f4(pc[c].x, pc[c].y);
