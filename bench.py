@@ -44,7 +44,12 @@ def pmc_traffic(kernel_key: str, n_org: int, n_snp: int):
     """HBM-side bytes per launch of `kernel_key` from the newest committed rocprofv3 PMC summary
     (profiles/*_pmc*.json, measured on the same C3 workload), or None."""
     import glob
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc*.json")), reverse=True):
+    # profiles/pmc_current.txt names the summary measured on the current kernels; then any other
+    current = os.path.join(REPO, "profiles", "pmc_current.txt")
+    first = []
+    if os.path.exists(current):
+        first = [os.path.join(REPO, "profiles", open(current).read().strip())]
+    for path in first + sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc*.json")), reverse=True):
         try:
             doc = json.load(open(path))
         except (OSError, ValueError):
