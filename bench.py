@@ -121,6 +121,9 @@ def main():
                          "whole genome (sum M ~ 600k, BASELINE.json configs[3]) spread over the GPUs by LPT; c5: one "
                          "eighth of the imputed genome per GPU (BASELINE.json configs[4]: M ~ 10M over 2.88 Gb, "
                          "--ld-wind-kb 1000; --n-snp defaults to 1.25M per GPU)")
+    ap.add_argument("--split", action="store_true",
+                    help="c3 with N > 1: split ONE chromosome over the GPUs by position (strong scaling) instead of "
+                         "one chromosome per GPU (weak scaling, the default)")
     ap.add_argument("--concurrent", type=int, default=3,
                     help="c4: chromosomes computed at once per GPU (host threads, one engine stream each)")
     args = ap.parse_args()
@@ -159,9 +162,26 @@ def main():
     N, M = args.n_org, args.n_snp
     flags = (_lib.FLAG_ADDITIVE_ONLY if args.additive_only else 0) | getattr(_lib, PATHS[args.path][0])
     t = time.perf_counter()
-    buf, pos = synth.device_bed(M, N, seed=7 + rank, length_cm=args.length_cm, missing=args.missing, device=local)
+    split = args.split and world > 1
+    buf, pos = synth.device_bed(M, N, seed=7 if split else 7 + rank, length_cm=args.length_cm,
+                                missing=args.missing, device=local)
     eng = Engine(local)
-    eng.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
+    own = (0, M)
+    if split:
+        # --split: ONE chromosome position-sharded over the ranks (strong scaling): rank g keeps only its
+        # owned SNP range plus one window of halo rows resident and computes the owned SNPs
+        from nldsc_amd.distributed import gather_ranges, halo_range, shard_ranges
+        lo, hi = shard_ranges(pos, args.window_cm, world)[rank]
+        a, b = halo_range(pos, args.window_cm, (lo, hi))
+        nb = (N + 3) // 4
+        sl = torch.cat([buf[:3], buf[3 + a * nb:3 + b * nb]])
+        eng.load_bed_device(sl.data_ptr(), sl.numel(), b - a, N)
+        del sl
+        own, own_rel, pos = (lo, hi), (lo - a, hi - a), pos[a:b]
+        full_local = {k: np.empty(M, np.float64 if k in ("l2", "l2d", "maf", "residuals_std") else np.int32)
+                      for k in ("l2", "l2d", "maf", "residuals_std", "l2_ws", "l2d_ws", "l2d_wse")}
+    else:
+        eng.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
     bed_host = None
     if rank == 0 and world == 1 and not args.no_cpu:
         bed_host = buf.cpu().numpy().tobytes()
@@ -174,6 +194,12 @@ def main():
 
     def step():
         nonlocal out
+        if split:  # owned slice of the one chromosome, then the table assembled on rank 0 (RCCL over xGMI)
+            out = eng.run(w, args.maf, args.std_thr, rsq, pos, own=own_rel, flags=flags, out=out)
+            for k, v in full_local.items():
+                v[own[0]:own[1]] = out[k][own_rel[0]:own_rel[1]]
+            gather_ranges(full_local, own, M, device=coll)
+            return eng.timings()
         out = eng.run(w, args.maf, args.std_thr, rsq, pos, flags=flags, out=out)
         if world > 1:  # assemble the score tables on rank 0 (RCCL over xGMI)
             tab = torch.from_numpy(np.stack([out["l2"], out["l2d"], out["maf"], out["residuals_std"],
@@ -220,7 +246,7 @@ def main():
                     "kernel": kname, "flop_alg_per_launch": flop}
         traffic, traffic_src = pmc_traffic(kname.split("<")[0], N, M)
         roof.update(frac=roof["achieved"] / peak, traffic=traffic, traffic_source=traffic_src,
-                    algorithmic_bytes_per_launch=M * 4 * ((((N + 3) // 4) + 31) // 32 * 8),
+                    algorithmic_bytes_per_launch=eng.n_snp * 4 * ((((N + 3) // 4) + 31) // 32 * 8),
                     avg_launch_ms=band_ms,
                     issued_per_launch=tims[-1]["flop_issued"], work_items=tims[-1]["band_items"],
                     mfma_pipe_frac=tims[-1]["flop_issued"] / (band_ms * 1e-3) / 1e12 / peak,
@@ -239,11 +265,11 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * t_max / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if split else "weak",
             "vs_baseline": None,
             "dtype": dtype,
-            "data": "synthetic (GPU-generated PLINK .bed, AR(1) haplotypes, %g%% missing calls; one chromosome per GPU)"
-                    % (100 * args.missing),
+            "data": "synthetic (GPU-generated PLINK .bed, AR(1) haplotypes, %g%% missing calls; %s)"
+                    % (100 * args.missing, "one chromosome split over the GPUs" if split else "one chromosome per GPU"),
             "config": {
                 "workload": (("C3 (BASELINE.json configs[2]): chr1-like N=%d individuals, M=%d SNPs over %.0f cM, "
                               "%s, --ld-wind-cm %g, maf %g, std-thr %g, rsq 1/M" %
@@ -256,7 +282,9 @@ def main():
                                "additive+dominance", w, args.maf, args.std_thr))),
                 "n_org": N, "n_snp": M, "mean_window": float(ws[ws > 0].mean()),
                 "pairs_per_step_per_gpu": tims[-1]["pairs"],
-                "parallelism": f"position sharding, one chromosome unit per GPU x {world}",
+                "parallelism": (f"one chromosome position-sharded over {world} GPUs (owned SNP ranges balanced by "
+                                f"pair work, one window of halo rows per rank, score table gathered over RCCL)"
+                                if split else f"position sharding, one chromosome unit per GPU x {world}"),
             },
             "roofline": roof,
             "stages_ms": stages,
