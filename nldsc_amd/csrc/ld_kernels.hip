@@ -1057,7 +1057,10 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
                 }
             }
         }
-        if constexpr (RM && CM) {
+        // full 8-product steps: VPM VALU after each MFMA; otherwise (additive-only items, missing-free
+        // blocks) the decode is spread evenly over the MFMAs there are (additive-only C2: -6.6 % band time,
+        // profiles/r01_ab_addspread.json)
+        if constexpr (RM && CM && DOM) {
 #pragma unroll
             for (int m = 0; m < 8 * NC; ++m) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);

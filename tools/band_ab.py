@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--variants", default="wps1:nc2,wps2:nc2,wps2:nc1,wps1:nc1")
     ap.add_argument("--window", type=float, default=1.0, help="window in position units (C5: 1e6 bp)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--additive-only", action="store_true", help="additive L2 only (C2)")
     ap.add_argument("--major", action="store_true",
                     help="swap hom-A1/hom-A2 codes of every SNP (.bim A2 = the major allele, as in PLINK's usual "
                          "A1 = minor convention)")
@@ -84,7 +85,7 @@ def main():
     outs = {}
     for r in range(args.rounds + 1):
         for v, e in engines.items():
-            o = e.run(args.window, 1e-4, 1e-5, 1.0 / M, pos)
+            o = e.run(args.window, 1e-4, 1e-5, 1.0 / M, pos, flags=2 if args.additive_only else 0)  # _lib.FLAG_ADDITIVE_ONLY
             t = e.timings()
             if r > 0:
                 res[v].append(t)
