@@ -60,13 +60,28 @@ class _Prefetch:
         return self.data
 
 
+def _readahead(path: str) -> None:
+    """Ask the kernel to start reading `path` into the page cache (asynchronous readahead)."""
+    try:
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_WILLNEED)
+        finally:
+            os.close(fd)
+    except (OSError, AttributeError):
+        pass
+
+
 def _default_runner(device: int):
+    """The GPU engine, fed by its own file reader (file -> pinned slots -> pitched H2D copies overlapping
+    the reads, ~20 GB/s from the page cache) instead of a host array copied from pageable memory."""
     from ..engine import Engine
     eng = Engine(device)
 
-    def run(bed: np.ndarray, n_snp: int, n_org: int, ld_wind, maf, std_thr, rsq_thr, positions, flags):
-        eng.load_bed_bytes(bed, n_snp, n_org)
+    def run(bed_path: str, n_snp: int, n_org: int, ld_wind, maf, std_thr, rsq_thr, positions, flags):
+        eng.load_bed_file(bed_path, n_snp, n_org)
         return eng.run(ld_wind, maf, std_thr, rsq_thr, positions, flags=flags), eng.timings()
+    run.wants_path = True
     return run
 
 
@@ -99,11 +114,22 @@ def estimate_lds_genome(bfile: str, ld_wind: float, wind_metric: str, maf_thr: f
         local = int(os.environ.get("LOCAL_RANK", "0")) if device is None else int(device)
         runner = _default_runner(local)
     results = {}
-    pre = _Prefetch(meta[mine[0]]["stem"] + ".bed") if mine else None
+    # a path-fed runner (the engine's own reader) gets the next file read ahead into the page cache;
+    # other runners get the bytes, read by a host thread while the current chromosome computes
+    by_path = getattr(runner, "wants_path", False)
+    pre = None
+    if mine and not by_path:
+        pre = _Prefetch(meta[mine[0]]["stem"] + ".bed")
     for k, u in enumerate(mine):
         m = meta[u]
-        bed = pre.get()
-        pre = _Prefetch(meta[mine[k + 1]]["stem"] + ".bed") if k + 1 < len(mine) else None
+        nxt = meta[mine[k + 1]]["stem"] + ".bed" if k + 1 < len(mine) else None
+        if by_path:
+            bed = m["stem"] + ".bed"
+            if nxt is not None:
+                threading.Thread(target=_readahead, args=(nxt,), daemon=True).start()
+        else:
+            bed = pre.get()
+            pre = _Prefetch(nxt) if nxt is not None else None
         n_snp = m["bim"].n_snp
         rsq = RSQThreshold(1.0 / n_snp if rsq_thr is None else rsq_thr).data
         t0 = time.perf_counter()
