@@ -43,8 +43,8 @@ extern "C" {
 #define NLDSC_FLAG_ADDITIVE_ONLY 2u      /* skip the dominance terms: l2d = NaN, l2d_ws = l2d_wse = -1 */
 #define NLDSC_FLAG_EXACT_I8 4u           /* correlations from exact integer Gram products (int8 MFMA) */
 #define NLDSC_FLAG_FP32 8u               /* correlations from fp32 standardised values (fp32 MFMA) */
-#define NLDSC_FLAG_EXACT_F4 16u          /* exact integer Gram products on fp4 MFMAs (n_org < 2^20; larger
-                                            cohorts fall back to EXACT_I8) */
+#define NLDSC_FLAG_EXACT_F4 16u          /* exact integer Gram products on fp4 MFMAs (n_org < 2^27, segmented
+                                            above 2^19; larger cohorts fall back to EXACT_I8) */
 /* None of EXACT_F4, EXACT_I8, FP32: the engine default, EXACT_F4 ($NLDSC_BAND_MODE = f4 | i8 | f32
  * overrides it). */
 

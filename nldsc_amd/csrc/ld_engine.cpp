@@ -143,7 +143,7 @@ struct nldsc_engine {
     int band_i8_nc = 1;    // column blocks per int8-path item (NLDSC_BAND_I8_NC)
     int band_f4_nc = 1;    // column blocks per fp4-path item (NLDSC_BAND_F4_NC)
     int band_mode = 2;     // default correlation path (NLDSC_BAND_MODE=f32|i8|f4): exact fp4
-                           // (int8 from N = 2^20)
+                           // (int8 from N = 2^27)
     bool band_tile = false;  // exact path on skewed 2x2 tiles sharing decoded strips (NLDSC_BAND_TILE)
     bool xcd = true;         // XCD-contiguous workgroup -> item order (NLDSC_XCD=0 disables)
     int f4_grp = -1;         // fp4 path on 4-wave workgroups of skewed 2x2 tiles (NLDSC_BAND_F4_GRP = barrier
@@ -584,11 +584,14 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     const bool strict = (p->flags & NLDSC_FLAG_STRICT_PLINK_ORDER) != 0;
     int path = (p->flags & NLDSC_FLAG_EXACT_F4) ? 2 : (p->flags & NLDSC_FLAG_EXACT_I8) ? 1
              : (p->flags & NLDSC_FLAG_FP32) ? 0 : e->band_mode;
-    if (path == 2 && N >= (1 << 20)) path = 1;  // fp32 accumulators are exact integers only below 2^24 >= 16N
+    // fp4 Gram entries are <= 16N: the segmented fp4 kernel keeps them exact in int32 up to N < 2^27
+    if (path == 2 && N >= (1 << 27)) path = 1;
     const bool use_i8 = path != 0, use_f4 = path == 2;
-    const bool f4_grp = use_f4 && e->f4_grp >= 0;
+    // rows longer than one fp32-exact segment: the segmented kernel (single blocks, register strips)
+    const bool f4_seg = use_f4 && row_pitch(N) / CHUNK_BYTES > nldsc::F4_SEG_CHUNKS;
+    const bool f4_grp = use_f4 && !f4_seg && e->f4_grp >= 0;
     const bool tiled = (path == 1 && e->band_tile) || f4_grp;
-    const int max_nc = tiled ? 1 : use_f4 ? e->band_f4_nc : use_i8 ? e->band_i8_nc : e->band_nc;
+    const int max_nc = tiled || f4_seg ? 1 : use_f4 ? e->band_f4_nc : use_i8 ? e->band_i8_nc : e->band_nc;
     HIPCHK(hipSetDevice(e->device));
     hipStream_t st = e->stream;
 
@@ -754,7 +757,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         if (gpu_plan) blocks = n_items;
         else for (const int4& it : tiled ? e->h_ones : e->h_items) blocks += it.z;
         // (the default fp4 kernel also skips m.x on diagonal blocks: the transpose of x.m)
-        const bool f4_diag_tr = use_f4 && !tiled && !(e->f4_ring > 0 && max_nc == 1);
+        const bool f4_diag_tr = use_f4 && !tiled && !(e->f4_ring > 0 && max_nc == 1 && !f4_seg);
         const double products = use_i8 ? blocks * (dom ? 8.0 : 4.0) - (dom ? 2.0 * n_diag : 0.0)
                                          - (f4_diag_tr ? 1.0 * n_diag : 0.0)
                                        : blocks * (dom ? 3.0 : 1.0) - (dom ? 1.0 * n_diag : 0.0);
@@ -791,7 +794,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
                                              e->ws_acc.p, e->xcd, st));
             }
             for (int off = 0; off < n_items && !split; off += per)
-                if (e->f4_ring > 0 && max_nc == 1)
+                if (e->f4_ring > 0 && max_nc == 1 && !f4_seg)
                     HIPCHK(nldsc::launch_band_f4_ring(dom, e->f4_ring, std::min(per, n_items - off), geno,
                                                       pitch_words, n_it, e->cst.p, e->items.p + off, e->pos.p, e->Lw.p,
                                                       e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr,

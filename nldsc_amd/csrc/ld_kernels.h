@@ -49,7 +49,11 @@ hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st);
-// exact path on fp4 MFMAs (N < 2^20), items (I, J0, nc <= max_nc, 0)
+// K-loop chunks (128 samples each) per fp32 accumulation segment of the fp4 path: rows longer than this
+// (N > 2^19) run the segmented kernel, which folds the fp32 Gram into int32 after every segment
+constexpr int F4_SEG_CHUNKS = 4096;
+// exact path on fp4 MFMAs (N < 2^27), items (I, J0, nc <= max_nc, 0); max_nc must be 1 when
+// n_it > F4_SEG_CHUNKS
 hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,

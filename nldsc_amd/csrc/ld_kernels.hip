@@ -970,7 +970,11 @@ __device__ __forceinline__ void ring_read(uint32_t row_addr, uint32_t col_addr, 
 // served from the CU's L1 / the XCD's L2; an inactive wave (!active) only keeps the barrier count.
 // tr (32 x 33 floats of LDS, or nullptr): on a diagonal block, m.x is the transpose of x.m, so its MFMAs
 // are skipped and the epilogue reads x.m transposed through tr.
-template <bool DOM, int NC, bool DIAG0, int SYNC = 0, int RING = 0, bool TR = false>
+// SEG > 0 (NC == 1, no ring / sync; rows longer than SEG chunks, N > 2^19): the K loop runs in segments of
+// SEG chunks (128 samples each, so a segment adds at most 16 * 128 * SEG <= 2^23 to an entry and the fp32
+// accumulators stay exact integers); after each segment the multiples of 2^16 are moved out into packed
+// 16-bit counters, and the epilogue sees int32 entries, exact while every entry is <= 16N < 2^31.
+template <bool DOM, int NC, bool DIAG0, int SYNC = 0, int RING = 0, bool TR = false, int SEG = 0>
 __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const uint32_t* __restrict__ geno,
                                              int pitch_words, int n_it, const SnpConst* __restrict__ cst,
                                              const double* __restrict__ pos, const int* __restrict__ Lw,
@@ -1111,16 +1115,18 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
     } else {
-    auto kloop = [&](auto RMc, auto CMc) {
-    uint4 pr = rowp[0], qr = rowp[2], pc[NC], qc[NC];
+    // chunks [t_lo, t_hi), t_lo and t_hi even (the default kernel: 0 and n_it)
+    auto kloop = [&](auto RMc, auto CMc, const int t_lo, const int t_hi) {
+    const int last = t_hi - 1;
+    uint4 pr = rowp[2 * t_lo], qr = rowp[2 * t_lo + 2], pc[NC], qc[NC];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) { pc[c] = colp[c][0]; qc[c] = colp[c][2]; }
+    for (int c = 0; c < NC; ++c) { pc[c] = colp[c][2 * t_lo]; qc[c] = colp[c][2 * t_lo + 2]; }
     // two named fragment sets: set 1 is decoded while set 0 feeds the MFMAs and vice versa, so no
     // fragment is copied (a single rotating set costs ~12 v_mov per K step)
     F4Frag a0 = decode_f4(pr.x, pr.y), a1, b0[NC], b1[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) b0[c] = decode_f4(pc[c].x, pc[c].y);
-    for (int t = 0; t < n_it; t += 2) {
+    for (int t = t_lo; t < t_hi; t += 2) {
         if (SYNC > 0 && (t >> 1) % (SYNC > 0 ? SYNC : 1) == 0) __builtin_amdgcn_s_barrier();
         a1 = decode_f4(pr.z, pr.w);
 #pragma unroll
@@ -1153,17 +1159,82 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     }
     };
     if constexpr (SYNC > 0) {
-        kloop(std::true_type{}, std::true_type{});
+        kloop(std::true_type{}, std::true_type{}, 0, n_it);
     } else {
         // wave-uniform: does the row block / do the column blocks hold a missing call (flag bit 2)?
         const bool rm = __any(lane < 32 && (sh.info[lane].fl & 4));
         const bool cm = __any(32 + lane < NS && (sh.info[32 + lane].fl & 4));
-        if (rm && cm) kloop(std::true_type{}, std::true_type{});
-        else if (rm) kloop(std::true_type{}, std::false_type{});
-        else if (cm) kloop(std::false_type{}, std::true_type{});
-        else kloop(std::false_type{}, std::false_type{});
+        auto run = [&](const int t_lo, const int t_hi) {
+            if (rm && cm) kloop(std::true_type{}, std::true_type{}, t_lo, t_hi);
+            else if (rm) kloop(std::true_type{}, std::false_type{}, t_lo, t_hi);
+            else if (cm) kloop(std::false_type{}, std::true_type{}, t_lo, t_hi);
+            else kloop(std::false_type{}, std::false_type{}, t_lo, t_hi);
+        };
+        if constexpr (SEG == 0) {
+            run(0, n_it);
+        } else {
+            static_assert(NC == 1 && RING == 0, "segmented K loop: one column block, register strips");
+            i32x16 ixx[1] = {}, ixo[1] = {}, iox[1] = {}, ioo[1] = {}, ixh[1] = {}, ioh[1] = {}, ihx[1] = {},
+                   iho[1] = {};
+            if constexpr (DOM) {
+            // add+dom (1 wave / SIMD either way): the fp32 Gram is added into int32 accumulators after every
+            // segment (measured 13 % faster than the packed counters below at N = 1 100 003)
+            for (int t0 = 0; t0 < n_it; t0 += SEG) {
+                run(t0, min(t0 + SEG, n_it));
+                ixx[0] += __builtin_convertvector(gxx[0], i32x16); ixo[0] += __builtin_convertvector(gxo[0], i32x16);
+                iox[0] += __builtin_convertvector(gox[0], i32x16); ioo[0] += __builtin_convertvector(goo[0], i32x16);
+                ixh[0] += __builtin_convertvector(gxh[0], i32x16); ioh[0] += __builtin_convertvector(goh[0], i32x16);
+                ihx[0] += __builtin_convertvector(ghx[0], i32x16); iho[0] += __builtin_convertvector(gho[0], i32x16);
+                gxx[0] = gxo[0] = gox[0] = goo[0] = gxh[0] = goh[0] = ghx[0] = gho[0] = f32x16v{};
+            }
+            } else {
+            // additive-only: after a segment every entry is < 2^16 + 2^23: its multiples of 2^16 move to a
+            // 16-bit counter (entry / 2^16 <= 16N / 2^16 < 2^15 for N < 2^27) and the fp32 remainder, < 2^16,
+            // stays in the accumulator (exact: both parts are integers below 2^24).  Two products share one
+            // 32-bit counter register, so the fold costs 32 registers, not 64, and the kernel keeps 2 waves
+            // per SIMD.
+            typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+            u32x16 kxx = {}, kox = {};  // (xx | xo << 16), (ox | oo << 16)
+            auto fold2 = [](f32x16v& a, f32x16v& b, u32x16& k) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float qa = floorf(a[r] * (1.0f / 65536.0f)), qb = floorf(b[r] * (1.0f / 65536.0f));
+                    a[r] = fmaf(qa, -65536.0f, a[r]);
+                    b[r] = fmaf(qb, -65536.0f, b[r]);
+                    k[r] += (uint32_t)qa | ((uint32_t)qb << 16);
+                }
+            };
+            for (int t0 = 0; t0 < n_it; t0 += SEG) {
+                run(t0, min(t0 + SEG, n_it));
+                fold2(gxx[0], gxo[0], kxx);
+                fold2(gox[0], goo[0], kox);
+            }
+            auto whole = [](const f32x16v& a, const u32x16& k, int half) {
+                i32x16 v;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v[r] = (int)a[r] + (int)(((k[r] >> (16 * half)) & 0xffffu) << 16);
+                return v;
+            };
+            ixx[0] = whole(gxx[0], kxx, 0); ixo[0] = whole(gxo[0], kxx, 1);
+            iox[0] = whole(gox[0], kox, 0); ioo[0] = whole(goo[0], kox, 1);
+            }
+            if constexpr (TR && DIAG0) {  // as below, on the int32 Gram (tr reused as 32 x 33 ints)
+                int* tri = reinterpret_cast<int*>(tr);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) tri[((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + i] = ixo[0][r];
+                __syncthreads();
+#pragma unroll
+                for (int r = 0; r < 16; ++r) iox[0][r] = tri[i * 33 + (r & 3) + 8 * (r >> 2) + 4 * h];
+            }
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+                pair_epilogue<DOM, i32x16, true>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * c,
+                                                 DIAG0 && c == 0, i, h, ixx[c], ixo[c], iox[c], ioo[c], ixh[c], ioh[c],
+                                                 ihx[c], iho[c], ld_wind, n_org, rsq_thr, n_org);
+        }
     }
     }
+    if constexpr (SEG == 0) {
     if constexpr (TR && DIAG0) {  // m.x(a, b) = x.m(b, a): lane (i, h) register r holds (row si(r), column i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) tr[((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + i] = gxo[0][r];
@@ -1176,6 +1247,7 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         pair_epilogue<DOM, f32x16v, true>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * c,
                                           DIAG0 && c == 0, i, h, gxx[c], gxo[c], gox[c], goo[c], gxh[c], goh[c],
                                           ghx[c], gho[c], ld_wind, n_org, rsq_thr, n_org);
+    }
     __syncthreads();
     for (int s = lane; s < NS; s += 64) {
         const int g = sh.info[s].g;
@@ -1236,7 +1308,7 @@ __global__ void __launch_bounds__(256, 2) band_f4_grp_kernel(
 
 // WPS 2: single block-pair items; WPS 1: items of up to 2 column blocks (1 wave per SIMD, the
 // 2 x 128 accumulator registers in AGPRs).
-template <bool DOM, int WPS>
+template <bool DOM, int WPS, int SEG = 0>
 __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
                                                         const SnpConst* __restrict__ cst, const int4* __restrict__ items,
                                                         const double* __restrict__ pos, const int* __restrict__ Lw,
@@ -1248,11 +1320,12 @@ __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __rest
     __shared__ float tr[32 * 33];
     const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
 #define NLDSC_BODY(NC_, DIAG_)                                                                                        \
-    band_f4_body<DOM, NC_, DIAG_, 0, 0, true>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp,      \
-                                              ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, true, \
-                                              nullptr, tr)
+    band_f4_body<DOM, NC_, DIAG_, 0, 0, true, SEG>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, \
+                                                   ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc,  \
+                                                   true, nullptr, tr)
     const bool diag = it.y == it.x;
-    if (WPS == 1 && it.z == 2) { if (diag) NLDSC_BODY(2, true); else NLDSC_BODY(2, false); }
+    if constexpr (SEG > 0) { if (diag) NLDSC_BODY(1, true); else NLDSC_BODY(1, false); }
+    else if (WPS == 1 && it.z == 2) { if (diag) NLDSC_BODY(2, true); else NLDSC_BODY(2, false); }
     else { if (diag) NLDSC_BODY(1, true); else NLDSC_BODY(1, false); }
 #undef NLDSC_BODY
 }
@@ -1639,12 +1712,15 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st) {
     if (n_items <= 0) return hipSuccess;
-#define NLDSC_BAND(DOM_, WPS_)                                                                                      \
-    hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, cst,   \
-                       items, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, \
-                       ws_acc, xcd ? 1 : 0)
-    if (dom) { if (max_nc == 2) NLDSC_BAND(true, 1); else NLDSC_BAND(true, 2); }
-    else { if (max_nc == 2) NLDSC_BAND(false, 1); else NLDSC_BAND(false, 2); }
+    if (n_it > F4_SEG_CHUNKS && max_nc != 1) return hipErrorInvalidValue;  // segmented kernel: single blocks only
+#define NLDSC_BAND(DOM_, WPS_, SEG_)                                                                                \
+    hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, \
+                       cst, items, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc,     \
+                       l2d_acc, ws_acc, xcd ? 1 : 0)
+    // segmented kernel: the add+dom variant needs more than 256 registers (2 waves / SIMD would spill)
+    if (n_it > F4_SEG_CHUNKS) { if (dom) NLDSC_BAND(true, 1, F4_SEG_CHUNKS); else NLDSC_BAND(false, 2, F4_SEG_CHUNKS); }
+    else if (dom) { if (max_nc == 2) NLDSC_BAND(true, 1, 0); else NLDSC_BAND(true, 2, 0); }
+    else { if (max_nc == 2) NLDSC_BAND(false, 1, 0); else NLDSC_BAND(false, 2, 0); }
 #undef NLDSC_BAND
     return hipGetLastError();
 }

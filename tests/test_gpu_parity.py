@@ -233,6 +233,28 @@ def test_f4_gram_is_bitwise_the_int8_gram(engine):
         same_gram(a, b, f"N={N}")
 
 
+@pytest.mark.parametrize("N", [524_292, 1_100_003])
+def test_segmented_f4_gram_is_bitwise_the_int8_gram(engine, N):
+    """Rows longer than one fp32-exact segment (N > 2^19: 4 096 chunks of 128 samples) run the segmented
+    fp4 kernel, which folds its fp32 accumulators into int32 after every segment (ld_kernels.hip
+    band_f4_body, SEG > 0).  N = 524 292 has a final segment of 2 chunks; N = 1 100 003 > 2^20 (which used
+    to fall back to the int8 path) has three segments.  Same exactness check as above, against the int8
+    path, plus the diagonal transpose and missing-call products (1 % missing calls)."""
+    from nldsc_amd import synth
+    M = 600
+    buf, pos = synth.device_bed(M, N, seed=11, length_cm=3.0)
+    engine.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
+    for args in ((1.0, 1e-4, 1e-5, 1.0 / M, pos), (0.4, 0.01, 1e-5, 0.05, pos)):
+        a = engine.run(*args, flags=MODES["i8"])
+        b = engine.run(*args, flags=MODES["f4"])
+        assert engine.timings()["path"] == "f4"
+        assert (b["l2_ws"] > 10).all()
+        same_gram(a, b, f"N={N}")
+        c = engine.run(*args, flags=MODES["f4"] | _lib_flag("FLAG_ADDITIVE_ONLY"))
+        np.testing.assert_array_equal(c["l2_ws"], a["l2_ws"])
+        np.testing.assert_allclose(c["l2"], a["l2"], rtol=1e-13, atol=1e-14)
+
+
 def same_gram(a, b, label):
     for k in ("maf", "residuals_std", "l2_ws", "l2d_ws", "l2d_wse"):
         np.testing.assert_array_equal(a[k], b[k], err_msg=f"{label} {k}")
