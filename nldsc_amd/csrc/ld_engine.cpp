@@ -29,6 +29,8 @@ constexpr int BLK = 32;             // SNPs per MFMA block
 constexpr int CHUNK_BYTES = 32;     // one K-loop chunk of a 2-bit row (16 B per lane half)
 // resident row pitch: an even number of 32-byte chunks (the fp4 K loop takes two per iteration)
 constexpr int ROW_ALIGN_BYTES = 64;
+// item order of the single-block-pair schedule: tiles of TILE_R row blocks x TILE_C diagonal offsets
+constexpr int TILE_R = 16, TILE_C = 16;
 
 // resident layout of a .bed image: row j of ceil(N/4) bytes at j * row_bytes, n_rows = M rounded up to 32
 int row_pitch(int32_t n_org) {
@@ -121,11 +123,11 @@ struct nldsc_engine {
     DevBuf<nldsc::SnpConst> cst;
     DevBuf<uint8_t> sflags;
     DevBuf<double> pos, maf, rstd, l2_acc, l2d_acc, l2, l2d;
-    DevBuf<int4> items, items2;
+    DevBuf<int4> items;
     // host scratch
     std::vector<uint8_t> h_flags, h_all_pass;
     std::vector<int> h_L, h_R;
-    std::vector<int4> h_items;
+    std::vector<int4> h_items, h_scratch;
     HostPinned h_stage;  // pinned upload staging of the plan (L, R, items)
     HostPinned h_meta;   // GPU plan counters (items, diagonal items)
     HostPinned h_pos;    // pinned copy of the positions (the upload does not stall this thread)
@@ -137,31 +139,16 @@ struct nldsc_engine {
     double ms[6] = {0, 0, 0, 0, 0, 0};
     double flop_alg = 0, flop_issued = 0, pairs = 0, ops_alg_i8 = 0;
     int32_t n_band_items = 0;
-    // tuning knobs (environment, read at engine creation): band kernel waves/SIMD, max column blocks
-    int band_wps = 2, band_nc = 2;
     int last_path = 0;     // path of the last run: 0 fp32, 1 exact int8, 2 exact fp4
-    int band_i8_nc = 1;    // column blocks per int8-path item (NLDSC_BAND_I8_NC)
-    int band_f4_nc = 1;    // column blocks per fp4-path item (NLDSC_BAND_F4_NC)
     int band_mode = 2;     // default correlation path (NLDSC_BAND_MODE=f32|i8|f4): exact fp4
                            // (int8 from N = 2^27)
-    bool band_tile = false;  // exact path on skewed 2x2 tiles sharing decoded strips (NLDSC_BAND_TILE)
-    bool xcd = true;         // XCD-contiguous workgroup -> item order (NLDSC_XCD=0 disables)
-    int f4_grp = -1;         // fp4 path on 4-wave workgroups of skewed 2x2 tiles (NLDSC_BAND_F4_GRP = barrier
-                             // period in chunk pairs, 0: no barriers; -1: one wave per block pair)
-    int f4_ring = 0;         // fp4 strips through a per-wave LDS ring of this depth (NLDSC_BAND_F4_RING, 0: registers)
-    int tile_r = 16, tile_c = 16;  // item order: tiles of R row blocks x C diagonal offsets (NLDSC_TILE_R/C; R <= 1: row-major)
-    int band_round = 0;      // exact-path items per launch (NLDSC_BAND_ROUND; 0: one launch, -1: one
-                             // launch per round of resident waves)
     int n_cu = 256;
-    int diag_last = 0;  // NLDSC_DIAG_LAST: 1 = diagonal block pairs at the end of each XCD run; 2 = diagonal
-                        // items in a launch of their own before the off-diagonal ones (fp4, timing study)
-    std::vector<int4> h_ones;
 
     ~nldsc_engine() {
         (void)hipSetDevice(device);
         bed.release(); lastb.release(); flip.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
         ws3.release(); lut.release(); cst.release(); sflags.release(); pos.release(); maf.release(); rstd.release();
-        l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release(); items2.release();
+        l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         if (ev_plan) (void)hipEventDestroy(ev_plan);
         Ew.release(); plan_counts.release(); plan_meta.release(); plan_rows.release();
@@ -336,29 +323,6 @@ void order_items_tiled(std::vector<int4>& items, int nblk, int R, int C, std::ve
     items.swap(scratch);
 }
 
-// Skewed 2x2 tiles of the exact path (band_tile_kernel) from the single-block-pair items: pair
-// (a, b), a <= b, goes to tile I = a & ~1, J = I + 2 * ((b - a) >> 1), wave 2 (a - I) + ((b - a) & 1)
-// (waves: (I, J), (I, J+1), (I+1, J+1), (I+1, J+2)).  Each pair lands in exactly one tile slot.
-void plan_tiles(const std::vector<int4>& ones, int nblk, std::vector<int4>& out) {
-    std::vector<std::pair<int64_t, int>> key;
-    key.reserve(ones.size());
-    for (const int4& it : ones) {
-        const int a = it.x, b = it.y;
-        const int I = a & ~1, d = b - a;
-        key.emplace_back((int64_t)I * (nblk + 1) + (d >> 1), 1 << (2 * (a - I) + (d & 1)));
-    }
-    std::sort(key.begin(), key.end());
-    out.clear();
-    for (size_t k = 0; k < key.size();) {
-        int mask = 0;
-        size_t e = k;
-        for (; e < key.size() && key[e].first == key[k].first; ++e) mask |= key[e].second;
-        const int I = (int)(key[k].first / (nblk + 1)), t = (int)(key[k].first % (nblk + 1));
-        out.push_back(make_int4(I, I + 2 * t, mask, 0));
-        k = e;
-    }
-}
-
 // device buffers of a resident image of n_snp rows (all rows, pitch padding, saved last bytes)
 hipError_t alloc_image(nldsc_engine* e, int32_t n_snp, int32_t n_org) {
     e->n_snp = e->n_org = 0;  // no valid image until finish_image
@@ -405,22 +369,10 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     nldsc_engine* e = new (std::nothrow) nldsc_engine();
     if (!e) return set_err(err, errlen, NLDSC_E_OOM, "out of host memory");
     e->device = d;
-    if (const char* v = std::getenv("NLDSC_BAND_WPS")) e->band_wps = std::atoi(v) == 1 ? 1 : 2;
-    if (const char* v = std::getenv("NLDSC_BAND_NC")) e->band_nc = std::atoi(v) == 1 ? 1 : 2;
-    if (const char* v = std::getenv("NLDSC_BAND_I8_NC")) e->band_i8_nc = std::atoi(v) == 2 ? 2 : 1;
-    if (const char* v = std::getenv("NLDSC_BAND_F4_NC")) e->band_f4_nc = std::atoi(v) == 2 ? 2 : 1;
     if (const char* v = std::getenv("NLDSC_BAND_MODE"))
-        e->band_mode = std::strcmp(v, "f32") == 0 ? 0 : std::strcmp(v, "f4") == 0 ? 2 : 1;
-    if (const char* v = std::getenv("NLDSC_BAND_TILE")) e->band_tile = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_XCD")) e->xcd = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_BAND_ROUND")) e->band_round = std::atoi(v);
+        e->band_mode = std::strcmp(v, "f32") == 0 ? 0 : std::strcmp(v, "i8") == 0 ? 1 : 2;
     if (const char* v = std::getenv("NLDSC_GPU_PLAN")) e->gpu_plan = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_ORIENT")) e->orient = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_TILE_R")) e->tile_r = std::atoi(v);
-    if (const char* v = std::getenv("NLDSC_TILE_C")) e->tile_c = std::max(1, std::atoi(v));
-    if (const char* v = std::getenv("NLDSC_BAND_F4_GRP")) e->f4_grp = std::atoi(v);
-    if (const char* v = std::getenv("NLDSC_BAND_F4_RING")) e->f4_ring = std::atoi(v);
-    if (const char* v = std::getenv("NLDSC_DIAG_LAST")) e->diag_last = std::atoi(v);
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
@@ -588,10 +540,8 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     if (path == 2 && N >= (1 << 27)) path = 1;
     const bool use_i8 = path != 0, use_f4 = path == 2;
     // rows longer than one fp32-exact segment: the segmented kernel (single blocks, register strips)
-    const bool f4_seg = use_f4 && row_pitch(N) / CHUNK_BYTES > nldsc::F4_SEG_CHUNKS;
-    const bool f4_grp = use_f4 && !f4_seg && e->f4_grp >= 0;
-    const bool tiled = (path == 1 && e->band_tile) || f4_grp;
-    const int max_nc = tiled || f4_seg ? 1 : use_f4 ? e->band_f4_nc : use_i8 ? e->band_i8_nc : e->band_nc;
+    // fp32 items pair a row block with up to 2 column blocks (2 waves / SIMD); the exact paths take one
+    const int max_nc = use_i8 ? 1 : 2;
     HIPCHK(hipSetDevice(e->device));
     hipStream_t st = e->stream;
 
@@ -628,7 +578,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     // band schedule: on the GPU when every position is >= 0 and sorted (the kernels run ahead of the
     // count and the host only waits for two counters), else the host replay of the reference's pointers
     const bool sorted = positions_sorted(p->positions, M);
-    const bool gpu_plan = e->gpu_plan && sorted && max_nc == 1 && !tiled &&
+    const bool gpu_plan = e->gpu_plan && sorted && max_nc == 1 &&
                           std::all_of(p->positions, p->positions + M, [](double x) { return x >= 0.0; });
     if (gpu_plan) {
         const size_t n_t = (size_t)(nblk + 15) / 16;
@@ -706,15 +656,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         if (it.x < 0 || it.y < it.x || (it.z != 1 && it.z != 2) || it.y + it.z > nblk)
             return set_err(err, errlen, NLDSC_E_ARG, "internal: bad work item (%d, %d, %d) for %d blocks", it.x,
                            it.y, it.z, nblk);
-    if (max_nc == 1 && !tiled) order_items_tiled(e->h_items, nblk, e->tile_r, e->tile_c, e->h_ones);
-    if (tiled) {
-        e->h_ones.swap(e->h_items);
-        plan_tiles(e->h_ones, nblk, e->h_items);
-        for (const int4& it : e->h_items)  // the tile kernel clamps strips past the last block itself
-            if (it.x < 0 || it.x >= nblk || it.y < it.x || it.y >= nblk || it.z <= 0 || it.z > 15)
-                return set_err(err, errlen, NLDSC_E_ARG, "internal: bad tile (%d, %d, %d) for %d blocks", it.x, it.y,
-                               it.z, nblk);
-    }
+    if (max_nc == 1) order_items_tiled(e->h_items, nblk, TILE_R, TILE_C, e->h_scratch);
     HIPCHK(e->items.ensure(std::max<size_t>(e->h_items.size(), 1)));
     // the plan goes up through pinned staging: a copy from pageable memory would block this thread
     // until the stream drains (the count kernel), pinned copies are queued and return at once
@@ -733,15 +675,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     HIPCHK(hipMemcpyAsync(e->Rw.p, e->h_stage.p + bL, bL, hipMemcpyHostToDevice, st));
     if (bI) HIPCHK(hipMemcpyAsync(e->items.p, e->h_stage.p + 2 * bL, bI, hipMemcpyHostToDevice, st));
     n_items = (int)e->h_items.size();
-    for (const int4& it : tiled ? e->h_ones : e->h_items) n_diag += it.x == it.y;
-    }
-    // single-block-pair items in one launch (exact paths): the diagonal items end every XCD run
-    if (e->diag_last && use_i8 && max_nc == 1 && !tiled && (!use_f4 || (e->band_round == 0 && e->f4_ring == 0)) &&
-        n_items > 0) {
-        HIPCHK(e->items2.ensure((size_t)n_items));
-        HIPCHK(nldsc::launch_diag_last(e->items.p, e->items2.p, n_items,
-                                         e->diag_last == 2 ? 1 : e->xcd ? 8 : 1, st));
-        std::swap(e->items, e->items2);
+    for (const int4& it : e->h_items) n_diag += it.x == it.y;
     }
     HIPCHK(hipMemsetAsync(e->l2_acc.p, 0, sizeof(double) * M, st));
     HIPCHK(hipMemsetAsync(e->l2d_acc.p, 0, sizeof(double) * M, st));
@@ -755,65 +689,25 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         // off the diagonal) per block pair; fp32 AA (+ AR, and RA off the diagonal)
         double blocks = 0;
         if (gpu_plan) blocks = n_items;
-        else for (const int4& it : tiled ? e->h_ones : e->h_items) blocks += it.z;
-        // (the default fp4 kernel also skips m.x on diagonal blocks: the transpose of x.m)
-        const bool f4_diag_tr = use_f4 && !tiled && !(e->f4_ring > 0 && max_nc == 1 && !f4_seg);
+        else for (const int4& it : e->h_items) blocks += it.z;
+        // (the fp4 kernel also skips m.x on diagonal blocks: the transpose of x.m)
         const double products = use_i8 ? blocks * (dom ? 8.0 : 4.0) - (dom ? 2.0 * n_diag : 0.0)
-                                         - (f4_diag_tr ? 1.0 * n_diag : 0.0)
+                                         - (use_f4 ? 1.0 * n_diag : 0.0)
                                        : blocks * (dom ? 3.0 : 1.0) - (dom ? 1.0 * n_diag : 0.0);
         e->flop_issued = products * 2.0 * BLK * BLK * (double)row_bytes * 4.0;
     }
     if (n_items > 0) {
-        if (f4_grp) {
-            const int n_tiles = n_items;
-            const int per = e->band_round < 0 ? e->n_cu * 2 : e->band_round > 0 ? e->band_round : n_tiles;
-            for (int off = 0; off < n_tiles; off += per)
-                HIPCHK(nldsc::launch_band_f4_grp(dom, e->f4_grp, std::min(per, n_tiles - off), geno, pitch_words,
-                                                 n_it, nblk, e->cst.p, e->items.p + off, e->pos.p, e->Lw.p, e->Rw.p,
-                                                 e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end,
-                                                 e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, e->xcd, st));
-        } else if (tiled)
-            HIPCHK(nldsc::launch_band_tile(dom, n_items, geno, pitch_words, n_it, nblk, e->cst.p,
-                                           e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
-                                           (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
-                                           e->ws_acc.p, e->xcd, st));
-        else if (use_f4) {
-            // Items of one launch start together and stream through the samples in near lockstep, so
-            // the strips they share stay in their XCD's L2; a round = the waves resident at once.
-            const int per = e->band_round < 0 ? e->n_cu * 4 * (max_nc == 2 ? 1 : 2)
-                          : e->band_round > 0 ? e->band_round : n_items;
-            const bool split = e->diag_last == 2 && max_nc == 1 && per == n_items && e->f4_ring == 0 && n_diag > 0;
-            if (split) {  // the diagonal items (the partition's tail) first, in a launch of their own
-                HIPCHK(nldsc::launch_band_f4(dom, 1, n_diag, geno, pitch_words, n_it, e->cst.p,
-                                             e->items.p + (n_items - n_diag), e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p,
-                                             M, p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p,
-                                             e->l2d_acc.p, e->ws_acc.p, e->xcd, st));
-                HIPCHK(nldsc::launch_band_f4(dom, 1, n_items - n_diag, geno, pitch_words, n_it, e->cst.p,
-                                             e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
-                                             (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
-                                             e->ws_acc.p, e->xcd, st));
-            }
-            for (int off = 0; off < n_items && !split; off += per)
-                if (e->f4_ring > 0 && max_nc == 1 && !f4_seg)
-                    HIPCHK(nldsc::launch_band_f4_ring(dom, e->f4_ring, std::min(per, n_items - off), geno,
-                                                      pitch_words, n_it, e->cst.p, e->items.p + off, e->pos.p, e->Lw.p,
-                                                      e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr,
-                                                      own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p,
-                                                      e->xcd, st));
-                else
-                HIPCHK(nldsc::launch_band_f4(dom, max_nc, std::min(per, n_items - off),
-                                             geno, pitch_words, n_it,
-                                             e->cst.p, e->items.p + off, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
-                                             p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p,
-                                             e->l2d_acc.p, e->ws_acc.p, e->xcd, st));
-        }
+        if (use_f4)
+            HIPCHK(nldsc::launch_band_f4(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p,
+                                         e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr,
+                                         own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true, st));
         else if (use_i8)
             HIPCHK(nldsc::launch_band_i8(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p,
                                          e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
                                          (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
-                                         e->ws_acc.p, e->xcd, st));
+                                         e->ws_acc.p, true, st));
         else
-            HIPCHK(nldsc::launch_band(dom, e->band_wps, n_items, geno, pitch_words, n_it,
+            HIPCHK(nldsc::launch_band(dom, 2, n_items, geno, pitch_words, n_it,
                                       e->lut.p, e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
                                       (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                       e->ws_acc.p, st));
@@ -880,16 +774,11 @@ int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, d
 int nldsc_plan_band(const double* positions, const uint8_t* flags, int32_t n_snp, double ld_wind, int32_t own_begin,
                     int32_t own_end, int32_t max_nc, int32_t* L, int32_t* R, int32_t* items, int32_t cap) {
     if (!positions || !flags || !L || !R || n_snp <= 0 || own_begin < 0 || own_end > n_snp || own_begin > own_end ||
-        (max_nc != 1 && max_nc != 2 && max_nc != 4))
+        (max_nc != 1 && max_nc != 2))
         return NLDSC_E_ARG;
     replay_windows(positions, flags, n_snp, ld_wind, L, R);
     std::vector<int4> it;
-    plan_items(positions, flags, n_snp, ld_wind, L, R, own_begin, own_end, max_nc == 4 ? 1 : max_nc, it);
-    if (max_nc == 4) {
-        std::vector<int4> ones;
-        ones.swap(it);
-        plan_tiles(ones, (n_snp + BLK - 1) / BLK, it);
-    }
+    plan_items(positions, flags, n_snp, ld_wind, L, R, own_begin, own_end, max_nc, it);
     if ((int64_t)it.size() > (int64_t)cap || !items) return (int)std::min<size_t>(it.size(), INT32_MAX);
     for (size_t k = 0; k < it.size(); ++k) {
         items[4 * k] = it[k].x; items[4 * k + 1] = it[k].y; items[4 * k + 2] = it[k].z; items[4 * k + 3] = 0;

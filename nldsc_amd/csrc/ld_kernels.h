@@ -38,9 +38,6 @@ hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const doubl
 hipError_t launch_plan(const double* pos, int n, double w, int own_lo, int own_hi, int* A, int* E, int* R,
                        int2* rows, int* counts, int* meta, hipStream_t st);
 hipError_t launch_plan_emit(int n, const int2* rows, const int* meta, const int* offsets, int4* items, hipStream_t st);
-// stable partition of each of `runs` contiguous runs of the item list (xcd_slot's XCD runs): off-diagonal
-// items first, diagonal ones last, written to `out`
-hipError_t launch_diag_last(const int4* in, int4* out, int n, int runs, hipStream_t st);
 hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                        const float2* lut, const int4* items, const double* pos, const int* Lw, const int* Rw,
                        const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
@@ -58,24 +55,6 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st);
-// fp4 exact path, one wave per block pair, strips through a `ring`-deep (3..5) per-wave LDS ring (LDS-DMA)
-hipError_t launch_band_f4_ring(bool dom, int ring, int n_items, const uint32_t* geno, int pitch_words, int n_it,
-                               const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
-                               const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr,
-                               int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd,
-                               hipStream_t st);
-// fp4 exact path on skewed 2x2 tiles (I, J, mask): one wave per block pair, four per workgroup sharing
-// strips through the CU's caches; `sync` = chunk pairs between workgroup barriers (0: none)
-hipError_t launch_band_f4_grp(bool dom, int sync, int n_tiles, const uint32_t* geno, int pitch_words, int n_it,
-                              int nblk, const SnpConst* cst, const int4* tiles, const double* pos, const int* Lw,
-                              const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind, double n_org,
-                              double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc,
-                              bool xcd, hipStream_t st);
-// skewed 2x2 tiles (I, J, mask) of the exact path, one 256-thread workgroup each
-hipError_t launch_band_tile(bool dom, int n_tiles, const uint32_t* geno, int pitch_words, int n_it, int nblk,
-                            const SnpConst* cst, const int4* tiles, const double* pos, const int* Lw, const int* Rw,
-                            const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
-                            int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st);
 hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2d_acc, const int* ws_acc, int n_snp,
                            int own_lo, int own_hi, bool dom, double* l2, double* l2d, int* ws3, hipStream_t st);
 hipError_t launch_synth_bed(uint8_t* rows, int n_snp, int n_org, int nb, const float* thr, float rho, float missing,

@@ -887,10 +887,9 @@ __global__ void __launch_bounds__(64, WPS) band_i8_kernel(const uint32_t* __rest
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 constexpr int E8M0_ONE = 127;  // block scale 2^0
-#ifndef NLDSC_F4_VPM
-#define NLDSC_F4_VPM 4  // VALU instructions interleaved after each MFMA of a one-column-block item (3, 5, 6
-                        // and alternating 4/5 measured slower: profiles/r01_ab_vpm.json)
-#endif
+// VALU instructions interleaved after each MFMA of a full 8-product K step (3, 5, 6 and alternating 4/5
+// measured slower in round 1)
+constexpr int F4_VPM = 4;
 
 struct F4Frag {
     i32x4 x, h, o;
@@ -913,13 +912,6 @@ __device__ __forceinline__ void decode_f4_word(uint32_t w, int& x0, int& x1, int
 }
 
 __device__ __forceinline__ F4Frag decode_f4(uint32_t wa, uint32_t wb) {
-#ifdef NLDSC_F4_DIAG_NODECODE  // diagnostic build: raw words as operands (timing only)
-    F4Frag g;
-    g.x = i32x4{(int)wa, (int)wb, (int)(wa ^ wb), (int)wa};
-    g.h = i32x4{(int)wb, (int)wa, (int)wa, (int)wb};
-    g.o = i32x4{(int)(wa | wb), (int)wb, (int)wa, (int)(wa & wb)};
-    return g;
-#endif
     int x0, x1, x2, x3, h0, h1, h2, h3, o0, o1, o2, o3;
     decode_f4_word(wa, x0, x1, h0, h1, o0, o1);
     decode_f4_word(wb, x2, x3, h2, h3, o2, o3);
@@ -930,59 +922,26 @@ __device__ __forceinline__ F4Frag decode_f4(uint32_t wa, uint32_t wb) {
     return f;
 }
 
-#ifndef NLDSC_F4_PERM
-#define NLDSC_F4_PERM 1426357  // 01426357: xx, xo, xh, ox, hx, oo, oh, ho (band_f4_body)
-#endif
-
 __device__ __forceinline__ f32x16v mfma_f4(const i32x4& a, const i32x4& b, const f32x16v& c) {
     const i32x8 A = {a[0], a[1], a[2], a[3], 0, 0, 0, 0}, B = {b[0], b[1], b[2], b[3], 0, 0, 0, 0};
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, c, 4, 4, 0, E8M0_ONE, 0, E8M0_ONE);
 }
 
-// ---- per-wave LDS ring of raw 2-bit chunks filled by LDS-DMA (global_load_lds_dwordx4) ----
-// hipcc waits vmcnt(0) before every ds_read that may alias a pending LDS-DMA, which would drain the
-// ring, so the DMA and the ring reads are inline asm with their own counted waits
-// (cdna_hip_programming.md §5.7): the wave's only vector-memory ops in the K loop are its DMAs.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) void* lds_void_ptr;
-
-__device__ __forceinline__ uint32_t lds_addr(void* p) { return (uint32_t)(uintptr_t)(lds_void_ptr)p; }
-
-// 64 lanes x 16 B from per-lane global addresses into LDS [dst, dst + 1 KiB), lane-linear
-__device__ __forceinline__ void dma16(const void* src, uint32_t dst) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
-}
-
-// wait until at most VM DMAs are in flight, then read this lane's 16 B of the row and column chunk
-template <int VM>
-__device__ __forceinline__ void ring_read(uint32_t row_addr, uint32_t col_addr, u32x4& wr, u32x4& wc) {
-    asm volatile("s_waitcnt vmcnt(%4)\n\tds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&v"(wr), "=&v"(wc) : "v"(row_addr), "v"(col_addr), "i"(VM) : "memory");
-}
-
 // NC column blocks J0 .. J0+NC-1 share the row strip's decode; DIAG0: block 0 is the diagonal.
-// RING > 0 (NC == 1 only): the strips' chunks stream through a RING-deep per-wave LDS ring by LDS-DMA
-// instead of registers, RING chunk pairs ahead of their decode.
-// SYNC > 0 (workgroups of several waves, band_f4_grp_kernel): a workgroup barrier every SYNC
-// chunk pairs keeps the waves that share strips at the same samples, so the strips they share are
-// served from the CU's L1 / the XCD's L2; an inactive wave (!active) only keeps the barrier count.
-// tr (32 x 33 floats of LDS, or nullptr): on a diagonal block, m.x is the transpose of x.m, so its MFMAs
-// are skipped and the epilogue reads x.m transposed through tr.
-// SEG > 0 (NC == 1, no ring / sync; rows longer than SEG chunks, N > 2^19): the K loop runs in segments of
-// SEG chunks (128 samples each, so a segment adds at most 16 * 128 * SEG <= 2^23 to an entry and the fp32
-// accumulators stay exact integers); after each segment the multiples of 2^16 are moved out into packed
-// 16-bit counters, and the epilogue sees int32 entries, exact while every entry is <= 16N < 2^31.
-template <bool DOM, int NC, bool DIAG0, int SYNC = 0, int RING = 0, bool TR = false, int SEG = 0>
+// tr (32 x 33 floats of LDS): on a diagonal block, m.x is the transpose of x.m, so its MFMAs are skipped and
+// the epilogue reads x.m transposed through tr.
+// SEG > 0 (NC == 1; rows longer than SEG chunks, N > 2^19): the K loop runs in segments of SEG chunks (128
+// samples each, so a segment adds at most 16 * 128 * SEG <= 2^23 to an entry and the fp32 accumulators stay
+// exact integers); after each segment the fp32 Gram is folded into int32 entries (add+dom) or its multiples
+// of 2^16 move to packed 16-bit counters (additive-only), exact while every entry is <= 16N < 2^31.
+template <bool DOM, int NC, bool DIAG0, int SEG = 0>
 __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const uint32_t* __restrict__ geno,
                                              int pitch_words, int n_it, const SnpConst* __restrict__ cst,
                                              const double* __restrict__ pos, const int* __restrict__ Lw,
                                              const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
                                              int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                                              int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
-                                             int* __restrict__ ws_acc, bool active = true,
-                                             uint4* ring = nullptr, float* tr = nullptr) {
+                                             int* __restrict__ ws_acc, float* tr) {
     constexpr int NS = 32 * (1 + NC);
     const int lane = threadIdx.x & 63;
     const int i = lane & 31, h = lane >> 5;
@@ -1002,75 +961,42 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         sh.wsa[s] = 0; sh.wsd[s] = 0; sh.wse[s] = 0;
     }
     __syncthreads();
-    if (!active) {
-        if (SYNC > 0)
-            for (int t = 0; t < n_it; t += 2)
-                if ((t >> 1) % (SYNC > 0 ? SYNC : 1) == 0) __builtin_amdgcn_s_barrier();
-        __syncthreads();
-        return;
-    }
 
     f32x16v gxx[NC], gxo[NC], gox[NC], goo[NC], gxh[NC], goh[NC], ghx[NC], gho[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) gxx[c] = gxo[c] = gox[c] = goo[c] = gxh[c] = goh[c] = ghx[c] = gho[c] = f32x16v{};
-#ifdef NLDSC_F4_DIAG_SAMEROWS  // diagnostic build: every item streams the same two strips (L2-resident)
-    const uint4* rowp = reinterpret_cast<const uint4*>(geno + (size_t)(i) * (size_t)pitch_words) + h;
-    const uint4* colp[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-        colp[c] = reinterpret_cast<const uint4*>(geno + (size_t)((1 + c) * 32 + i) * (size_t)pitch_words) + h;
-#else
     const uint4* rowp = reinterpret_cast<const uint4*>(geno + (size_t)(I * 32 + i) * (size_t)pitch_words) + h;
     const uint4* colp[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c)
         colp[c] = reinterpret_cast<const uint4*>(geno + (size_t)((J0 + c) * 32 + i) * (size_t)pitch_words) + h;
-#endif
-    // n_it is even (rows are padded to 64 bytes).  Two chunk buffers: P holds even chunks, Q odd
-    // ones; each is reloaded right after its last word is decoded and read again two K steps
-    // later, with no register copies of loads in flight (those would force vmcnt(0)).
-    const int last = n_it - 1;
     // RM / CM: the row / column block holds missing calls.  A block without any has an all-zero m plane,
     // so the products with it are skipped (imputed hard calls: 3 of the 8 MFMAs remain).
     auto mfmas_v = [&](const F4Frag& a, const F4Frag (&b)[NC], auto RMc, auto CMc) {
         constexpr bool RM = decltype(RMc)::value, CM = decltype(CMc)::value;
-#ifdef NLDSC_F4_PRIO  // study build: raised wave priority over each MFMA group
-        __builtin_amdgcn_s_setprio(NLDSC_F4_PRIO);
-#endif
-        // Issue order of the 8 products = the digits of NLDSC_F4_PERM (0 xx, 1 xo, 2 ox, 3 oo, 4 xh, 5 oh,
-        // 6 hx, 7 ho).  The order alone moves the band kernel by up to 12 % (decode interleave, register
-        // assignment); the default xx, xo, xh, ox, hx, oo, oh, ho measured best of 18 orders, -1.2 % vs
-        // 0..7 (profiles/r01_ab_perm*.json).  On a diagonal block m.x and h.x are the transposes of x.m
-        // and x.h (skipped).
+        // Issue order xx, xo, xh, ox, hx, oo, oh, ho: the order alone moves the band kernel by up to 12 %
+        // (decode interleave, register assignment); this one measured best of 18 orders in round 1.  On a
+        // diagonal block m.x and h.x are the transposes of x.m and x.h (skipped).
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                constexpr long long perm = NLDSC_F4_PERM;
-                long long d = perm;
-                for (int u = 0; u < 7 - q; ++u) d /= 10;
-                switch ((int)(d % 10)) {
-                    case 0: gxx[c] = mfma_f4(a.x, b[c].x, gxx[c]); break;
-                    case 1: if (CM) gxo[c] = mfma_f4(a.x, b[c].o, gxo[c]); break;
-                    case 2: if (RM && !(TR && DIAG0 && c == 0)) gox[c] = mfma_f4(a.o, b[c].x, gox[c]); break;
-                    case 3: if (RM && CM) goo[c] = mfma_f4(a.o, b[c].o, goo[c]); break;
-                    case 4: if (DOM) gxh[c] = mfma_f4(a.x, b[c].h, gxh[c]); break;
-                    case 5: if (DOM && RM) goh[c] = mfma_f4(a.o, b[c].h, goh[c]); break;
-                    case 6: if (DOM && !(DIAG0 && c == 0)) ghx[c] = mfma_f4(a.h, b[c].x, ghx[c]); break;
-                    default: if (DOM && CM && !(DIAG0 && c == 0)) gho[c] = mfma_f4(a.h, b[c].o, gho[c]); break;
-                }
-            }
+            gxx[c] = mfma_f4(a.x, b[c].x, gxx[c]);
+            if (CM) gxo[c] = mfma_f4(a.x, b[c].o, gxo[c]);
+            if (DOM) gxh[c] = mfma_f4(a.x, b[c].h, gxh[c]);
+            if (RM && !(DIAG0 && c == 0)) gox[c] = mfma_f4(a.o, b[c].x, gox[c]);
+            if (DOM && !(DIAG0 && c == 0)) ghx[c] = mfma_f4(a.h, b[c].x, ghx[c]);
+            if (RM && CM) goo[c] = mfma_f4(a.o, b[c].o, goo[c]);
+            if (DOM && RM) goh[c] = mfma_f4(a.o, b[c].h, goh[c]);
+            if (DOM && CM && !(DIAG0 && c == 0)) gho[c] = mfma_f4(a.h, b[c].o, gho[c]);
         }
-        // full 8-product steps: VPM VALU after each MFMA; otherwise (additive-only items, missing-free
-        // blocks) the decode is spread evenly over the MFMAs there are (additive-only C2: -6.6 % band time,
-        // profiles/r01_ab_addspread.json)
+        // full 8-product steps: F4_VPM VALU after each MFMA; otherwise (additive-only items, missing-free
+        // blocks) the decode is spread evenly over the MFMAs there are (additive-only C2: -6.6 % band time)
         if constexpr (RM && CM && DOM) {
 #pragma unroll
             for (int m = 0; m < 8 * NC; ++m) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, NC == 1 ? NLDSC_F4_VPM : 4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, NC == 1 ? F4_VPM : 4, 0);
             }
-        } else {  // fewer MFMAs for the same decode: spread the VALU evenly over them
+        } else {
             constexpr int n_mfma = NC * (1 + CM + RM + (RM && CM) + (DOM ? 2 + RM + CM : 0));
             constexpr int n_valu = NC * (RM ? 9 : 7) * 2 + NC * (CM ? 9 : 7) * 2;
 #pragma unroll
@@ -1079,115 +1005,83 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
                 __builtin_amdgcn_sched_group_barrier(0x002, (n_valu + n_mfma - 1) / n_mfma, 0);
             }
         }
-#ifdef NLDSC_F4_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
     };
-    auto mfmas = [&](const F4Frag& a, const F4Frag (&b)[NC]) {
-        mfmas_v(a, b, std::true_type{}, std::true_type{});
-    };
-    if constexpr (RING > 0 && NC == 1) {
-        // ring slot k: row chunk at [k][0][lane], column chunk at [k][1][lane] (uint4 ring[RING][2][64])
-        const uint32_t rb = lds_addr(ring), lane_off = (uint32_t)lane * 16u;
-        for (int k = 0; k < RING; ++k) {
-            dma16(rowp + 2 * min(k, last), rb + (uint32_t)k * 2048u);
-            dma16(colp[0] + 2 * min(k, last), rb + (uint32_t)k * 2048u + 1024u);
-        }
-        u32x4 wr, wc;
-        ring_read<2 * (RING - 1)>(rb + lane_off, rb + 1024u + lane_off, wr, wc);
-        dma16(rowp + 2 * min(RING, last), rb);
-        dma16(colp[0] + 2 * min(RING, last), rb + 1024u);
-        F4Frag a0 = decode_f4(wr.x, wr.y), a1, b0[1], b1[1];
-        b0[0] = decode_f4(wc.x, wc.y);
-        int slot = 1 % RING;
-        for (int t = 0; t < n_it; ++t) {  // chunk t is in (wr, wc)
-            a1 = decode_f4(wr.z, wr.w);
-            b1[0] = decode_f4(wc.z, wc.w);
-            mfmas(a0, b0);  // K step 2t
-            const uint32_t sa = rb + (uint32_t)slot * 2048u;
-            ring_read<2 * (RING - 1)>(sa + lane_off, sa + 1024u + lane_off, wr, wc);  // chunk t+1
-            dma16(rowp + 2 * min(t + 1 + RING, last), sa);
-            dma16(colp[0] + 2 * min(t + 1 + RING, last), sa + 1024u);
-            slot = slot + 1 == RING ? 0 : slot + 1;
-            a0 = decode_f4(wr.x, wr.y);
-            b0[0] = decode_f4(wc.x, wc.y);
-            mfmas(a1, b1);  // K step 2t+1
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
-    } else {
-    // chunks [t_lo, t_hi), t_lo and t_hi even (the default kernel: 0 and n_it)
+    // chunks [t_lo, t_hi), t_lo and t_hi even (rows are padded to 64 bytes).  Two chunk buffers: P holds
+    // even chunks, Q odd ones; each is reloaded right after its last word is decoded and read again two K
+    // steps later, with no register copies of loads in flight (those would force vmcnt(0)).
     auto kloop = [&](auto RMc, auto CMc, const int t_lo, const int t_hi) {
-    const int last = t_hi - 1;
-    uint4 pr = rowp[2 * t_lo], qr = rowp[2 * t_lo + 2], pc[NC], qc[NC];
+        const int last = t_hi - 1;
+        uint4 pr = rowp[2 * t_lo], qr = rowp[2 * t_lo + 2], pc[NC], qc[NC];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) { pc[c] = colp[c][2 * t_lo]; qc[c] = colp[c][2 * t_lo + 2]; }
-    // two named fragment sets: set 1 is decoded while set 0 feeds the MFMAs and vice versa, so no
-    // fragment is copied (a single rotating set costs ~12 v_mov per K step)
-    F4Frag a0 = decode_f4(pr.x, pr.y), a1, b0[NC], b1[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) b0[c] = decode_f4(pc[c].x, pc[c].y);
-    for (int t = t_lo; t < t_hi; t += 2) {
-        if (SYNC > 0 && (t >> 1) % (SYNC > 0 ? SYNC : 1) == 0) __builtin_amdgcn_s_barrier();
-        a1 = decode_f4(pr.z, pr.w);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) b1[c] = decode_f4(pc[c].z, pc[c].w);
-        mfmas_v(a0, b0, RMc, CMc);  // K step 2t   (chunk t, words 0-1)
-        pr = rowp[2 * min(t + 2, last)];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) pc[c] = colp[c][2 * min(t + 2, last)];
-#ifdef NLDSC_F4_LDPIN  // study build: keep the prefetch loads where they are issued (no sinking)
-        __builtin_amdgcn_sched_barrier(0);
-#endif
-        a0 = decode_f4(qr.x, qr.y);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) b0[c] = decode_f4(qc[c].x, qc[c].y);
-        mfmas_v(a1, b1, RMc, CMc);  // K step 2t+1 (chunk t, words 2-3)
-        a1 = decode_f4(qr.z, qr.w);
-#pragma unroll
-        for (int c = 0; c < NC; ++c) b1[c] = decode_f4(qc[c].z, qc[c].w);
-        mfmas_v(a0, b0, RMc, CMc);  // K step 2t+2 (chunk t+1, words 0-1)
-        qr = rowp[2 * min(t + 3, last)];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) qc[c] = colp[c][2 * min(t + 3, last)];
-#ifdef NLDSC_F4_LDPIN
-        __builtin_amdgcn_sched_barrier(0);
-#endif
-        a0 = decode_f4(pr.x, pr.y);
+        for (int c = 0; c < NC; ++c) { pc[c] = colp[c][2 * t_lo]; qc[c] = colp[c][2 * t_lo + 2]; }
+        // two named fragment sets: set 1 is decoded while set 0 feeds the MFMAs and vice versa, so no
+        // fragment is copied (a single rotating set costs ~12 v_mov per K step)
+        F4Frag a0 = decode_f4(pr.x, pr.y), a1, b0[NC], b1[NC];
 #pragma unroll
         for (int c = 0; c < NC; ++c) b0[c] = decode_f4(pc[c].x, pc[c].y);
-        mfmas_v(a1, b1, RMc, CMc);  // K step 2t+3 (chunk t+1, words 2-3)
-    }
+        for (int t = t_lo; t < t_hi; t += 2) {
+            a1 = decode_f4(pr.z, pr.w);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) b1[c] = decode_f4(pc[c].z, pc[c].w);
+            mfmas_v(a0, b0, RMc, CMc);  // K step 2t   (chunk t, words 0-1)
+            pr = rowp[2 * min(t + 2, last)];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) pc[c] = colp[c][2 * min(t + 2, last)];
+            a0 = decode_f4(qr.x, qr.y);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) b0[c] = decode_f4(qc[c].x, qc[c].y);
+            mfmas_v(a1, b1, RMc, CMc);  // K step 2t+1 (chunk t, words 2-3)
+            a1 = decode_f4(qr.z, qr.w);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) b1[c] = decode_f4(qc[c].z, qc[c].w);
+            mfmas_v(a0, b0, RMc, CMc);  // K step 2t+2 (chunk t+1, words 0-1)
+            qr = rowp[2 * min(t + 3, last)];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) qc[c] = colp[c][2 * min(t + 3, last)];
+            a0 = decode_f4(pr.x, pr.y);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) b0[c] = decode_f4(pc[c].x, pc[c].y);
+            mfmas_v(a1, b1, RMc, CMc);  // K step 2t+3 (chunk t+1, words 2-3)
+        }
     };
-    if constexpr (SYNC > 0) {
-        kloop(std::true_type{}, std::true_type{}, 0, n_it);
+    // wave-uniform: does the row block / do the column blocks hold a missing call (flag bit 2)?
+    const bool rm = __any(lane < 32 && (sh.info[lane].fl & 4));
+    const bool cm = __any(32 + lane < NS && (sh.info[32 + lane].fl & 4));
+    auto run = [&](const int t_lo, const int t_hi) {
+        if (rm && cm) kloop(std::true_type{}, std::true_type{}, t_lo, t_hi);
+        else if (rm) kloop(std::true_type{}, std::false_type{}, t_lo, t_hi);
+        else if (cm) kloop(std::false_type{}, std::true_type{}, t_lo, t_hi);
+        else kloop(std::false_type{}, std::false_type{}, t_lo, t_hi);
+    };
+    if constexpr (SEG == 0) {
+        run(0, n_it);
+        if constexpr (DIAG0) {  // m.x(a, b) = x.m(b, a): lane (i, h) register r holds (row si(r), column i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) tr[((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + i] = gxo[0][r];
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < 16; ++r) gox[0][r] = tr[i * 33 + (r & 3) + 8 * (r >> 2) + 4 * h];
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+            pair_epilogue<DOM, f32x16v, true>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * c,
+                                              DIAG0 && c == 0, i, h, gxx[c], gxo[c], gox[c], goo[c], gxh[c], goh[c],
+                                              ghx[c], gho[c], ld_wind, n_org, rsq_thr, n_org);
     } else {
-        // wave-uniform: does the row block / do the column blocks hold a missing call (flag bit 2)?
-        const bool rm = __any(lane < 32 && (sh.info[lane].fl & 4));
-        const bool cm = __any(32 + lane < NS && (sh.info[32 + lane].fl & 4));
-        auto run = [&](const int t_lo, const int t_hi) {
-            if (rm && cm) kloop(std::true_type{}, std::true_type{}, t_lo, t_hi);
-            else if (rm) kloop(std::true_type{}, std::false_type{}, t_lo, t_hi);
-            else if (cm) kloop(std::false_type{}, std::true_type{}, t_lo, t_hi);
-            else kloop(std::false_type{}, std::false_type{}, t_lo, t_hi);
-        };
-        if constexpr (SEG == 0) {
-            run(0, n_it);
-        } else {
-            static_assert(NC == 1 && RING == 0, "segmented K loop: one column block, register strips");
-            i32x16 ixx[1] = {}, ixo[1] = {}, iox[1] = {}, ioo[1] = {}, ixh[1] = {}, ioh[1] = {}, ihx[1] = {},
-                   iho[1] = {};
-            if constexpr (DOM) {
+        static_assert(NC == 1, "segmented K loop: one column block");
+        i32x16 ixx = {}, ixo = {}, iox = {}, ioo = {}, ixh = {}, ioh = {}, ihx = {}, iho = {};
+        if constexpr (DOM) {
             // add+dom (1 wave / SIMD either way): the fp32 Gram is added into int32 accumulators after every
             // segment (measured 13 % faster than the packed counters below at N = 1 100 003)
             for (int t0 = 0; t0 < n_it; t0 += SEG) {
                 run(t0, min(t0 + SEG, n_it));
-                ixx[0] += __builtin_convertvector(gxx[0], i32x16); ixo[0] += __builtin_convertvector(gxo[0], i32x16);
-                iox[0] += __builtin_convertvector(gox[0], i32x16); ioo[0] += __builtin_convertvector(goo[0], i32x16);
-                ixh[0] += __builtin_convertvector(gxh[0], i32x16); ioh[0] += __builtin_convertvector(goh[0], i32x16);
-                ihx[0] += __builtin_convertvector(ghx[0], i32x16); iho[0] += __builtin_convertvector(gho[0], i32x16);
+                ixx += __builtin_convertvector(gxx[0], i32x16); ixo += __builtin_convertvector(gxo[0], i32x16);
+                iox += __builtin_convertvector(gox[0], i32x16); ioo += __builtin_convertvector(goo[0], i32x16);
+                ixh += __builtin_convertvector(gxh[0], i32x16); ioh += __builtin_convertvector(goh[0], i32x16);
+                ihx += __builtin_convertvector(ghx[0], i32x16); iho += __builtin_convertvector(gho[0], i32x16);
                 gxx[0] = gxo[0] = gox[0] = goo[0] = gxh[0] = goh[0] = ghx[0] = gho[0] = f32x16v{};
             }
-            } else {
+        } else {
             // additive-only: after a segment every entry is < 2^16 + 2^23: its multiples of 2^16 move to a
             // 16-bit counter (entry / 2^16 <= 16N / 2^16 < 2^15 for N < 2^27) and the fp32 remainder, < 2^16,
             // stays in the accumulator (exact: both parts are integers below 2^24).  Two products share one
@@ -1215,38 +1109,19 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
                 for (int r = 0; r < 16; ++r) v[r] = (int)a[r] + (int)(((k[r] >> (16 * half)) & 0xffffu) << 16);
                 return v;
             };
-            ixx[0] = whole(gxx[0], kxx, 0); ixo[0] = whole(gxo[0], kxx, 1);
-            iox[0] = whole(gox[0], kox, 0); ioo[0] = whole(goo[0], kox, 1);
-            }
-            if constexpr (TR && DIAG0) {  // as below, on the int32 Gram (tr reused as 32 x 33 ints)
-                int* tri = reinterpret_cast<int*>(tr);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) tri[((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + i] = ixo[0][r];
-                __syncthreads();
-#pragma unroll
-                for (int r = 0; r < 16; ++r) iox[0][r] = tri[i * 33 + (r & 3) + 8 * (r >> 2) + 4 * h];
-            }
-#pragma unroll
-            for (int c = 0; c < NC; ++c)
-                pair_epilogue<DOM, i32x16, true>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * c,
-                                                 DIAG0 && c == 0, i, h, ixx[c], ixo[c], iox[c], ioo[c], ixh[c], ioh[c],
-                                                 ihx[c], iho[c], ld_wind, n_org, rsq_thr, n_org);
+            ixx = whole(gxx[0], kxx, 0); ixo = whole(gxo[0], kxx, 1);
+            iox = whole(gox[0], kox, 0); ioo = whole(goo[0], kox, 1);
         }
-    }
-    }
-    if constexpr (SEG == 0) {
-    if constexpr (TR && DIAG0) {  // m.x(a, b) = x.m(b, a): lane (i, h) register r holds (row si(r), column i)
+        if constexpr (DIAG0) {  // as above, on the int32 Gram (tr reused as 32 x 33 ints)
+            int* tri = reinterpret_cast<int*>(tr);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) tr[((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + i] = gxo[0][r];
-        __syncthreads();
+            for (int r = 0; r < 16; ++r) tri[((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + i] = ixo[r];
+            __syncthreads();
 #pragma unroll
-        for (int r = 0; r < 16; ++r) gox[0][r] = tr[i * 33 + (r & 3) + 8 * (r >> 2) + 4 * h];
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-        pair_epilogue<DOM, f32x16v, true>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * c,
-                                          DIAG0 && c == 0, i, h, gxx[c], gxo[c], gox[c], goo[c], gxh[c], goh[c],
-                                          ghx[c], gho[c], ld_wind, n_org, rsq_thr, n_org);
+            for (int r = 0; r < 16; ++r) iox[r] = tri[i * 33 + (r & 3) + 8 * (r >> 2) + 4 * h];
+        }
+        pair_epilogue<DOM, i32x16, true>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32, DIAG0, i, h,
+                                         ixx, ixo, iox, ioo, ixh, ioh, ihx, iho, ld_wind, n_org, rsq_thr, n_org);
     }
     __syncthreads();
     for (int s = lane; s < NS; s += 64) {
@@ -1264,48 +1139,6 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     }
 }
 
-// One wave per block pair (items (I, J, 1, 0)), strips streamed through a RING-deep LDS ring.
-template <bool DOM, int RING>
-__global__ void __launch_bounds__(64, 2) band_f4_ring_kernel(
-    const uint32_t* __restrict__ geno, int pitch_words, int n_it, const SnpConst* __restrict__ cst,
-    const int4* __restrict__ items, const double* __restrict__ pos, const int* __restrict__ Lw,
-    const int* __restrict__ Rw, const uint8_t* __restrict__ sflags, int n_snp, double ld_wind, double n_org,
-    double rsq_thr, int own_lo, int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
-    int* __restrict__ ws_acc, int xcd) {
-    __shared__ BandI8Lds sh;
-    __shared__ uint4 ring[RING * 2 * 64];
-    const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
-#define NLDSC_BODY(DIAG_)                                                                                           \
-    band_f4_body<DOM, 1, DIAG_, 0, RING>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, \
-                                         n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, true, ring)
-    if (it.x == it.y) NLDSC_BODY(true); else NLDSC_BODY(false);
-#undef NLDSC_BODY
-}
-
-// Skewed 2x2 tiles (I, J, mask) of single block pairs, one wave per pair (wave 0 -> (I, J), 1 -> (I, J+1),
-// 2 -> (I+1, J+1), 3 -> (I+1, J+2); bit w of mask = wave w's pair is scheduled): the four waves of a
-// workgroup run on one CU and read five strips between them instead of eight, so every strip
-// they share is fetched beyond the CU once.  Each wave decodes its own operands (no LDS traffic).
-template <bool DOM, int SYNC>
-__global__ void __launch_bounds__(256, 2) band_f4_grp_kernel(
-    const uint32_t* __restrict__ geno, int pitch_words, int n_it, const SnpConst* __restrict__ cst,
-    const int4* __restrict__ tiles, const double* __restrict__ pos, const int* __restrict__ Lw,
-    const int* __restrict__ Rw, const uint8_t* __restrict__ sflags, int n_snp, int nblk, double ld_wind,
-    double n_org, double rsq_thr, int own_lo, int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
-    int* __restrict__ ws_acc, int xcd) {
-    __shared__ BandI8Lds sh[4];
-    const int4 tile = tiles[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int a = min(tile.x + (w >> 1), nblk - 1), b = min(tile.y + (w & 1) + (w >> 1), nblk - 1);
-    const bool active = (tile.z >> w) & 1;
-    const int4 it = make_int4(a, b, 1, 0);
-#define NLDSC_BODY(DIAG_)                                                                                           \
-    band_f4_body<DOM, 1, DIAG_, SYNC>(sh[w], it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, \
-                                      n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, active)
-    if (a == b) NLDSC_BODY(true); else NLDSC_BODY(false);
-#undef NLDSC_BODY
-}
-
 // WPS 2: single block-pair items; WPS 1: items of up to 2 column blocks (1 wave per SIMD, the
 // 2 x 128 accumulator registers in AGPRs).
 template <bool DOM, int WPS, int SEG = 0>
@@ -1320,169 +1153,13 @@ __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __rest
     __shared__ float tr[32 * 33];
     const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
 #define NLDSC_BODY(NC_, DIAG_)                                                                                        \
-    band_f4_body<DOM, NC_, DIAG_, 0, 0, true, SEG>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, \
-                                                   ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc,  \
-                                                   true, nullptr, tr)
+    band_f4_body<DOM, NC_, DIAG_, SEG>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind,   \
+                                       n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, tr)
     const bool diag = it.y == it.x;
     if constexpr (SEG > 0) { if (diag) NLDSC_BODY(1, true); else NLDSC_BODY(1, false); }
     else if (WPS == 1 && it.z == 2) { if (diag) NLDSC_BODY(2, true); else NLDSC_BODY(2, false); }
     else { if (diag) NLDSC_BODY(1, true); else NLDSC_BODY(1, false); }
 #undef NLDSC_BODY
-}
-
-// ---- skewed 2x2 tiles: the four waves of a workgroup share every decoded strip through LDS ----
-// Tile (I, J, mask): wave 0 -> block pair (I, J), 1 -> (I, J+1), 2 -> (I+1, J+1), 3 -> (I+1, J+2);
-// bit w of mask = wave w's pair is scheduled.  The shape follows the band (row I+1's columns are
-// row I's shifted by one block): on the C3 geometry 94.5% of the slots are needed pairs, and the
-// five strips R0=I, R1=I+1, C0=J, C1=J+1, C2=J+2 are decoded ONCE per K step for four MFMA waves
-// (1.25 words per thread and step instead of 2, and each strip fetched once per tile).
-// Thread (w, lane) decodes strip w (R0, R1, C0, C1) for its own MFMA lane slot; strip C2 is split
-// by K step: wave w decodes its word q == w of every 4-step chunk.
-constexpr int TS = 5;  // strips per tile
-
-struct TileLds {
-    i32x4 ring[2][TS][3][64];  // [K step & 1][strip][x, h, o][lane]: decoded MFMA operands
-    SnpSlot info[TS * 32];
-    SnpConst cst[TS * 32];
-    double l2[TS * 32], l2d[TS * 32];
-    int wsa[TS * 32], wsd[TS * 32], wse[TS * 32];
-};
-
-// workgroup barrier that orders LDS only (no wait on the global prefetch in flight)
-__device__ __forceinline__ void tile_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-__device__ __forceinline__ void tile_put(TileLds& sh, bool dom, int slot, int strip, int lane, uint32_t word) {
-    i32x4 X, H, O;
-    decode16(word, X, H, O);
-    sh.ring[slot][strip][0][lane] = X;
-    if (dom) sh.ring[slot][strip][1][lane] = H;
-    sh.ring[slot][strip][2][lane] = O;
-}
-
-// K loop of one wave.  Step k's operands live in ring slot k & 1: written (decoded) during step
-// k - 2, read into registers during step k - 1, consumed by the MFMAs of step k; one barrier per
-// step.  MODE 0: full pair, 1: diagonal pair (R_i . A_j skipped), 2: unscheduled pair (this wave
-// only decodes for the others).
-template <bool DOM, int MODE>
-__device__ __forceinline__ void tile_kloop(TileLds& sh, int w, int lane, int rs, int cs, const uint4* __restrict__ own_p,
-                                           const uint32_t* __restrict__ c2_p, int n_it, i32x16 (&g)[8]) {
-    auto ld4 = [&](int t) { return own_p[2 * min(t, n_it - 1)]; };
-    auto ld1 = [&](int t) { return c2_p[8 * min(t, n_it - 1)]; };
-    uint4 g0 = ld4(0), g1 = ld4(1), g2 = ld4(2);
-    uint32_t c0 = ld1(0), c1 = ld1(1), c2 = ld1(2);
-    i32x4 Xi{}, Hi{}, Oi{}, Xj{}, Hj{}, Oj{};
-    // prologue: step 0 into slot 0, read it; step 1 into slot 1
-    tile_put(sh, DOM, 0, w, lane, g0.x);
-    if (w == 0) tile_put(sh, DOM, 0, 4, lane, c0);
-    tile_sync();
-    if (MODE != 2) {
-        Xi = sh.ring[0][rs][0][lane]; Oi = sh.ring[0][rs][2][lane];
-        Xj = sh.ring[0][cs][0][lane]; Oj = sh.ring[0][cs][2][lane];
-        if (DOM) { Hi = sh.ring[0][rs][1][lane]; Hj = sh.ring[0][cs][1][lane]; }
-    }
-    tile_put(sh, DOM, 1, w, lane, g0.y);
-    if (w == 1) tile_put(sh, DOM, 1, 4, lane, c0);
-    tile_sync();
-    for (int t = 0; t < n_it; ++t) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int cur = q & 1, nxt = cur ^ 1;
-            i32x4 Xin{}, Hin{}, Oin{}, Xjn{}, Hjn{}, Ojn{};
-            if (MODE != 2) {  // step k+1's operands (its slot was completed before the last barrier)
-                Xin = sh.ring[nxt][rs][0][lane]; Oin = sh.ring[nxt][rs][2][lane];
-                Xjn = sh.ring[nxt][cs][0][lane]; Ojn = sh.ring[nxt][cs][2][lane];
-                if (DOM) { Hin = sh.ring[nxt][rs][1][lane]; Hjn = sh.ring[nxt][cs][1][lane]; }
-            }
-            {  // decode step k+2 into the slot step k's operands were read from (steps K, K+1 are
-               // decoded from the clamped last chunk into slots nobody reads)
-                const uint32_t wd = q == 0 ? g0.z : q == 1 ? g0.w : q == 2 ? g1.x : g1.y;
-                tile_put(sh, DOM, cur, w, lane, wd);
-                if (w == ((q + 2) & 3)) tile_put(sh, DOM, cur, 4, lane, q < 2 ? c0 : c1);
-            }
-            if (MODE != 2) {
-                g[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Xj, g[0], 0, 0, 0);
-                g[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Oj, g[1], 0, 0, 0);
-                g[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Xj, g[2], 0, 0, 0);
-                g[3] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Oj, g[3], 0, 0, 0);
-                if (DOM) {
-                    g[4] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Xi, Hj, g[4], 0, 0, 0);
-                    g[5] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Oi, Hj, g[5], 0, 0, 0);
-                    if (MODE == 0) {
-                        g[6] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Hi, Xj, g[6], 0, 0, 0);
-                        g[7] = __builtin_amdgcn_mfma_i32_32x32x32_i8(Hi, Oj, g[7], 0, 0, 0);
-                    }
-                }
-            }
-            tile_sync();
-            if (MODE != 2) {
-                Xi = Xin; Hi = Hin; Oi = Oin; Xj = Xjn; Hj = Hjn; Oj = Ojn;
-            }
-        }
-        g0 = g1; g1 = g2; g2 = ld4(t + 3);
-        c0 = c1; c1 = c2; c2 = ld1(t + 3);
-    }
-}
-
-template <bool DOM>
-__global__ void __launch_bounds__(256, 2) band_tile_kernel(
-    const uint32_t* __restrict__ geno, int pitch_words, int n_it, const SnpConst* __restrict__ cst,
-    const int4* __restrict__ items, const double* __restrict__ pos, const int* __restrict__ Lw,
-    const int* __restrict__ Rw, const uint8_t* __restrict__ sflags, int n_snp, int nblk, double ld_wind, double n_org,
-    double rsq_thr, int own_lo, int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
-    int* __restrict__ ws_acc, int xcd) {
-    __shared__ TileLds sh;
-    const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches on it
-    const int i = lane & 31, h = lane >> 5;
-    const int I = it.x, J = it.y, mask = it.z;
-    // strip s -> block (strips past the last block are clamped; their pairs are never scheduled)
-    auto strip_blk = [&](int s) { return min(s < 2 ? I + s : J + s - 2, nblk - 1); };
-    for (int s = tid; s < TS * 32; s += 256) {
-        const int g = strip_blk(s >> 5) * 32 + (s & 31);
-        SnpSlot si;
-        si.g = g;
-        if (g < n_snp) {
-            si.pos = pos[g]; si.L = Lw[g]; si.R = Rw[g]; si.fl = sflags[g];
-        } else {
-            si.pos = 0.0; si.L = -1; si.R = -2; si.fl = 0;
-        }
-        sh.info[s] = si;
-        sh.cst[s] = cst[g];
-        sh.l2[s] = 0.0; sh.l2d[s] = 0.0;
-        sh.wsa[s] = 0; sh.wsd[s] = 0; sh.wse[s] = 0;
-    }
-    const int rs = w >> 1, cs = 2 + (w & 1) + rs;  // this wave's row strip and column strip
-    const uint4* own_p = reinterpret_cast<const uint4*>(geno + (size_t)(strip_blk(w) * 32 + i) * pitch_words) + h;
-    const uint32_t* c2_p = geno + (size_t)(strip_blk(4) * 32 + i) * pitch_words + 4 * h + w;
-    i32x16 g[8];
-#pragma unroll
-    for (int b = 0; b < 8; ++b) g[b] = i32x16{};
-    const bool active = (mask >> w) & 1, diag = J == I && !(w & 1);
-    if (!active) tile_kloop<DOM, 2>(sh, w, lane, rs, cs, own_p, c2_p, n_it, g);
-    else if (diag) tile_kloop<DOM, 1>(sh, w, lane, rs, cs, own_p, c2_p, n_it, g);
-    else tile_kloop<DOM, 0>(sh, w, lane, rs, cs, own_p, c2_p, n_it, g);
-    if (active)
-        pair_epilogue<DOM>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, rs * 32, cs * 32, diag, i, h, g[0],
-                           g[1], g[2], g[3], g[4], g[5], g[6], g[7], ld_wind, n_org, rsq_thr);
-    __syncthreads();
-    for (int s = tid; s < TS * 32; s += 256) {
-        const int gg = sh.info[s].g;
-        if (gg < own_lo || gg >= own_hi || gg >= n_snp) continue;
-        if (sh.wsa[s]) {
-            unsafeAtomicAdd(&l2_acc[gg], sh.l2[s]);
-            atomicAdd(&ws_acc[gg], sh.wsa[s]);
-        }
-        if (DOM && sh.wsd[s]) {
-            unsafeAtomicAdd(&l2d_acc[gg], sh.l2d[s]);
-            atomicAdd(&ws_acc[(size_t)n_snp + gg], sh.wsd[s]);
-            if (sh.wse[s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + gg], sh.wse[s]);
-        }
-    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1627,57 +1304,6 @@ hipError_t launch_plan_emit(int n, const int2* rows, const int* meta, const int*
     return hipGetLastError();
 }
 
-// One workgroup per run of the item list (the XCD runs of xcd_slot, or the whole list): a stable partition
-// of the run into its off-diagonal items, then its diagonal items.  The diagonal block pairs issue 6 of the
-// 8 MFMAs per K step, so a run whose last items are diagonal drains its XCD's slots sooner.
-__global__ void __launch_bounds__(1024) diag_last_kernel(const int4* __restrict__ in, int4* __restrict__ out, int n,
-                                                         int runs) {
-    __shared__ int wave_off[16], total;
-    const int x = blockIdx.x, per = n / runs, rem = n % runs;
-    const int s0 = x * per + min(x, rem), len = per + (x < rem ? 1 : 0);
-    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    if (t == 0) total = 0;
-    __syncthreads();
-    int cnt = 0;  // pass 1: off-diagonal items of the run (coalesced 16-byte reads)
-    for (int k = t; k < len; k += 1024) cnt += in[s0 + k].x != in[s0 + k].y;
-    atomicAdd(&total, cnt);
-    __syncthreads();
-    const int n_off = total;
-    // pass 2: rounds of 1024 consecutive items; rank within the round from wave ballots
-    int base_off = 0, base_diag = n_off;
-    for (int r = 0; r < len; r += 1024) {
-        const int k = r + t;
-        int4 it = make_int4(0, 0, 0, 0);
-        if (k < len) it = in[s0 + k];
-        const bool off = k < len && it.x != it.y, diag = k < len && it.x == it.y;
-        const uint64_t bo = __ballot(off);
-        const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-        if (lane == 0) wave_off[w] = __popcll(bo);
-        __syncthreads();
-        int pre = 0, all = 0;
-        for (int v = 0; v < 16; ++v) {
-            const int c = wave_off[v];
-            pre += v < w ? c : 0;
-            all += c;
-        }
-        const int n_round = min(1024, len - r);
-        const int wave_base = w * 64;  // items of this wave before it in the round
-        const int in_wave_off = __popcll(bo & below);
-        if (off) out[s0 + base_off + pre + in_wave_off] = it;
-        if (diag) out[s0 + base_diag + (wave_base - pre) + (lane - in_wave_off)] = it;
-        base_off += all;
-        base_diag += n_round - all;
-        __syncthreads();
-    }
-}
-
-hipError_t launch_diag_last(const int4* in, int4* out, int n, int runs, hipStream_t st) {
-    if (n <= 0) return hipSuccess;
-    runs = max(1, min(runs, n));
-    hipLaunchKernelGGL(diag_last_kernel, dim3(runs), dim3(1024), 0, st, in, out, n, runs);
-    return hipGetLastError();
-}
-
 hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                        const float2* lut, const int4* items, const double* pos, const int* Lw, const int* Rw,
                        const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
@@ -1721,57 +1347,6 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
     if (n_it > F4_SEG_CHUNKS) { if (dom) NLDSC_BAND(true, 1, F4_SEG_CHUNKS); else NLDSC_BAND(false, 2, F4_SEG_CHUNKS); }
     else if (dom) { if (max_nc == 2) NLDSC_BAND(true, 1, 0); else NLDSC_BAND(true, 2, 0); }
     else { if (max_nc == 2) NLDSC_BAND(false, 1, 0); else NLDSC_BAND(false, 2, 0); }
-#undef NLDSC_BAND
-    return hipGetLastError();
-}
-
-hipError_t launch_band_f4_ring(bool dom, int ring, int n_items, const uint32_t* geno, int pitch_words, int n_it,
-                               const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
-                               const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr,
-                               int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd,
-                               hipStream_t st) {
-    if (n_items <= 0) return hipSuccess;
-#define NLDSC_BAND(DOM_, RING_)                                                                                      \
-    hipLaunchKernelGGL((band_f4_ring_kernel<DOM_, RING_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it,  \
-                       cst, items, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc,     \
-                       l2d_acc, ws_acc, xcd ? 1 : 0)
-    if (dom) { if (ring >= 5) NLDSC_BAND(true, 5); else if (ring == 4) NLDSC_BAND(true, 4); else NLDSC_BAND(true, 3); }
-    else { if (ring >= 5) NLDSC_BAND(false, 5); else if (ring == 4) NLDSC_BAND(false, 4); else NLDSC_BAND(false, 3); }
-#undef NLDSC_BAND
-    return hipGetLastError();
-}
-
-hipError_t launch_band_f4_grp(bool dom, int sync, int n_tiles, const uint32_t* geno, int pitch_words, int n_it,
-                              int nblk, const SnpConst* cst, const int4* tiles, const double* pos, const int* Lw,
-                              const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind, double n_org,
-                              double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc,
-                              bool xcd, hipStream_t st) {
-    if (n_tiles <= 0) return hipSuccess;
-#define NLDSC_BAND(DOM_, SYNC_)                                                                                      \
-    hipLaunchKernelGGL((band_f4_grp_kernel<DOM_, SYNC_>), dim3(n_tiles), dim3(256), 0, st, geno, pitch_words, n_it,   \
-                       cst, tiles, pos, Lw, Rw, sflags, n_snp, nblk, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, \
-                       l2d_acc, ws_acc, xcd ? 1 : 0)
-    if (dom) {
-        if (sync >= 8) NLDSC_BAND(true, 8); else if (sync >= 2) NLDSC_BAND(true, 2); else if (sync == 1) NLDSC_BAND(true, 1);
-        else NLDSC_BAND(true, 0);
-    } else {
-        if (sync >= 8) NLDSC_BAND(false, 8); else if (sync >= 2) NLDSC_BAND(false, 2); else if (sync == 1) NLDSC_BAND(false, 1);
-        else NLDSC_BAND(false, 0);
-    }
-#undef NLDSC_BAND
-    return hipGetLastError();
-}
-
-hipError_t launch_band_tile(bool dom, int n_tiles, const uint32_t* geno, int pitch_words, int n_it, int nblk,
-                            const SnpConst* cst, const int4* tiles, const double* pos, const int* Lw, const int* Rw,
-                            const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
-                            int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st) {
-    if (n_tiles <= 0) return hipSuccess;
-#define NLDSC_BAND(DOM_)                                                                                            \
-    hipLaunchKernelGGL((band_tile_kernel<DOM_>), dim3(n_tiles), dim3(256), 0, st, geno, pitch_words, n_it, cst, tiles, \
-                       pos, Lw, Rw, sflags, n_snp, nblk, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc,   \
-                       ws_acc, xcd ? 1 : 0)
-    if (dom) NLDSC_BAND(true); else NLDSC_BAND(false);
 #undef NLDSC_BAND
     return hipGetLastError();
 }

@@ -426,31 +426,6 @@ def test_allele_orientation_is_invisible(name):
     assert_ld_close(out["1", "f32"], exp, label=f"{name} oriented f32")
 
 
-@pytest.mark.parametrize("knob", ["1", "2"])
-def test_item_order_knobs_change_nothing(engine, knob, monkeypatch):
-    """NLDSC_DIAG_LAST=1 (diagonal block pairs last in every XCD run, diag_last_kernel) and =2 (diagonal
-    items in a launch of their own) reorder the fp4 and int8 work items only: every count equals the
-    default order's, the sums agree to fp64 summation-order rounding."""
-    from nldsc_amd import synth
-    from nldsc_amd.engine import Engine
-    N, M = 1003, 30000  # 938 row blocks, ~16k items: two 1024-item scan rounds per XCD run
-    spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=60.0, seed=11, missing=0.01)
-    rows = synth.pack_bed_rows(synth.genotypes(spec))
-    pos = synth.positions_cm(spec)
-    bed = synth.bed_bytes(rows)
-    args = (1.0, 0.01, 1e-5, 1.0 / M, pos)
-    monkeypatch.setenv("NLDSC_DIAG_LAST", knob)
-    alt = Engine(0)
-    try:
-        alt.load_bed_bytes(bed, M, N)
-        engine.load_bed_bytes(bed, M, N)
-        for mode in EXACT:
-            same_gram(alt.run(*args, flags=MODES[mode]), engine.run(*args, flags=MODES[mode]),
-                      f"DIAG_LAST={knob} {mode}")
-    finally:
-        alt.close()
-
-
 @pytest.mark.parametrize("N", [301, 1003, 4096])
 def test_missing_free_blocks_skip_m_products(engine, N):
     """32-SNP blocks without any missing call have an all-zero missing-indicator plane, and the fp4 kernel

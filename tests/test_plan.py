@@ -83,49 +83,6 @@ def test_plan_is_tight_on_c3_geometry():
     assert len(items) / ((M + 31) // 32) < 10.6
 
 
-def tile_pairs(tiles):
-    """Block pairs scheduled by skewed 2x2 tiles (I, J, mask): waves (I,J), (I,J+1), (I+1,J+1), (I+1,J+2)."""
-    out = []
-    for I, J, mask, _ in tiles:
-        for w, (a, b) in enumerate(((I, J), (I, J + 1), (I + 1, J + 1), (I + 1, J + 2))):
-            if mask >> w & 1:
-                out.append((int(a), int(b)))
-    return out
-
-
-@pytest.mark.parametrize("seed", range(4))
-def test_tiles_partition_single_pair_schedule(seed):
-    """max_nc=4 (exact-path tiles) schedules exactly the block pairs of the max_nc=1 plan, each once."""
-    from nldsc_amd import _lib
-    rng = np.random.default_rng(100 + seed)
-    n = int(rng.integers(1, 3000))
-    pos = np.cumsum(rng.exponential(0.01, n))
-    pos[rng.random(n) < 0.03] = -1.0
-    passed = (pos >= 0) & (rng.random(n) > 0.1)
-    w = float(rng.choice([0.02, 0.3, 2.0]))
-    a = int(rng.integers(0, n))
-    for own in (None, (a, min(n, a + 500))):
-        _, _, ones = _lib.plan_band(pos, passed.astype(np.uint8), w, own=own, max_nc=1)
-        _, _, tiles = _lib.plan_band(pos, passed.astype(np.uint8), w, own=own, max_nc=4)
-        pairs = tile_pairs(tiles)
-        assert len(pairs) == len(set(pairs))
-        assert set(pairs) == {(int(I), int(J)) for I, J, _, _ in ones}
-        nblk = (n + 31) // 32
-        assert all(0 <= I < nblk and I <= J < nblk and 0 < m < 16 for I, J, m, _ in tiles)
-
-
-def test_tiles_fill_on_c3_geometry():
-    """Skewed tiles follow the band: >= 93% of the tile slots are needed pairs on the C3 geometry."""
-    from nldsc_amd import _lib
-    rng = np.random.default_rng(7)
-    M = 80_000
-    rng.uniform(0.02, 0.5, size=M)
-    pos = np.round(np.cumsum(rng.exponential(280.0 / M, size=M)), 6)
-    _, _, ones = _lib.plan_band(pos, np.ones(M, np.uint8), 1.0)
-    _, _, tiles = _lib.plan_band(pos, np.ones(M, np.uint8), 1.0, max_nc=4)
-    assert len(ones) / (4 * len(tiles)) > 0.93
-
-
 def left_pointers_from_all_pass(pos, passed, A):
     """The rule left_pointer_kernel applies (sorted positions): L_j = first used passing SNP in
     [A_j, j), else j; -1 where A_j < 0 or j fails MAF."""
