@@ -72,7 +72,32 @@ static float mean_f(const float* x, int n) {
     return (a + b) / (float)n;
 }
 
-/* arma::dot for fvec: own two-accumulator loop up to 32 elements, BLAS sdot above */
+/* arma::dot for fvec (op_dot::direct_dot): its own two-accumulator loop up to 32 elements, BLAS sdot above.
+ * The sdot is OpenBLAS's x86-64 SkylakeX kernel as shipped with scipy (OpenBLAS 0.3.28, DYNAMIC_ARCH, one
+ * thread), restated from its observable arithmetic and pinned bit for bit against that library by
+ * tests/test_oracle.py::test_dot_matches_openblas_sdot: n1 = n & -32 elements go through 4 x 16 fp32 FMA
+ * accumulators (64 elements per step), folded to 4 x 8 (lane k + lane k+8), one more 4 x 8 FMA step for the
+ * last 32 when n1 % 64 = 32, the four summed left to right, 128-bit halves added and two horizontal adds;
+ * the remaining n - n1 products (fp32) are added to that sum in double and the result is rounded to float. */
+static float sdot_kernel(const float* x, const float* y, int n1) {
+    float a[4][16];
+    memset(a, 0, sizeof a);
+    int i = 0;
+    for (; i + 64 <= n1; i += 64)
+        for (int q = 0; q < 4; ++q)
+            for (int k = 0; k < 16; ++k) a[q][k] = fmaf(x[i + 16 * q + k], y[i + 16 * q + k], a[q][k]);
+    float b[4][8];
+    for (int q = 0; q < 4; ++q)
+        for (int k = 0; k < 8; ++k) b[q][k] = a[q][k] + a[q][k + 8];
+    for (; i < n1; i += 32)
+        for (int q = 0; q < 4; ++q)
+            for (int k = 0; k < 8; ++k) b[q][k] = fmaf(x[i + 8 * q + k], y[i + 8 * q + k], b[q][k]);
+    float c[8], h[4];
+    for (int k = 0; k < 8; ++k) c[k] = ((b[0][k] + b[1][k]) + b[2][k]) + b[3][k];
+    for (int k = 0; k < 4; ++k) h[k] = c[k] + c[k + 4];
+    return (h[0] + h[1]) + (h[2] + h[3]);
+}
+
 static float dot_f(const float* x, const float* y, int n) {
     if (n <= 32) {
         float a = 0.f, b = 0.f;
@@ -81,22 +106,18 @@ static float dot_f(const float* x, const float* y, int n) {
         if (i < n) a += x[i] * y[i];
         return a + b;
     }
-    typedef float v8 __attribute__((vector_size(32)));
-    v8 s0 = {0}, s1 = {0}, s2 = {0}, s3 = {0};
-    int i = 0;
-    for (; i + 32 <= n; i += 32) {
-        v8 a0, a1, a2, a3, b0, b1, b2, b3;
-        memcpy(&a0, x + i, 32); memcpy(&a1, x + i + 8, 32);
-        memcpy(&a2, x + i + 16, 32); memcpy(&a3, x + i + 24, 32);
-        memcpy(&b0, y + i, 32); memcpy(&b1, y + i + 8, 32);
-        memcpy(&b2, y + i + 16, 32); memcpy(&b3, y + i + 24, 32);
-        s0 += a0 * b0; s1 += a1 * b1; s2 += a2 * b2; s3 += a3 * b3;
+    const int n1 = n & -32;
+    double dot = (double)sdot_kernel(x, y, n1);
+    for (int i = n1; i < n; ++i) {
+        const float p = x[i] * y[i];
+        dot += (double)p;
     }
-    v8 s = (s0 + s1) + (s2 + s3);
-    float r = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-    for (; i < n; ++i) r += x[i] * y[i];
-    return r;
+    return (float)dot;
 }
+
+/* exported for the pinning test only */
+float oracle_sdot(const float* x, const float* y, int n) { return dot_f(x, y, n); }
+float oracle_mean(const float* x, int n) { return mean_f(x, n); }
 
 static double dot_d(const float* x, const float* y, int n) {
     double a = 0, b = 0, c = 0, d = 0;
@@ -434,4 +455,72 @@ done:
     if (cache) for (int i = 0; i < n_snp; ++i) { free(cache[i].add); free(cache[i].res); }
     free(cache); free(idx); free(pass); free(mafs); free(L); free(R);
     return rc;
+}
+
+/*
+ * Exact-arithmetic helpers for the fp64 truth (oracle.py run_f64_targets): integer genotype-code
+ * counts per SNP and 4x4 code contingency tables of SNP pairs, over the samples the reference reads
+ * (stream.h:43-69, same last-byte rule as unpack_row).  Counting only — no floating point.
+ */
+int oracle_code_counts(size_t bed_len, const uint8_t* bed, int n_snp, int n_org, unsigned flags,
+                       int n_threads, int64_t* counts /* [n_snp][4] */) {
+    int rc = oracle_check_bed(bed_len, bed, n_snp, n_org);
+    if (rc) return rc;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#else
+    (void)n_threads;
+#endif
+    const int nb = n_org / 4 + (n_org % 4 > 0);
+    int fail = 0;
+    #pragma omp parallel reduction(|:fail)
+    {
+        uint8_t* codes = (uint8_t*)malloc((size_t)nb * 4);
+        if (!codes) fail = 1;
+        #pragma omp for schedule(dynamic, 16)
+        for (int i = 0; i < n_snp; ++i) {
+            if (!codes) continue;
+            unpack_row(bed + 3 + (size_t)i * nb, n_org, nb, codes, flags);
+            int64_t c[4] = {0, 0, 0, 0};
+            for (int s = 0; s < n_org; ++s) c[codes[s] >> 6]++;
+            for (int g = 0; g < 4; ++g) counts[4 * (size_t)i + g] = c[g];
+        }
+        free(codes);
+    }
+    return fail ? ORC_OOM : ORC_OK;
+}
+
+int oracle_code_tables(size_t bed_len, const uint8_t* bed, int n_snp, int n_org, unsigned flags,
+                       int n_threads, int j, const int32_t* ks, int n_k, int64_t* tables /* [n_k][4][4] */) {
+    int rc = oracle_check_bed(bed_len, bed, n_snp, n_org);
+    if (rc) return rc;
+    if (j < 0 || j >= n_snp) return ORC_ARG;
+    for (int q = 0; q < n_k; ++q) if (ks[q] < 0 || ks[q] >= n_snp) return ORC_ARG;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#else
+    (void)n_threads;
+#endif
+    const int nb = n_org / 4 + (n_org % 4 > 0);
+    uint8_t* cj = (uint8_t*)malloc((size_t)nb * 4);
+    if (!cj) return ORC_OOM;
+    unpack_row(bed + 3 + (size_t)j * nb, n_org, nb, cj, flags);
+    for (int s = 0; s < n_org; ++s) cj[s] = (uint8_t)((cj[s] >> 6) << 2); /* row code g -> 4g */
+    int fail = 0;
+    #pragma omp parallel reduction(|:fail)
+    {
+        uint8_t* ck = (uint8_t*)malloc((size_t)nb * 4);
+        if (!ck) fail = 1;
+        #pragma omp for schedule(dynamic, 4)
+        for (int q = 0; q < n_k; ++q) {
+            if (!ck) continue;
+            unpack_row(bed + 3 + (size_t)ks[q] * nb, n_org, nb, ck, flags);
+            int64_t c[16] = {0};
+            for (int s = 0; s < n_org; ++s) c[cj[s] | (ck[s] >> 6)]++;
+            memcpy(tables + 16 * (size_t)q, c, sizeof c);
+        }
+        free(ck);
+    }
+    free(cj);
+    return fail ? ORC_OOM : ORC_OK;
 }

@@ -1,5 +1,7 @@
 """The oracle against the committed golden vectors, the fp64 restatement and the reference's
 documented quirks (CPU only)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -101,3 +103,39 @@ def test_f64_targets_contingency_truth(name):
                             pos, t)
     for k in got:
         np.testing.assert_allclose(got[k], f64[k][t], rtol=1e-12, atol=1e-12, err_msg=k)
+
+
+def _openblas_arch():
+    try:
+        from threadpoolctl import threadpool_info
+        import scipy.linalg  # noqa: F401  (loads scipy's OpenBLAS)
+    except ImportError:
+        return None
+    for d in threadpool_info():
+        if d.get("internal_api") == "openblas" and "scipy" in os.path.basename(d.get("filepath", "")):
+            return d.get("architecture"), d.get("version")
+    return None
+
+
+@pytest.mark.skipif(_openblas_arch() is None or _openblas_arch()[0] != "SkylakeX",
+                    reason="needs scipy's OpenBLAS with its SkylakeX sdot kernel (this container's CPU)")
+def test_dot_matches_openblas_sdot():
+    """The oracle's arma::dot -> BLAS sdot (n > 32) is OpenBLAS's own arithmetic: bit-identical to the
+    single-threaded sdot of the OpenBLAS that scipy ships (0.3.28, SkylakeX kernel) — the library the
+    survey's probe of the reference linked — on lengths around every kernel boundary (32-element tail,
+    64-element main step) and at the BASELINE sizes."""
+    import ctypes
+
+    from scipy.linalg import blas
+    from threadpoolctl import threadpool_limits
+    L = O.lib()
+    L.oracle_sdot.restype = ctypes.c_float
+    fp = ctypes.POINTER(ctypes.c_float)
+    rng = np.random.default_rng(9)
+    with threadpool_limits(1):
+        for n in list(range(33, 140)) + [1000, 4097, 10001, 50_000, 315_599]:
+            for kind in range(2):
+                x = rng.standard_normal(n).astype(np.float32)
+                y = (rng.standard_normal(n) if kind else rng.integers(0, 3, n) - 0.7).astype(np.float32)
+                got = L.oracle_sdot(x.ctypes.data_as(fp), y.ctypes.data_as(fp), n)
+                assert np.float32(got) == np.float32(blas.sdot(x, y)), n
