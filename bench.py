@@ -4,12 +4,14 @@
 One step = one full `calculate` pass (repack + statistics + window schedule + band correlation kernel
 + finalize + results to host) over a chromosome-sized synthetic .bed image already resident in HBM
 (BASELINE.json configs[2]: N = 315 599, M = 80 000 over 280 cM, additive + dominance, --ld-wind-cm 1).
-With N GPUs (torchrun, one process per GPU, RCCL) every rank processes its own chromosome unit
-(weak scaling: position sharding across chromosomes has no hot-path exchange) and the per-SNP score
-tables are gathered to rank 0 over RCCL at the end of every step.
+With N GPUs (torchrun, one process per GPU, RCCL) the ONE chromosome is position-sharded over the ranks
+(strong scaling, as the BASELINE metric reads: chr1 at 1/2/4/8 GPUs): rank g keeps its owned SNP range plus
+one window of halo rows resident, computes the owned SNPs (no hot-path exchange) and the score table is
+gathered to rank 0 over RCCL every step.  `--weak` runs one chromosome per GPU instead.
 
 Prints ONE JSON line on rank 0.  `roofline` is for the band correlation kernel (HIP events on the
-engine's stream, averaged over the timed steps); `cpu_baseline` times the C port of the reference's
+engine's stream, averaged over the timed steps), on SURVEY.md §8(d3)'s FLOP basis; `wall_clock_from_file_s`
+times the drop-in `_ldscore.calculate` from the .bed written to local disk; `cpu_baseline` times the C port of the reference's
 CPU path (oracle/, fp32 sdot per pair, OpenMP over window neighbours) on the first SNPs of the same
 chromosome (rank 0, N = 1 only).
 """
@@ -40,26 +42,41 @@ PATHS = {
 }
 
 
-def pmc_traffic(kernel_key: str, n_org: int, n_snp: int):
-    """HBM-side bytes per launch of `kernel_key` from the newest committed rocprofv3 PMC summary
-    (profiles/*_pmc*.json, measured on the same C3 workload), or None."""
+def kernel_source_sha16() -> str:
+    """Fingerprint of the kernels' source (a PMC summary counts only for the kernels it was measured on)."""
+    import hashlib
+    with open(os.path.join(REPO, "nldsc_amd", "csrc", "ld_kernels.hip"), "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
+def pmc_traffic(kernel_key: str, n_org: int, n_snp: int, missing: float):
+    """HBM-side bytes per launch of `kernel_key` from the committed rocprofv3 PMC summary measured on the same
+    workload AND the same kernel source (profiles/*_pmc*.json carrying `kernels_source_sha16`): (bytes, file),
+    or (None, reason) when no summary matches the current kernels."""
     import glob
     # profiles/pmc_current.txt names the summary measured on the current kernels; then any other
     current = os.path.join(REPO, "profiles", "pmc_current.txt")
     first = []
     if os.path.exists(current):
         first = [os.path.join(REPO, "profiles", open(current).read().strip())]
+    sha = kernel_source_sha16()
+    stale = None
     for path in first + sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc*.json")), reverse=True):
         try:
             doc = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if f"N={n_org}" not in doc.get("workload", "") or f"M={n_snp}" not in doc.get("workload", ""):
+        wl = doc.get("workload", "")
+        if f"N={n_org}" not in wl or f"M={n_snp}" not in wl or f"missing={missing:g}" not in wl:
+            continue
+        if doc.get("kernels_source_sha16") != sha:
+            stale = stale or os.path.relpath(path, REPO)
             continue
         for name, k in doc.get("kernels", {}).items():
             if name.startswith(kernel_key):
                 return k["traffic_bytes"], os.path.relpath(path, REPO)
-    return None, None
+    return None, (f"no PMC summary of the current kernels (source sha {sha}); newest for this workload: {stale}"
+                  if stale else "no PMC summary for this workload")
 
 
 def log(*a):
@@ -95,6 +112,55 @@ def cpu_baseline(bed_host: bytes, n_snp, n_org, w, maf, std_thr, rsq, pos, targe
                        f"fp32 sdot + per-pair vector copies, OpenMP over neighbours)")
 
 
+def file_wall_clock(bed_host: bytes, n_snp, n_org, w, maf, std_thr, rsq, pos, flags) -> dict:
+    """The metric's wall-clock half: the synthetic .bed written to a local file once, then the drop-in
+    `_ldscore.calculate(params)` (nldsc/ldscore/_ldscore/ldscore.cpp:17-54 — file read, H2D, every kernel,
+    results back as Python lists) timed from that file, first after the file's pages were dropped from the
+    page cache (fsync + posix_fadvise DONTNEED: read from the device), then again with the file cached."""
+    import tempfile
+    from nldsc_amd.ldscore import _ldscore as lds
+    d = tempfile.mkdtemp(prefix="nldsc_bench_", dir=os.environ.get("TMPDIR", "/tmp"))
+    path = os.path.join(d, "chr1.bed")
+    out = {}
+    try:
+        t = time.perf_counter()
+        with open(path, "wb") as fh:
+            fh.write(bed_host)
+            fh.flush()
+            os.fsync(fh.fileno())
+        write_s = time.perf_counter() - t
+        p = lds.LDScoreParams(path, n_snp=n_snp, n_org=n_org, ld_wind=w, maf=maf, std_thr=std_thr, rsq_thr=rsq,
+                              positions=[float(x) for x in pos])
+        p.flags = flags
+        times = []
+        for drop in (True, False):
+            if drop:
+                fd = os.open(path, os.O_RDONLY)
+                os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+                os.close(fd)
+            t = time.perf_counter()
+            r = lds.calculate(p)
+            times.append(time.perf_counter() - t)
+        ws = np.asarray(r.l2_ws)
+        out["wall_clock_from_file_s"] = times[0]
+        out["wall_clock_from_file"] = {
+            "what": "_ldscore.calculate(LDScoreParams(bedfile, ...)) on the same chromosome, from a %.2f GB .bed on "
+                    "local disk (written in %.1f s): file -> pinned slots -> pitched H2D -> kernels -> result lists"
+                    % (len(bed_host) / 1e9, write_s),
+            "page_cache_dropped_s": times[0], "page_cache_warm_s": times[1],
+            "pairs": int(ws[ws > 0].sum()), "file_gbps_cold": len(bed_host) / times[0] / 1e9}
+    except OSError as ex:
+        out["wall_clock_from_file_s"] = None
+        out["wall_clock_from_file"] = {"error": f"{type(ex).__name__}: {ex}"}
+    finally:
+        try:
+            os.unlink(path)
+            os.rmdir(d)
+        except OSError:
+            pass
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -121,9 +187,14 @@ def main():
                          "whole genome (sum M ~ 600k, BASELINE.json configs[3]) spread over the GPUs by LPT; c5: one "
                          "eighth of the imputed genome per GPU (BASELINE.json configs[4]: M ~ 10M over 2.88 Gb, "
                          "--ld-wind-kb 1000; --n-snp defaults to 1.25M per GPU)")
-    ap.add_argument("--split", action="store_true",
-                    help="c3 with N > 1: split ONE chromosome over the GPUs by position (strong scaling) instead of "
-                         "one chromosome per GPU (weak scaling, the default)")
+    ap.add_argument("--weak", action="store_true",
+                    help="c3 with N > 1: one chromosome per GPU (weak scaling) instead of the default, ONE chromosome "
+                         "position-sharded over the GPUs (strong scaling, what the BASELINE metric reads: chr1 at "
+                         "1/2/4/8 GPUs)")
+    ap.add_argument("--split", action="store_true", help=argparse.SUPPRESS)  # the default since round 2
+    ap.add_argument("--no-file", action="store_true",
+                    help="skip the wall clock from a PLINK file (rank 0, N = 1: the synthetic .bed written to "
+                         "$TMPDIR, then _ldscore.calculate timed from the file)")
     ap.add_argument("--concurrent", type=int, default=3,
                     help="c4: chromosomes computed at once per GPU (host threads, one engine stream each)")
     args = ap.parse_args()
@@ -162,7 +233,7 @@ def main():
     N, M = args.n_org, args.n_snp
     flags = (_lib.FLAG_ADDITIVE_ONLY if args.additive_only else 0) | getattr(_lib, PATHS[args.path][0])
     t = time.perf_counter()
-    split = args.split and world > 1
+    split = world > 1 and not args.weak
     buf, pos = synth.device_bed(M, N, seed=7 if split else 7 + rank, length_cm=args.length_cm,
                                 missing=args.missing, device=local)
     eng = Engine(local)
@@ -183,7 +254,8 @@ def main():
     else:
         eng.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
     bed_host = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    want_file = rank == 0 and world == 1 and not args.no_file and args.workload == "c3"
+    if rank == 0 and world == 1 and (not args.no_cpu or want_file):
         bed_host = buf.cpu().numpy().tobytes()
     del buf
     torch.cuda.empty_cache()
@@ -196,10 +268,13 @@ def main():
         nonlocal out
         if split:  # owned slice of the one chromosome, then the table assembled on rank 0 (RCCL over xGMI)
             out = eng.run(w, args.maf, args.std_thr, rsq, pos, own=own_rel, flags=flags, out=out)
+            tim = eng.timings()
             for k, v in full_local.items():
                 v[own[0]:own[1]] = out[k][own_rel[0]:own_rel[1]]
+            tg = time.perf_counter()
             gather_ranges(full_local, own, M, device=coll)
-            return eng.timings()
+            tim["gather_ms"] = 1e3 * (time.perf_counter() - tg)
+            return tim
         out = eng.run(w, args.maf, args.std_thr, rsq, pos, flags=flags, out=out)
         if world > 1:  # assemble the score tables on rank 0 (RCCL over xGMI)
             tab = torch.from_numpy(np.stack([out["l2"], out["l2d"], out["maf"], out["residuals_std"],
@@ -227,34 +302,50 @@ def main():
         dist.all_reduce(pairs_step, op=dist.ReduceOp.SUM)
     t_max = float(el.item())
     total_pairs = float(pairs_step.item()) * args.steps
+    # per-rank stage times (band kernel, gather, engine total) for the scaling record
+    mine = torch.tensor([float(np.mean([x["band_ms"] for x in tims])),
+                         float(np.mean([x.get("gather_ms", 0.0) for x in tims])),
+                         float(np.mean([x["total_ms"] for x in tims])), float(tims[-1]["pairs"]),
+                         float(own[1] - own[0])], dtype=torch.float64, device=coll)
+    per_rank = [mine]
+    if world > 1:
+        per_rank = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(per_rank, mine)
 
     res = None
     if rank == 0:
         band_ms = float(np.mean([x["band_ms"] for x in tims]))
+        t_band = band_ms * 1e-3
         flop = tims[-1]["flop_alg"]
-        fp32_equiv = flop / (band_ms * 1e-3) / 1e12
         path = tims[-1]["path"]
         _, peak, unit, kname, dtype = PATHS[path]
+        # roofline on SURVEY.md §8(d3)'s basis for every path: FLOP_alg = 2N(1/2 sumWSA + sumWSD) (the reference
+        # formulation's multiply-adds) over the band kernel's time, against the dense MFMA peak of the dtype
+        # that ran.  The exact paths issue more: 8 integer Gram entries per pair (frac_8_product_basis).
+        roof = {"bound": "mfma", "achieved": flop / t_band / 1e12, "peak": peak, "unit": unit, "kernel": kname,
+                "flop_alg_per_launch": flop,
+                "flop_alg_definition": "SURVEY.md §8(d3): 2N(1/2 sumWSA + sumWSD) multiply-adds x2 (additive Gram "
+                                       "once per unordered pair, dominance cross term per ordered pair)"}
+        roof["frac"] = roof["achieved"] / peak
         if path != "f32":
             ops = tims[-1]["ops_alg_i8"]
-            roof = {"bound": "mfma", "achieved": ops / (band_ms * 1e-3) / 1e12, "peak": peak, "unit": unit,
-                    "kernel": kname, "ops_alg_per_launch": ops,
-                    "ops_alg_definition": "2N(4*(1/2)sumWSA + 2*sumWSD): 4 integer dots per unordered additive "
-                                          "pair (xx,xo,ox,oo), 2 per ordered dominance pair (xh,oh)"}
-        else:
-            roof = {"bound": "mfma", "achieved": fp32_equiv, "peak": peak, "unit": unit,
-                    "kernel": kname, "flop_alg_per_launch": flop}
-        traffic, traffic_src = pmc_traffic(kname.split("<")[0], N, M)
-        roof.update(frac=roof["achieved"] / peak, traffic=traffic, traffic_source=traffic_src,
+            roof.update(ops_8_product_per_launch=ops, achieved_8_product_basis=ops / t_band / 1e12,
+                        frac_8_product_basis=ops / t_band / 1e12 / peak,
+                        ops_8_product_definition="2N(4*(1/2)sumWSA + 2*sumWSD): the exact formulation's 8 integer "
+                                                 "Gram entries per pair (vv, vm, mv, mm additive; vh, mh, hv, hm "
+                                                 "dominance), skipped products of missing-free blocks included")
+        traffic, traffic_src = pmc_traffic(kname.split("<")[0], N, M, args.missing)
+        roof.update(traffic=traffic, traffic_source=traffic_src,
                     algorithmic_bytes_per_launch=eng.n_snp * 4 * ((((N + 3) // 4) + 31) // 32 * 8),
                     avg_launch_ms=band_ms,
                     issued_per_launch=tims[-1]["flop_issued"], work_items=tims[-1]["band_items"],
-                    mfma_pipe_frac=tims[-1]["flop_issued"] / (band_ms * 1e-3) / 1e12 / peak,
-                    fp32_formulation_flop_per_launch=flop, fp32_equivalent_tflops=fp32_equiv,
-                    fp32_equivalent_frac_of_fp32_peak=fp32_equiv / FP32_MFMA_PEAK_TFLOPS)
-        achieved = roof["achieved"]
+                    mfma_pipe_frac=tims[-1]["flop_issued"] / t_band / 1e12 / peak,
+                    fp32_equivalent_tflops=flop / t_band / 1e12,
+                    fp32_equivalent_frac_of_fp32_peak=flop / t_band / 1e12 / FP32_MFMA_PEAK_TFLOPS)
         stages = {k: round(float(np.mean([x[k] for x in tims])), 3)
                   for k in ("count_ms", "stats_ms", "schedule_ms", "band_ms", "finalize_ms", "total_ms")}
+        if split:
+            stages["gather_ms"] = round(float(np.mean([x["gather_ms"] for x in tims])), 3)
         ws = out["l2_ws"]
         res = {
             "metric": METRIC,
@@ -283,14 +374,21 @@ def main():
                 "n_org": N, "n_snp": M, "mean_window": float(ws[ws > 0].mean()),
                 "pairs_per_step_per_gpu": tims[-1]["pairs"],
                 "parallelism": (f"one chromosome position-sharded over {world} GPUs (owned SNP ranges balanced by "
-                                f"pair work, one window of halo rows per rank, score table gathered over RCCL)"
+                                f"pair work, one window of halo rows per rank, score table gathered over "
+                                f"{'RCCL' if coll == 'cuda' else 'gloo'})"
                                 if split else f"position sharding, one chromosome unit per GPU x {world}"),
             },
             "roofline": roof,
             "stages_ms": stages,
+            "per_rank": [dict(rank=g, band_ms=round(float(v[0]), 3), gather_ms=round(float(v[1]), 3),
+                              engine_ms=round(float(v[2]), 3), pairs=int(v[3]), owned_snps=int(v[4]))
+                         for g, v in enumerate(x.cpu() for x in per_rank)],
             "cpu_baseline": None,
         }
-    if bed_host is not None:
+    if want_file:
+        log("[rank 0] wall clock from a PLINK file ...")
+        res.update(file_wall_clock(bed_host, M, N, w, args.maf, args.std_thr, rsq, pos, flags))
+    if bed_host is not None and not args.no_cpu:
         log("[rank 0] timing the CPU baseline ...")
         res["cpu_baseline"] = cpu_baseline(bed_host, M, N, w, args.maf, args.std_thr, rsq, pos,
                                            target_s=args.cpu_seconds)

@@ -53,10 +53,11 @@ def main():
               is_flag=True, default=False)
 @click.option("--additive-only", help="Skip the dominance terms (L2D = NaN)", is_flag=True, default=False)
 @click.option("--device", help="HIP device ordinal", type=int, default=None)
+@click.option("--quiet", help="No progress lines on stderr", is_flag=True, default=False)
 @click.option("--display", help="Display traceback", is_flag=True, default=False)
 @handle_exception
 def est_ld(bfile, out, ld_wind_kb, ld_wind_cm, maf_thr, std_thr, rsq_thr, extra, write_m, strict_plink_order,
-           additive_only, device):
+           additive_only, device, quiet):
     if sum(map(bool, [ld_wind_kb, ld_wind_cm])) != 1:
         raise RuntimeError("Please, specify exactly one --ld-wind option")
     elif ld_wind_kb:
@@ -69,10 +70,12 @@ def est_ld(bfile, out, ld_wind_kb, ld_wind_cm, maf_thr, std_thr, rsq_thr, extra,
     if "@" in bfile:  # whole genome: one output per chromosome, chromosomes spread over GPUs
         from .ldscore.genome import estimate_lds_genome
         estimate_lds_genome(bfile, ld_wind=ld_wind, wind_metric=wind_metric, maf_thr=maf_thr, std_thr=std_thr,
-                            rsq_thr=rsq_thr, out=out, extra=extra, write_m=write_m, flags=flags, device=device)
+                            rsq_thr=rsq_thr, out=out, extra=extra, write_m=write_m, flags=flags, device=device,
+                            progress=not quiet)
         return
     estimate_lds(bfile, ld_wind=ld_wind, wind_metric=wind_metric, maf_thr=maf_thr, std_thr=std_thr,
-                 rsq_thr=rsq_thr, out=out, extra=extra, summary=True, write_m=write_m, flags=flags, device=device)
+                 rsq_thr=rsq_thr, out=out, extra=extra, summary=True, write_m=write_m, flags=flags, device=device,
+                 progress=not quiet)
 
 
 @main.command("h2", help="(not part of this engine) heritability estimation")

@@ -53,7 +53,8 @@ def halo_range(positions: np.ndarray, ld_wind: float, own: tuple[int, int]) -> t
     lo, hi = own
     if hi <= lo:
         return lo, lo
-    if n == 0 or (pos < 0).any() or (np.diff(pos) < 0).any():
+    # `not (pos >= 0)` also catches NaN positions, which the reference treats as unused (is_used: pos >= 0)
+    if n == 0 or not (pos >= 0).all() or (np.diff(pos) < 0).any():
         return 0, n
     # a few ulps of slack: the kernels test |pos_k - pos_j| <= w, not pos_k >= pos_j - w (extra rows are harmless)
     eps = 8.0 * np.finfo(np.float64).eps * (float(pos[-1]) + abs(ld_wind))

@@ -89,7 +89,8 @@ def _default_runner(device: int):
 def estimate_lds_genome(bfile: str, ld_wind: float, wind_metric: str, maf_thr: float = 1e-5,
                         std_thr: float = 1e-5, rsq_thr: float | None = None, *, out: str | None = None,
                         extra: bool = False, write_m: bool = False, flags: int = 0, device: int | None = None,
-                        runner=None, rank: int | None = None, world: int | None = None) -> dict:
+                        runner=None, rank: int | None = None, world: int | None = None,
+                        progress: bool | None = None) -> dict:
     """Returns {chromosome: output DataFrame (None when written to `out`)} for the chromosomes this rank
     processed."""
     units = expand_bfile(bfile)
@@ -111,8 +112,17 @@ def estimate_lds_genome(bfile: str, ld_wind: float, wind_metric: str, maf_thr: f
     log.info(f"[rank {rank}/{world}] {len(mine)} of {len(units)} chromosomes: "
              f"{', '.join(meta[u]['chrom'] for u in mine)}")
     if runner is None:
-        local = int(os.environ.get("LOCAL_RANK", "0")) if device is None else int(device)
+        if device is None:  # torchrun: one rank per GPU (ranks beyond the visible GPUs share them round-robin)
+            from .. import _lib
+            local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, _lib.lib().nldsc_device_count())
+        else:
+            local = int(device)
         runner = _default_runner(local)
+    from ..core.progress import Progress
+    total_snp = sum(meta[u]["bim"].n_snp for u in mine)
+    bar = Progress(total_snp, "SNPs", label=f"ld rank {rank}" if world > 1 else "ld", enabled=progress,
+                   any_rank=True)
+    done_snp = 0
     results = {}
     # a path-fed runner (the engine's own reader) gets the next file read ahead into the page cache;
     # other runners get the bytes, read by a host thread while the current chromosome computes
@@ -145,6 +155,9 @@ def estimate_lds_genome(bfile: str, ld_wind: float, wind_metric: str, maf_thr: f
         results[m["chrom"]] = df
         log.info(f"[rank {rank}] chr{m['chrom']}: M={n_snp} N={m['n_org']} "
                  f"in {time.perf_counter() - t0:.2f} s")
+        done_snp += n_snp
+        bar.update(done_snp, f"{k + 1}/{len(mine)} chromosomes, chr{m['chrom']} done")
+    bar.close(f"{len(mine)} chromosomes")
     return results
 
 

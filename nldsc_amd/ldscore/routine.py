@@ -8,6 +8,7 @@ to `out`.  Additions: `write_m` writes the `M`/`MD` file the h2 reader looks for
 """
 from __future__ import annotations
 
+import os
 from pathlib import Path
 
 import numpy as np
@@ -111,38 +112,52 @@ class _Result:
             setattr(self, k, v.tolist())
 
 
+def _backend() -> str:
+    """Collectives backend of the torchrun path: RCCL ("nccl", one GPU per rank) unless $NLDSC_DIST_BACKEND
+    says "gloo" (CPU collectives; ranks may then share GPUs, e.g. a 2-rank rehearsal on one GPU)."""
+    return os.environ.get("NLDSC_DIST_BACKEND", "nccl")
+
+
+def _local_device() -> int:
+    import torch
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return local if _backend() == "nccl" else local % max(1, torch.cuda.device_count())
+
+
 def _process_group():
     """The torch.distributed module when launched by torchrun with WORLD_SIZE > 1, else None."""
-    import os
     if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
         return None
     import torch
     import torch.distributed as dist
     if not dist.is_initialized():
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        dev = _local_device()
+        torch.cuda.set_device(dev)
+        if _backend() == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
+        else:
+            dist.init_process_group(_backend())
     return dist
 
 
 def _calculate_sharded(dist, params):
-    import os
-
     import torch
 
     from .. import distributed as D
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = _local_device()
     pos = np.asarray(params.positions, dtype=np.float64)
     run = D.engine_runner(params.bedfile, params.n_snp, params.n_org, params.ld_wind, params.maf, params.std_thr,
-                          params.rsq_thr, pos, flags=params.flags, device=local)
-    full = D.calculate_sharded(run, pos, params.ld_wind, params.n_snp, device=torch.device(f"cuda:{local}"))
+                          params.rsq_thr, pos, flags=params.flags, device=dev)
+    full = D.calculate_sharded(run, pos, params.ld_wind, params.n_snp,
+                               device=torch.device(f"cuda:{dev}") if _backend() == "nccl" else None)
     return None if full is None else _Result(full)
 
 
 @elapsed_time
 def estimate_lds(bfile: str, ld_wind: float, wind_metric: str, maf_thr: float = 1e-5, std_thr: float = 1e-5,
                  rsq_thr: float | None = None, *, out: str | None = None, extra: bool = False, summary: bool = False,
-                 verbose: int = 0, write_m: bool = False, flags: int = 0, device: int | None = None):
+                 verbose: int = 0, write_m: bool = False, flags: int = 0, device: int | None = None,
+                 progress: bool | None = None):
     bed_, bim_, fam_ = PLINKFile.parse(bfile)
     ld_wind_ = LDWindow(ld_wind, metric=wind_metric)
     maf_thr_ = MAF(maf_thr)
@@ -160,6 +175,9 @@ def estimate_lds(bfile: str, ld_wind: float, wind_metric: str, maf_thr: float = 
     if device is not None:
         params.device = int(device)
     log.info("Running the estimator. It may take a long time.")
+    from ..core.progress import Progress
+    bar = Progress(bim_.n_snp, "SNPs", enabled=progress)
+    bar.update(0, "reading the .bed and computing on the GPU", force=True)
     dist = _process_group()
     if dist is None:
         ld = lds.calculate(params)
@@ -167,6 +185,8 @@ def estimate_lds(bfile: str, ld_wind: float, wind_metric: str, maf_thr: float = 
         ld = _calculate_sharded(dist, params)
         if ld is None:
             return None
+    ws = np.asarray(ld.l2_ws)
+    bar.close(f"{int(ws[ws > 0].sum()):,} SNP pairs")
     log.info("Estimation completed")
 
     if summary:

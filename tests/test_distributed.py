@@ -91,6 +91,8 @@ def test_halo_range_bounds():
     assert D.halo_range(neg, 1.0, (4, 6)) == (0, len(pos))  # unused SNP: the reference's pointers need it all
     uns = pos[::-1].copy()
     assert D.halo_range(uns, 1.0, (4, 6)) == (0, len(pos))
+    nan = pos.copy(); nan[7] = np.nan  # NaN position: unused for the reference (pos >= 0 is false)
+    assert D.halo_range(nan, 1.0, (4, 6)) == (0, len(pos))
 
 
 @pytest.mark.parametrize("world", [2, 3, 5])

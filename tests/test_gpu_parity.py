@@ -176,35 +176,150 @@ def test_random_small_configs_vs_f64(engine, seed, mode):
     assert_ld_close(got, exp, tol=tol, wse_budget=0.02, label=f"seed{seed} N{N} M{M}")
 
 
-@pytest.mark.parametrize("mode", sorted(MODES))
-def test_full_size_spot_check_vs_oracle(engine, mode):
-    """N = 315 599 (N % 4 = 3, BASELINE.json configs[2]) on a 2 000-SNP chromosome slice generated on the
-    GPU: 12 SNPs against the oracle's targets mode, the rest by invariants."""
+def c3_targets(M):
+    """>= 64 SNPs of a full-size slice: both edges of every 32-SNP block in a band of 16 blocks (j mod 32 in
+    {0, 1, 30, 31}: first/last rows and columns of the diagonal blocks and of their neighbours), plus the
+    chromosome ends, where the windows are one-sided."""
+    t = {0, 1, 31, 32, M - 33, M - 2, M - 1}
+    for b in range(20, 36):
+        t.update(32 * b + k for k in (0, 1, 30, 31))
+    return np.array(sorted(x for x in t if 0 <= x < M), np.int32)
+
+
+@pytest.fixture(scope="module")
+def c3_slice(engine):
+    """N = 315 599 (N % 4 = 3, BASELINE.json configs[2]) on a 2 000-SNP chr1-density slice generated on the
+    GPU, with the oracle (fp32, the reference's structure) and the exact fp64 truth at c3_targets."""
     from nldsc_amd import synth
     N, M = 315_599, 2000
     buf, pos = synth.device_bed(M, N, seed=3, length_cm=7.0)
-    engine.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
-    w, maf, std_thr, rsq = 1.0, 1e-4, 1e-5, 1.0 / M
-    got = engine.run(w, maf, std_thr, rsq, pos, flags=MODES[mode])
     bed = buf.cpu().numpy().tobytes()
-    t = np.linspace(0, M - 1, 12).astype(np.int32)
-    exp = O.run_c(bed, M, N, w, maf, std_thr, rsq, pos, targets=t)
-    sub = {k: v[t] for k, v in got.items()}
+    args = (1.0, 1e-4, 1e-5, 1.0 / M)
+    t = c3_targets(M)
+    exp = O.run_c(bed, M, N, *args, pos, targets=t, flags=O.NO_COPIES)
     rows = np.frombuffer(bed, np.uint8, offset=3).reshape(M, -1)
-    truth = O.run_f64_targets(rows, N, w, maf, std_thr, rsq, pos, t)
+    truth = O.run_f64_targets(rows, N, *args, pos, t, bed=bed)
+    yield dict(buf=buf, pos=pos, N=N, M=M, args=args, t=t, exp=exp, truth=truth)
+
+
+@pytest.mark.parametrize("mode", sorted(MODES))
+def test_full_size_block_edges_vs_oracle(engine, c3_slice, mode):
+    """C3 shape at full N: 71 target SNPs (every block edge in a band of 16 blocks, both sides of each
+    diagonal block, the chromosome ends) against the oracle's targets mode and the exact fp64 truth; every
+    other SNP by invariants; integer outputs reproducible run to run."""
+    d = c3_slice
+    buf, pos, N, M, t = d["buf"], d["pos"], d["N"], d["M"], d["t"]
+    engine.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
+    got = engine.run(*d["args"], pos, flags=MODES[mode])
+    sub = {k: v[t] for k, v in got.items()}
+    exp, truth = d["exp"], d["truth"]
     record(f"full_size_{mode}", dict(n_org=N, n_snp=M, targets=t.tolist(), gpu_vs_oracle=max_errors(sub, exp),
-                             gpu_vs_truth=max_errors(sub, truth), oracle_vs_truth=max_errors(exp, truth)))
+                                     gpu_vs_truth=max_errors(sub, truth), oracle_vs_truth=max_errors(exp, truth)))
+    assert len(t) >= 64
     assert_ld_close(sub, truth, label="N=315599 vs fp64 truth")
     if mode in EXACT:
         for k in ("l2", "l2d"):
             assert np.max(np.abs(sub[k] - truth[k])) < 1e-8, k
     assert_ld_close(sub, exp, label="N=315599")
     assert (got["l2_ws"] > 100).all() and np.isfinite(got["l2"]).all()
-    # determinism of the integer outputs and closeness of a second run
-    again = engine.run(w, maf, std_thr, rsq, pos, flags=MODES[mode])
+    again = engine.run(*d["args"], pos, flags=MODES[mode])
     np.testing.assert_array_equal(again["l2_ws"], got["l2_ws"])
     np.testing.assert_array_equal(again["l2d_wse"], got["l2d_wse"])
     np.testing.assert_allclose(again["l2"], got["l2"], rtol=1e-13)
+
+
+@pytest.fixture(scope="module")
+def c5_slice(engine):
+    """C5 shape (BASELINE.json configs[4], imputed genome): N = 315 599, no missing calls (hard calls), bp
+    positions at 288 bp per SNP (2.88 Gb / 10 M SNPs, duplicates from integer rounding), --ld-wind-kb 1000:
+    ~6 900 neighbours per SNP, so the plan's tiled wide-band item order and the missing-free 3-of-8 fp4
+    products run at full N.  12 000 SNPs (3.5 Mb); oracle + fp64 truth at 64 targets."""
+    from nldsc_amd import synth
+    N, M = 315_599, 12_000
+    buf, pos = synth.device_bed(M, N, seed=21, length_cm=288.0 * M, missing=0.0)
+    pos = np.round(pos)
+    bed = buf.cpu().numpy().tobytes()
+    args = (1.0e6, 1e-4, 1e-5, 1.0 / M)
+    t = set()
+    for b in range(180, 192):  # mid-chromosome band, full windows
+        t.update(32 * b + k for k in (0, 1, 30, 31))
+    t.update({0, 1, 31, 32, 3000, 3001, 3039, 3040})    # left end: one-sided windows; within one window of it
+    t.update({M - 1, M - 2, M - 32, M - 33, 9000, 9031, 9032, 9063})
+    for k in range(8):
+        t.add(4000 + 331 * k)                            # interior SNPs at various block offsets
+    t = np.array(sorted(t), np.int32)
+    exp = O.run_c(bed, M, N, *args, pos, targets=t, flags=O.NO_COPIES)
+    rows = np.frombuffer(bed, np.uint8, offset=3).reshape(M, -1)
+    truth = O.run_f64_targets(rows, N, *args, pos, t, bed=bed)
+    yield dict(buf=buf, pos=pos, N=N, M=M, args=args, t=t, exp=exp, truth=truth)
+
+
+@pytest.mark.parametrize("mode", ["f4", "i8", "f32"])
+def test_c5_shape_1000kb_vs_oracle(engine, c5_slice, mode):
+    d = c5_slice
+    buf, pos, N, M, t = d["buf"], d["pos"], d["N"], d["M"], d["t"]
+    engine.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
+    got = engine.run(*d["args"], pos, flags=MODES[mode])
+    tim = engine.timings()
+    sub = {k: v[t] for k, v in got.items()}
+    exp, truth = d["exp"], d["truth"]
+    record(f"c5_shape_{mode}", dict(n_org=N, n_snp=M, targets=t.tolist(), band_items=tim["band_items"],
+                                    mean_window=float(got["l2_ws"].mean()), gpu_vs_oracle=max_errors(sub, exp),
+                                    gpu_vs_truth=max_errors(sub, truth), oracle_vs_truth=max_errors(exp, truth)))
+    assert len(t) >= 64
+    assert got["l2_ws"][M // 2] > 6000  # ~6 900 neighbours mid-chromosome
+    assert_ld_close(sub, truth, label="C5 shape vs fp64 truth")
+    assert_ld_close(sub, exp, label="C5 shape vs oracle")
+    if mode in EXACT:
+        for k in ("l2", "l2d"):
+            assert np.max(np.abs(sub[k] - truth[k])) < 1e-8, k
+        for k in ("l2_ws", "l2d_ws", "l2d_wse"):
+            np.testing.assert_array_equal(sub[k], truth[k], err_msg=k)
+    assert np.isfinite(got["l2"]).all() and (got["l2_ws"] > 2000).all()
+
+
+@pytest.fixture(scope="module")
+def c2_slice(engine):
+    """C2 shape (BASELINE.json configs[1]): N = 50 000 (N % 4 = 0), chr1 SNP density (80 000 SNPs over
+    280 cM: ~570 neighbours at 1 cM), 1 % missing calls, additive scores only.  3 000 SNPs: the whole
+    chromosome slice against the full oracle run, 160 SNPs against the fp64 truth."""
+    from nldsc_amd import synth
+    N, M = 50_000, 3000
+    buf, pos = synth.device_bed(M, N, seed=8, length_cm=280.0 * M / 80_000)
+    bed = buf.cpu().numpy().tobytes()
+    args = (1.0, 1e-4, 1e-5, 1.0 / M)
+    exp = O.run_c(bed, M, N, *args, pos, flags=O.NO_COPIES)
+    t = np.unique(np.concatenate([np.arange(0, M, 32), np.arange(31, M, 32)])[::2]).astype(np.int32)
+    rows = np.frombuffer(bed, np.uint8, offset=3).reshape(M, -1)
+    truth = O.run_f64_targets(rows, N, *args, pos, t, bed=bed)
+    yield dict(buf=buf, pos=pos, N=N, M=M, args=args, t=t, exp=exp, truth=truth)
+
+
+@pytest.mark.parametrize("mode", ["f4", "i8", "f32"])
+def test_c2_shape_additive_only_vs_oracle(engine, c2_slice, mode):
+    from nldsc_amd import _lib
+    d = c2_slice
+    buf, pos, N, M, t = d["buf"], d["pos"], d["N"], d["M"], d["t"]
+    engine.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
+    got = engine.run(*d["args"], pos, flags=MODES[mode] | _lib.FLAG_ADDITIVE_ONLY)
+    exp, truth = d["exp"], d["truth"]
+    record(f"c2_shape_{mode}", dict(n_org=N, n_snp=M, mean_window=float(got["l2_ws"].mean()),
+                                    gpu_vs_oracle=max_errors(got, exp), gpu_vs_truth_targets=max_errors(
+                                        {k: v[t] for k, v in got.items()}, truth)))
+    assert np.isnan(got["l2d"]).all() and (got["l2d_ws"] == -1).all() and (got["l2d_wse"] == -1).all()
+    assert got["l2_ws"].mean() > 450
+    add_only = dict(l2=exp["l2"], maf=exp["maf"], residuals_std=exp["residuals_std"], l2_ws=exp["l2_ws"])
+    for k in ("l2_ws", "maf"):
+        np.testing.assert_array_equal(got[k], add_only[k], err_msg=k)
+    tol = {k: v for k, v in __import__("conftest").TOL.items()}
+    for k in ("l2", "residuals_std"):
+        atol, rtol = tol[k]
+        np.testing.assert_allclose(got[k], add_only[k], rtol=rtol, atol=atol, err_msg=f"{k} vs oracle")
+    sub = {k: v[t] for k, v in got.items()}
+    np.testing.assert_array_equal(sub["l2_ws"], truth["l2_ws"])
+    np.testing.assert_allclose(sub["l2"], truth["l2"], rtol=1e-4, atol=1e-3)
+    if mode in EXACT:
+        assert np.max(np.abs(sub["l2"] - truth["l2"])) < 1e-9
 
 
 def test_f4_gram_is_bitwise_the_int8_gram(engine):

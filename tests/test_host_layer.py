@@ -159,3 +159,41 @@ def test_native_f5_matches_python_formatting():
     exp = ["p\t%.5f\t0.00000" % v for v in x]
     bad = [(v, a, b) for v, a, b in zip(x, lines, exp) if a != b]
     assert not bad, bad[:5]
+
+
+def test_progress_is_throttled_and_quiet():
+    """a13: at most one line per interval plus the final one (the reference ticks stdout once per SNP,
+    ldscalc.h:59); nothing with enabled=False / $NLDSC_QUIET; only RANK 0 unless any_rank."""
+    import io
+
+    from nldsc_amd.core.progress import Progress
+    t = [0.0]
+    buf = io.StringIO()
+    bar = Progress(1000, "SNPs", interval=1.0, enabled=True, stream=buf, clock=lambda: t[0])
+    for k in range(1, 1001):
+        t[0] = k * 0.01            # 10 s in total, 1000 updates
+        bar.update(k)
+    bar.close()
+    lines = buf.getvalue().splitlines()
+    assert 9 <= len(lines) <= 12, lines
+    assert lines[-1].startswith("[ld] 1,000/1,000 SNPs") and "100 SNPs/s" in lines[-1]
+    assert "ETA" in lines[1]
+    quiet = io.StringIO()
+    q = Progress(10, enabled=False, stream=quiet)
+    q.update(5, force=True)
+    q.close()
+    assert quiet.getvalue() == ""
+    import os
+    old = os.environ.get("RANK")
+    os.environ["RANK"] = "3"
+    try:
+        r = io.StringIO()
+        Progress(10, enabled=True, stream=r).close()
+        assert r.getvalue() == ""
+        Progress(10, enabled=True, any_rank=True, stream=r).close()
+        assert r.getvalue() != ""
+    finally:
+        if old is None:
+            os.environ.pop("RANK")
+        else:
+            os.environ["RANK"] = old

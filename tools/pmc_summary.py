@@ -89,7 +89,10 @@ def main():
         if hit is not None and miss is not None:
             k.update(l2_hit=hit, l2_miss=miss, l2_hit_rate=hit / max(hit + miss, 1.0))
         kernels[name] = k
+    import hashlib
+    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "nldsc_amd", "csrc", "ld_kernels.hip")
     json.dump({"workload": args.workload,
+               "kernels_source_sha16": hashlib.sha256(open(src, "rb").read()).hexdigest()[:16],
                "method": "rocprofv3 --pmc <one counter group> --kernel-trace, separate passes for FETCH_SIZE, "
                          "WRITE_SIZE and SQ/GRBM; FETCH_SIZE/WRITE_SIZE in KB; FETCH_SIZE doubled per "
                          "MI355X_MICROARCH.md §HBM (gfx950 reports half of wide streaming reads; calibrated by the "
