@@ -45,6 +45,12 @@ extern "C" {
 #define NLDSC_FLAG_FP32 8u               /* correlations from fp32 standardised values (fp32 MFMA) */
 #define NLDSC_FLAG_EXACT_F4 16u          /* exact integer Gram products on fp4 MFMAs (n_org < 2^27, segmented
                                             above 2^19; larger cohorts fall back to EXACT_I8) */
+#define NLDSC_FLAG_EXACT_RARE 32u        /* rare variants (<= 16 calls in one genotype class): exact standardised
+                                            vectors instead of the default, the reference's fp32 ones replayed
+                                            step for step (encoder.h:124-133, tools.h:54-85) — its rounding is
+                                            not small against a nearly constant vector: the fp32 mean does not
+                                            centre it, and a residual without hom-A1 calls is exactly constant
+                                            (std 0) but rounding noise in the reference, often above --std-thr */
 /* None of EXACT_F4, EXACT_I8, FP32: the engine default, EXACT_F4 ($NLDSC_BAND_MODE = f4 | i8 | f32
  * overrides it). */
 

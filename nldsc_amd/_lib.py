@@ -22,6 +22,7 @@ FLAG_ADDITIVE_ONLY = 2
 FLAG_EXACT_I8 = 4
 FLAG_FP32 = 8
 FLAG_EXACT_F4 = 16
+FLAG_EXACT_RARE = 32
 
 # every symbol include/nldsc_ld.h declares (tests check the library exports all of them)
 EXPORTED = (

@@ -489,6 +489,11 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     HIPCHK(hipEventRecord(e->ev[1], st));
     HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->oriented ? e->flip.p : nullptr, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->cst.p,
                                    e->sflags.p, e->maf.p, e->rstd.p, st));
+    // rare variants: the reference's fp32 residual replayed (its sums assume N < 2^23)
+    if (N < (1 << 23) && !(p->flags & NLDSC_FLAG_EXACT_RARE))
+        HIPCHK(nldsc::launch_reference_residuals(e->bed.p, row_bytes, N, strict, e->counts.p,
+                                                 e->oriented ? e->flip.p : nullptr, M, p->std_thr, e->cst.p, e->lut.p,
+                                                 e->sflags.p, e->rstd.p, st));
     HIPCHK(hipEventRecord(e->ev[2], st));
 
     // ---- window replay + schedule ----

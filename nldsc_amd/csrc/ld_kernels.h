@@ -7,12 +7,17 @@ namespace nldsc {
 
 // Per-SNP constants of the exact-integer path: with x = additive count, h = [genotype >= 1],
 // o = [observed] (all 0 for missing calls and padding), the reference's standardised vectors are
-// A = (x - mu o) / sa and R = (2h - beta x - c o) / s.
+// A = (x - mu o) / sa + ka and R = (2h - beta x - c o) / s + kr over the individuals.  ka = kr = 0 except for
+// rare variants whose vectors are replayed in the reference's fp32 arithmetic (reference_residual_kernel:
+// the fp32 mean of a nearly constant vector does not centre it, and missing calls take the value of the
+// fp32 mean, not 0).
 // X, H, Ob: sums of x, h, o over the SNP's sample slots (the fp4 path's Gram uses the missing
-// indicator m = 1 - o over all slots, so o-products are recovered as X - x.m, Ob_i + Ob_j - K + m.m, ...).
+// indicator m = 1 - o over all slots, so o-products are recovered as X - x.m, Ob_i + Ob_j - K + m.m, ...);
+// SA, SR: sums of (x - mu o) / sa and (2h - beta x - c o) / s over the individuals (for the ka / kr terms).
 struct SnpConst {
     double mu, sa, c, beta, s;
     double X, H, Ob;
+    double ka, kr, SA, SR;
 };
 
 // resident rows: after a load, save each row's last byte and fill the pitch padding (rows >= n_snp all 0x55)
@@ -27,6 +32,13 @@ hipError_t launch_count_rows(uint8_t* img, const uint8_t* last, int n_snp, int n
 hipError_t launch_snp_stats(const int* counts, const uint8_t* flip, const double* pos, int n_snp, int n_snp_pad,
                             int n_org, double maf_thr, double std_thr, float2* lut, SnpConst* cst, uint8_t* sflags,
                             double* maf_out, double* rstd_out, hipStream_t st);
+// SNPs with at most REF_RESIDUAL_MIN_CLASS calls in one genotype class (rare variants: residual nearly degenerate):
+// residual std, residual-pass flag bit 2, exact constants and fp32 table of the reference's fp32 residual,
+// replayed in its arithmetic (ld_kernels.hip reference_residual_kernel)
+constexpr int REF_RESIDUAL_MIN_CLASS = 16;
+hipError_t launch_reference_residuals(const uint8_t* img, int row_bytes, int n_org, bool strict, const int* counts,
+                                     const uint8_t* flip, int n_snp, double std_thr, SnpConst* cst, float2* lut,
+                                     uint8_t* sflags, double* rstd_out, hipStream_t st);
 // after a load: swap 00 <-> 11 in rows (and saved last bytes) with more hom-A2 than hom-A1 calls; flip[j] = 1
 hipError_t launch_orient_rows(uint8_t* img, uint8_t* last, int n_snp, int row_bytes, uint8_t* flip, hipStream_t st);
 // exact left pointers L from the all-pass replay's A and the device MAF flags (sorted positions)

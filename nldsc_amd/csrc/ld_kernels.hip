@@ -208,7 +208,7 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const uint8_t* 
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_snp_pad) return;
     float2 L[4] = {make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
-    SnpConst K = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    SnpConst K = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     uint8_t fl = 0;
     double sX = 0.0, sH = 0.0, sOb = 0.0;
     if (j < n_snp) {
@@ -234,7 +234,7 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const uint8_t* 
                     // every call missing: the reference's vectors are all NaN (MAF NaN passes the
                     // filter); they poison every window containing this SNP.
                     for (int c = 0; c < 4; ++c) L[c] = make_float2(qnan, 0.f);
-                    K = SnpConst{qnan, qnan, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+                    K = SnpConst{qnan, qnan, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
                 } else {
                     const Coding f = coding_moments(c0, c1, c2, N);
                     rstd_d = f.rstd;
@@ -251,7 +251,7 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const uint8_t* 
                     L[3] = make_float2(ic, rc);   // stored code 11
                     // exact path: A = (x - mu o) / sa,  R = (2h - beta x - c o) / s   (x, h, o integer)
                     K = SnpConst{m.abar, m.sd_a, rpass ? m.dbar - m.beta * m.abar : 0.0, rpass ? m.beta : 0.0,
-                                 rpass ? m.rstd : 0.0, 0.0, 0.0, 0.0};
+                                 rpass ? m.rstd : 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
                 }
             }
         }
@@ -261,8 +261,276 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const uint8_t* 
     }
     for (int c = 0; c < 4; ++c) lut[(size_t)j * 4 + c] = L[c];
     K.X = sX; K.H = sH; K.Ob = sOb;
+    K.SA = K.sa != 0.0 ? (sX - K.mu * sOb) / K.sa : 0.0;  // ~0: exactly centred
+    K.SR = K.s != 0.0 ? (2.0 * sH - K.beta * sX - K.c * sOb) / K.s : 0.0;
     cst[j] = K;
     sflags[j] = fl;
+}
+
+// ------------------------------------------------------------------------------------------
+// 2b. the reference's residual of nearly degenerate SNPs, in its own fp32 arithmetic
+// ------------------------------------------------------------------------------------------
+// SNPs with a nearly empty genotype class (rare variants; at most REF_RESIDUAL_MIN_CLASS calls in one class) have
+// a residual close to degenerate, where the reference's fp32 rounding is not small against it: at N = 315 599
+// its residual std is off the exact one by up to ~1e-2 relative for SNPs with <= 7 calls in a class (the
+// oracle: tests/test_oracle.py), and its residual vector carries a noise component along the additive one.
+// The extreme case: a SNP whose read samples hold het and hom-A2 calls but no hom-A1 call has a constant dominance coding
+// (2 for every observed call, and 2 imputed for missing ones), so its regression residual is exactly
+// constant and the closed form above reports std 0.  The reference computes that residual in fp32
+// (encoder.h:124-133, tools.h:54-85): slope = (x.y/n - x_mean y_mean) / (x.x/n - x_mean^2) from fp32 sums in
+// two different orders (arma::mean: two interleaved accumulators; BLAS sdot: 64 lanes), so the slope is not
+// exactly 0 and the residual 2 - slope x has a rounding-noise std that mostly exceeds --std-thr (all 96 of
+// such SNPs at N = 50 000, std-thr 1e-5: tests/test_oracle.py) — the reference then counts the SNP in its
+// neighbours' WSD and L2D with that noise vector, which is +-its additive vector.  These SNPs are rare
+// variants with A1 the minor allele (PLINK's default) and only exist when every sample slot the reference
+// reads is an individual (N % 4 == 0, or the strict PLINK order): for N % 4 != 0 it reads a padding
+// hom-A1 call in every row.  This kernel replays that arithmetic step for step, in the sample order the
+// reference reads, with the oracle's model of the third-party sums (oracle/ldscore_oracle.c: arma::mean,
+// OpenBLAS 0.3.28's SkylakeX sdot, g++'s FMA contraction of `dot/n - x_mean*y_mean` and `y - slope*x`): the
+// residual takes one fp32 value per genotype code, which enter the exact epilogue as R = (2h - beta x - c o) / s
+// and the fp32 path's lookup table.  One wave per SNP; SNPs of any other kind return at once.
+// Every operation is an explicit correctly rounded one and contraction is off: hipcc would otherwise fuse a*b+c.
+
+// a value per 2-bit code, selected in registers (indexing a private array would go through scratch memory)
+struct Vals4 {
+    float v0, v1, v2, v3;
+    __device__ __forceinline__ float operator()(int c) const { return c == 0 ? v0 : c == 1 ? v1 : c == 2 ? v2 : v3; }
+};
+
+// The row goes through LDS in chunks of REF_CHUNK bytes (4 REF_CHUNK samples, a multiple of 64): every lane loads
+// its share of the next chunk into registers before the current one is processed, so the loads hide behind the
+// sequential sums.
+constexpr int REF_CHUNK = 2048;
+
+struct RefPass {
+    // per pass: up to two sdots (all lanes: lane L takes samples t = L mod 64 below n64) and two means (lanes 0-1:
+    // the even / odd accumulators of the first, lanes 2-3 of the second)
+    Vals4 dx, dy, du, dv, mv, mw;
+    bool two_dots, two_means, means;
+};
+
+// One pass over the n samples of `row` in the reference's order; codes are read as stored (values are given per
+// stored code, the file's coding folded in).  Returns the lane's sdot accumulators (x.y, u.v) and, on lanes 0-3,
+// its mean accumulator.
+__device__ void ref_pass(const uint8_t* row, int n, int row_bytes, bool strict, const RefPass& P, uint32_t* buf,
+                         float2* tab, float& acc_d, float& acc_e, float& acc_m) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63;
+    // the mean lanes read, per byte, the values of their two samples in it (tab[m][byte], m = lane: 0 / 1 the
+    // even / odd samples of the first mean, 2 / 3 of the second)
+    if (P.means) {
+        __syncthreads();
+        for (int e = lane; e < 4 * 256; e += 64) {
+            const int m = e >> 8, byte = e & 255, k0 = m & 1;
+            const Vals4 V = m < 2 ? P.mv : P.mw;
+            const int sa = strict ? 2 * k0 : 6 - 2 * k0, sb = strict ? 2 * (k0 + 2) : 6 - 2 * (k0 + 2);
+            tab[e] = make_float2(V((byte >> sa) & 3), V((byte >> sb) & 3));
+        }
+    }
+    const int n64 = (n & -32) & ~63;
+    const int n_bytes = (n + 3) >> 2;
+    const uint4* src = reinterpret_cast<const uint4*>(row);
+    const int n_vec = row_bytes >> 4;  // 16-byte vectors in the row (never read past it)
+    constexpr int PER = REF_CHUNK / 16 / 64;  // 16-byte vectors per lane per chunk
+    uint4 nxt[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) nxt[u] = (u * 64 + lane < n_vec) ? src[u * 64 + lane] : make_uint4(0, 0, 0, 0);
+    const int par = lane & 1;
+    const Vals4 M = lane < 2 ? P.mv : P.mw;  // the tail samples
+    const bool my_mean = P.means && (lane < 2 || (P.two_means && lane < 4));
+    for (int b0 = 0; b0 < n_bytes; b0 += REF_CHUNK) {
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < PER; ++u) reinterpret_cast<uint4*>(buf)[u * 64 + lane] = nxt[u];
+        __syncthreads();
+        const int b1 = b0 + REF_CHUNK;
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int v = (b1 >> 4) + u * 64 + lane;
+            nxt[u] = (b1 < n_bytes && v < n_vec) ? src[v] : make_uint4(0, 0, 0, 0);
+        }
+        const uint8_t* bb = reinterpret_cast<const uint8_t*>(buf);
+        // sdots: sample t = 4 b0 + 64 s + lane, byte 16 s + lane / 4
+        const int sh_l = strict ? 2 * (lane & 3) : 6 - 2 * (lane & 3);
+        const int s_end = min(REF_CHUNK / 16, (n64 - 4 * b0 + 63 - lane) / 64);
+        for (int s = 0; s < s_end; ++s) {
+            const int c = (bb[16 * s + (lane >> 2)] >> sh_l) & 3;
+            acc_d = __fmaf_rn(P.dx(c), P.dy(c), acc_d);
+            if (P.two_dots) acc_e = __fmaf_rn(P.du(c), P.dv(c), acc_e);
+        }
+        // means: lane 0 / 2 the even samples, 1 / 3 the odd ones, in order
+        if (my_mean) {
+            const int t_end = min(4 * REF_CHUNK, n - 4 * b0);  // samples of this chunk
+            const int n_full = t_end >> 4;                    // whole 16-sample words
+            const uint32_t* bw = buf;
+            const float2* T = tab + 256 * lane;
+#pragma unroll 2
+            for (int q = 0; q < n_full; ++q) {
+                const uint32_t x = bw[q];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {  // byte b: samples 16 q + 4 b + par, then + 2
+                    const float2 v = T[(x >> (8 * b)) & 0xFFu];
+                    acc_m = acc_m + v.x;
+                    acc_m = acc_m + v.y;
+                }
+            }
+            for (int t = 16 * n_full + par; t < t_end; t += 2) {
+                const int shift = strict ? 2 * (t & 3) : 6 - 2 * (t & 3);
+                acc_m = acc_m + M((bb[t >> 2] >> shift) & 3);
+            }
+        }
+    }
+}
+
+// the lanes' sdot accumulators -> arma::dot (oracle/ldscore_oracle.c dot_f): lanes folded (k, k + 8), one
+// 32-sample FMA step if n1 % 64 = 32, summed, then the tail in double.  n <= 32: Armadillo's two FMA
+// accumulators.  On every lane.
+__device__ float ref_dot_finish(const uint8_t* row, int n, bool strict, float acc, Vals4 X, Vals4 Y, float* sh) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63;
+    auto code = [&](int t) { return (row[t >> 2] >> (strict ? 2 * (t & 3) : 6 - 2 * (t & 3))) & 3; };
+    __syncthreads();
+    sh[lane] = acc;
+    __syncthreads();
+    if (lane == 0) {
+        if (n <= 32) {
+            float a = 0.f, b = 0.f;
+            int t = 0;
+            for (; t + 1 < n; t += 2) {
+                const int c0 = code(t), c1 = code(t + 1);
+                a = __fmaf_rn(X(c0), Y(c0), a);
+                b = __fmaf_rn(X(c1), Y(c1), b);
+            }
+            if (t < n) { const int c0 = code(t); a = __fmaf_rn(X(c0), Y(c0), a); }
+            sh[64] = a + b;
+        } else {
+            const int n1 = n & -32, n64 = n1 & ~63;
+            float b[4][8];
+            for (int q = 0; q < 4; ++q)
+                for (int k = 0; k < 8; ++k) b[q][k] = sh[16 * q + k] + sh[16 * q + k + 8];
+            if (n1 > n64)
+                for (int q = 0; q < 4; ++q)
+                    for (int k = 0; k < 8; ++k) {
+                        const int c = code(n64 + 8 * q + k);
+                        b[q][k] = __fmaf_rn(X(c), Y(c), b[q][k]);
+                    }
+            float cc[8], h[4];
+            for (int k = 0; k < 8; ++k) cc[k] = ((b[0][k] + b[1][k]) + b[2][k]) + b[3][k];
+            for (int k = 0; k < 4; ++k) h[k] = cc[k] + cc[k + 4];
+            double d = (double)((h[0] + h[1]) + (h[2] + h[3]));
+            for (int t = n1; t < n; ++t) {
+                const int c = code(t);
+                d = d + (double)(X(c) * Y(c));
+            }
+            sh[64] = (float)d;
+        }
+    }
+    __syncthreads();
+    return sh[64];
+}
+
+// lanes 0 / 1 (or 2 / 3) accumulators -> arma::mean = (a + b) / n, on every lane
+__device__ float ref_mean_finish(int n, float acc, int first, float* sh) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63;
+    __syncthreads();
+    if (lane < 4) sh[lane] = acc;
+    __syncthreads();
+    return (sh[first] + sh[first + 1]) / (float)n;
+}
+
+__global__ void __launch_bounds__(64) reference_residual_kernel(const uint8_t* __restrict__ img, int row_bytes,
+                                                                int n_org, int strict, const int* __restrict__ counts,
+                                                                const uint8_t* __restrict__ flip, int n_snp,
+                                                                double std_thr, SnpConst* __restrict__ cst,
+                                                                float2* __restrict__ lut, uint8_t* __restrict__ sflags,
+                                                                double* __restrict__ rstd_out) {
+#pragma clang fp contract(off)
+    const int j = blockIdx.x;
+    if (j >= n_snp || !(sflags[j] & 1)) return;  // MAF-failed or unused: no residual
+    const int s0 = counts[4 * (size_t)j], c1 = counts[4 * (size_t)j + 1], s2 = counts[4 * (size_t)j + 2];
+    const bool fj = flip != nullptr && flip[j];
+    const int c0 = fj ? s2 : s0, c2 = fj ? s0 : s2;
+    if (c0 + c1 + c2 == 0 || min(c0, min(c1, c2)) > REF_RESIDUAL_MIN_CLASS) return;
+    __shared__ uint32_t buf[REF_CHUNK / 4];
+    __shared__ float2 tab[4 * 256];
+    __shared__ float sh[72];
+    const uint8_t* row = img + (size_t)j * (size_t)row_bytes;
+    const bool st = strict != 0;
+    const double nn = (double)n_org, n_obs = (double)(c0 + c1 + c2);
+    // per STORED code (00, 01, 10, 11): the file's code is 3, 1, 2, 0 when the row is stored flipped
+    auto stored = [&](float hom1, float miss, float het, float hom2) {
+        return fj ? Vals4{hom2, miss, het, hom1} : Vals4{hom1, miss, het, hom2};
+    };
+    // decode (encoder.h:95-129): fp64 sums of integers, means cast to fp32 impute the missing calls
+    const float mua = (float)(((double)c1 + 2.0 * (double)c2) / n_obs);
+    const float mud = (float)(2.0 * ((double)c1 + (double)c2) / n_obs);
+    const Vals4 X = stored(0.f, mua, 1.f, 2.f), Y = stored(0.f, mud, 2.f, 2.f);
+    // pass 1: arma::mean of x and y, x.y and x.x (Math::regression_residuals, tools.h:54-68)
+    float d1 = 0.f, e1 = 0.f, m1 = 0.f;
+    ref_pass(row, n_org, row_bytes, st, RefPass{X, Y, X, X, X, Y, true, true, true}, buf, tab, d1, e1, m1);
+    const float x_mean_f = ref_mean_finish(n_org, m1, 0, sh);
+    const double x_mean = (double)x_mean_f, y_mean = (double)ref_mean_finish(n_org, m1, 2, sh);
+    const double dxy = (double)ref_dot_finish(row, n_org, st, d1, X, Y, sh);
+    const double dxx = (double)ref_dot_finish(row, n_org, st, e1, X, X, sh);
+    // g++'s FMA contractions of `dot/n - x_mean*y_mean` and `y - slope * x`
+    const double slope = __fma_rn(-x_mean, y_mean, dxy / nn) / __fma_rn(-x_mean, x_mean, dxx / nn);
+    const float k = (float)slope;
+    const Vals4 R = {__fmaf_rn(-X.v0, k, Y.v0), __fmaf_rn(-X.v1, k, Y.v1), __fmaf_rn(-X.v2, k, Y.v2),
+                     __fmaf_rn(-X.v3, k, Y.v3)};
+    // Math::standardise (tools.h:70-85): mean, centre, var_ = sdot * (1 / n), sqrt, divide — of the additive
+    // vector (encoder.h:130-132; its mean is x_mean) and of the residual
+    const Vals4 CA = {X.v0 - x_mean_f, X.v1 - x_mean_f, X.v2 - x_mean_f, X.v3 - x_mean_f};
+    float d2 = 0.f, e2 = 0.f, m2 = 0.f;  // pass 2: mean of the residual, (x - x_mean).(x - x_mean)
+    ref_pass(row, n_org, row_bytes, st, RefPass{CA, CA, CA, CA, R, R, false, false, true}, buf, tab, d2, e2, m2);
+    const float m = ref_mean_finish(n_org, m2, 0, sh);
+    const float var_a = (float)((double)ref_dot_finish(row, n_org, st, d2, CA, CA, sh) * (1.0 / nn));
+    const Vals4 C = {R.v0 - m, R.v1 - m, R.v2 - m, R.v3 - m};
+    float d3 = 0.f, e3 = 0.f, m3 = 0.f;  // pass 3: (r - m).(r - m)
+    ref_pass(row, n_org, row_bytes, st, RefPass{C, C, C, C, C, C, false, false, false}, buf, tab, d3, e3, m3);
+    const float var = (float)((double)ref_dot_finish(row, n_org, st, d3, C, C, sh) * (1.0 / nn));
+    const float sd = (float)sqrt((double)var);  // = correctly rounded sqrtf (__fsqrt_rn is the native 1-ulp one)
+    const float sd_a = (float)sqrt((double)var_a);
+    if ((threadIdx.x & 63) != 0) return;
+    rstd_out[j] = (double)sd;
+    SnpConst K = cst[j];
+    float2* L = lut + (size_t)j * 4;
+    // stored codes 00, 10, 11 (slots 0, 2, 3 of the tables) and their call counts; missing is slot 1
+    const int sc[3] = {0, 2, 3};
+    const int ns[3] = {s0, c1, s2};
+    // A = (x - mu o) / sa + ka: ka = the missing calls' value, then a line in x through the two stored codes
+    // with the most calls (the third, with <= REF_RESIDUAL_MIN_CLASS calls, is off it by rounding noise)
+    double a[3];
+    const double ka = (double)(CA(1) / sd_a);
+    for (int q = 0; q < 3; ++q) a[q] = (double)(CA(sc[q]) / sd_a) - ka;
+    const int drop = (ns[0] <= ns[1] && ns[0] <= ns[2]) ? 0 : (ns[1] <= ns[2] ? 1 : 2);
+    const double u = drop == 0 ? a[2] - a[1] : drop == 1 ? 0.5 * (a[2] - a[0]) : a[1] - a[0];  // 1 / sa
+    const double w = drop == 0 ? u - a[1] : -a[0];                                               // mu / sa
+    K.sa = 1.0 / u;
+    K.mu = w / u;
+    K.ka = ka;
+    K.SA = (K.X - K.mu * K.Ob) / K.sa;
+    for (int c = 0; c < 4; ++c) L[c].x = CA(c) / sd_a;
+    if (!((double)sd > std_thr)) {  // SNPFilter::residuals_std: excluded (also NaN: a constant additive coding)
+        sflags[j] &= (uint8_t)~2u;
+        K.c = K.beta = K.s = K.kr = K.SR = 0.0;
+        for (int c = 0; c < 4; ++c) L[c].y = 0.f;
+        cst[j] = K;
+        return;
+    }
+    sflags[j] |= 2;
+    // R = (2h - beta x - c o) / s + kr: exact on all four codes (the second difference 2 r10 - r00 - r11 is
+    // 2 / sd before standardising, never 0)
+    double r[3];
+    const double kr = (double)(C(1) / sd);
+    for (int q = 0; q < 3; ++q) r[q] = (double)(C(sc[q]) / sd) - kr;
+    K.s = 2.0 / (2.0 * r[1] - r[0] - r[2]);
+    K.beta = -(r[2] - r[1]) * K.s;
+    K.c = -r[0] * K.s;
+    K.kr = kr;
+    K.SR = (2.0 * K.H - K.beta * K.X - K.c * K.Ob) / K.s;
+    for (int c = 0; c < 4; ++c) L[c].y = C(c) / sd;
+    cst[j] = K;
 }
 
 // Exact left pointer of ChunkwiseReader (stream.h:182-197) for positions sorted over the used SNPs,
@@ -558,6 +826,7 @@ __device__ __forceinline__ void band_body(BandLds& sh, const int4 it, const uint
     }
 
     // ---- fused epilogue: r2adj, window / MAF / residual masks, per-SNP sums ------------------
+    const double n_pad = 16.0 * (double)pitch_words - n_org;
 #pragma unroll
     for (int b = 0; b < NC; ++b) {
         const int sj = 32 + 32 * b + i;
@@ -576,17 +845,20 @@ __device__ __forceinline__ void band_body(BandLds& sh, const int4 it, const uint
             // i in N(j): only for off-diagonal blocks (a diagonal block holds both orders)
             const bool nji = !diag && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
             if (nij || nji) {
-                const double r2 = r2_adjusted((double)haa[b][r], n_org);
+                // the n_pad non-individual slots hold code 01 (missing): remove their products (non-zero only
+                // for the replayed rare variants, whose missing calls are not centred at 0)
+                const float2 mi = tab[1][si], mj = tab[1][sj];
+                const double r2 = r2_adjusted((double)haa[b][r] - n_pad * mi.x * mj.x, n_org);
                 if (nij) { atomicAdd(&s_l2[si], r2); atomicAdd(&s_wsa[si], 1); }
                 if (nji) { atomicAdd(&s_l2[sj], r2); atomicAdd(&s_wsa[sj], 1); }
                 if (DOM) {
                     if (nij && rpj) {  // a_i . r_j -> L2D_i (ldscalc.h:40-46)
-                        const double rd = r2_adjusted((double)har[b][r], n_org);
+                        const double rd = r2_adjusted((double)har[b][r] - n_pad * mi.x * mj.y, n_org);
                         atomicAdd(&s_l2d[si], rd); atomicAdd(&s_wsd[si], 1);
                         if (rd > rsq_thr) atomicAdd(&s_wse[si], 1);
                     }
                     if (nji && rpi) {  // r_i . a_j -> L2D_j
-                        const double rd = r2_adjusted((double)hra[b][r], n_org);
+                        const double rd = r2_adjusted((double)hra[b][r] - n_pad * mi.y * mj.x, n_org);
                         atomicAdd(&s_l2d[sj], rd); atomicAdd(&s_wsd[sj], 1);
                         if (rd > rsq_thr) atomicAdd(&s_wse[sj], 1);
                     }
@@ -701,7 +973,8 @@ __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpCons
             const double xo = MB ? ki.X - 0.5 * ((double)gxo[r] - mm) : (double)gxo[r];
             const double ox = MB ? kj.X - 0.5 * ((double)gox[r] - mm) : (double)gox[r];
             const double oo = MB ? ki.Ob + kj.Ob - kslots + mm : mm;
-            const double aa = (xx - kj.mu * xo - ki.mu * (ox - kj.mu * oo)) / (ki.sa * kj.sa);
+            const double aa = (xx - kj.mu * xo - ki.mu * (ox - kj.mu * oo)) / (ki.sa * kj.sa) + kj.ka * ki.SA +
+                              ki.ka * (kj.SA + kj.ka * n_org);
             const double r2 = r2_adjusted(aa, n_org);
             if (nij) { atomicAdd(&s_l2[si], r2); atomicAdd(&s_wsa[si], 1); }
             if (nji) { atomicAdd(&s_l2[sj], r2); atomicAdd(&s_wsa[sj], 1); }
@@ -710,7 +983,8 @@ __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpCons
                     const double xh = MB ? 0.5 * ((double)gxh[r] - (double)goh[r]) : (double)gxh[r];
                     const double oh = MB ? kj.H - (double)goh[r] : (double)goh[r];
                     const double ar = (2.0 * xh - kj.beta * xx - kj.c * xo -
-                                       ki.mu * (2.0 * oh - kj.beta * ox - kj.c * oo)) / (ki.sa * kj.s);
+                                       ki.mu * (2.0 * oh - kj.beta * ox - kj.c * oo)) / (ki.sa * kj.s) +
+                                      kj.kr * ki.SA + ki.ka * (kj.SR + kj.kr * n_org);
                     const double rd = r2_adjusted(ar, n_org);
                     atomicAdd(&s_l2d[si], rd); atomicAdd(&s_wsd[si], 1);
                     if (rd > rsq_thr) atomicAdd(&s_wse[si], 1);
@@ -719,7 +993,8 @@ __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpCons
                     const double hx = MB ? 0.5 * ((double)ghx[r] - (double)gho[r]) : (double)ghx[r];
                     const double ho = MB ? ki.H - (double)gho[r] : (double)gho[r];
                     const double ra = (2.0 * hx - ki.beta * xx - ki.c * ox -
-                                       kj.mu * (2.0 * ho - ki.beta * xo - ki.c * oo)) / (ki.s * kj.sa);
+                                       kj.mu * (2.0 * ho - ki.beta * xo - ki.c * oo)) / (ki.s * kj.sa) +
+                                      ki.kr * kj.SA + kj.ka * (ki.SR + ki.kr * n_org);
                     const double rd = r2_adjusted(ra, n_org);
                     atomicAdd(&s_l2d[sj], rd); atomicAdd(&s_wsd[sj], 1);
                     if (rd > rsq_thr) atomicAdd(&s_wse[sj], 1);
@@ -1268,6 +1543,15 @@ hipError_t launch_snp_stats(const int* counts, const uint8_t* flip, const double
     const int blocks = (n_snp_pad + 255) / 256;
     hipLaunchKernelGGL(snp_stats_kernel, dim3(blocks), dim3(256), 0, st, counts, flip, pos, n_snp, n_snp_pad, n_org,
                        maf_thr, std_thr, lut, cst, sflags, maf_out, rstd_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_reference_residuals(const uint8_t* img, int row_bytes, int n_org, bool strict, const int* counts,
+                                     const uint8_t* flip, int n_snp, double std_thr, SnpConst* cst, float2* lut,
+                                     uint8_t* sflags, double* rstd_out, hipStream_t st) {
+    if (n_snp <= 0) return hipSuccess;
+    hipLaunchKernelGGL(reference_residual_kernel, dim3(n_snp), dim3(64), 0, st, img, row_bytes, n_org, (int)strict,
+                       counts, flip, n_snp, std_thr, cst, lut, sflags, rstd_out);
     return hipGetLastError();
 }
 

@@ -131,4 +131,5 @@ PYBIND11_MODULE(_ldscore, m) {
     m.attr("FLAG_EXACT_I8") = NLDSC_FLAG_EXACT_I8;
     m.attr("FLAG_FP32") = NLDSC_FLAG_FP32;
     m.attr("FLAG_EXACT_F4") = NLDSC_FLAG_EXACT_F4;
+    m.attr("FLAG_EXACT_RARE") = NLDSC_FLAG_EXACT_RARE;
 }

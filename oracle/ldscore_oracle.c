@@ -25,6 +25,7 @@
  * the x86-64 OpenBLAS sdot kernels); neither has a pinned version in the
  * reference (CMakeLists.txt:22-27).
  */
+#include <immintrin.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -80,30 +81,28 @@ static float mean_f(const float* x, int n) {
  * last 32 when n1 % 64 = 32, the four summed left to right, 128-bit halves added and two horizontal adds;
  * the remaining n - n1 products (fp32) are added to that sum in double and the result is rounded to float. */
 static float sdot_kernel(const float* x, const float* y, int n1) {
-    float a[4][16];
-    memset(a, 0, sizeof a);
+    __m256 a[8]; /* accumulator q = lanes 0-7 in a[2q], lanes 8-15 in a[2q+1] */
+    for (int k = 0; k < 8; ++k) a[k] = _mm256_setzero_ps();
     int i = 0;
     for (; i + 64 <= n1; i += 64)
-        for (int q = 0; q < 4; ++q)
-            for (int k = 0; k < 16; ++k) a[q][k] = fmaf(x[i + 16 * q + k], y[i + 16 * q + k], a[q][k]);
-    float b[4][8];
-    for (int q = 0; q < 4; ++q)
-        for (int k = 0; k < 8; ++k) b[q][k] = a[q][k] + a[q][k + 8];
+        for (int k = 0; k < 8; ++k) a[k] = _mm256_fmadd_ps(_mm256_loadu_ps(x + i + 8 * k), _mm256_loadu_ps(y + i + 8 * k), a[k]);
+    __m256 b[4];
+    for (int q = 0; q < 4; ++q) b[q] = _mm256_add_ps(a[2 * q], a[2 * q + 1]);
     for (; i < n1; i += 32)
-        for (int q = 0; q < 4; ++q)
-            for (int k = 0; k < 8; ++k) b[q][k] = fmaf(x[i + 8 * q + k], y[i + 8 * q + k], b[q][k]);
-    float c[8], h[4];
-    for (int k = 0; k < 8; ++k) c[k] = ((b[0][k] + b[1][k]) + b[2][k]) + b[3][k];
+        for (int q = 0; q < 4; ++q) b[q] = _mm256_fmadd_ps(_mm256_loadu_ps(x + i + 8 * q), _mm256_loadu_ps(y + i + 8 * q), b[q]);
+    float c[8];
+    _mm256_storeu_ps(c, _mm256_add_ps(_mm256_add_ps(_mm256_add_ps(b[0], b[1]), b[2]), b[3]));
+    float h[4];
     for (int k = 0; k < 4; ++k) h[k] = c[k] + c[k + 4];
     return (h[0] + h[1]) + (h[2] + h[3]);
 }
 
 static float dot_f(const float* x, const float* y, int n) {
-    if (n <= 32) {
+    if (n <= 32) { /* op_dot::direct_dot_arma; g++ contracts `val += A[i] * B[i]` into an FMA (see below) */
         float a = 0.f, b = 0.f;
         int i = 0;
-        for (; i + 1 < n; i += 2) { a += x[i] * y[i]; b += x[i + 1] * y[i + 1]; }
-        if (i < n) a += x[i] * y[i];
+        for (; i + 1 < n; i += 2) { a = fmaf(x[i], y[i], a); b = fmaf(x[i + 1], y[i + 1], b); }
+        if (i < n) a = fmaf(x[i], y[i], a);
         return a + b;
     }
     const int n1 = n & -32;
@@ -188,10 +187,14 @@ static int decode_snp(const uint8_t* codes, int n, double maf_thr, snp_t* s) {
     /* regression_residuals(x = add, y = nadd) */
     double x_mean = mean_f(add, n), y_mean = mean_f(nadd, n);
     double nn = (double)n;
-    double slope = ((double)dot_f(add, nadd, n) / nn - x_mean * y_mean) /
-                   ((double)dot_f(add, add, n) / nn - x_mean * x_mean);
+    /* The reference is C++ built with -O3 -march=native (CMakeLists.txt:14,24): g++ contracts a*b +- c into an
+     * FMA by default in C++ (-ffp-contract=fast; only ISO C turns it off), so `dot/n - x_mean*y_mean` and
+     * `y - slope * x` (tools.h:64-66) are fused multiply-adds on FMA hardware.  This file is C11, where nothing
+     * is contracted implicitly: the fusions are written out. */
+    double slope = fma(-x_mean, y_mean, (double)dot_f(add, nadd, n) / nn) /
+                   fma(-x_mean, x_mean, (double)dot_f(add, add, n) / nn);
     float k = (float)slope; /* Armadillo converts the scalar to the element type */
-    for (int i = 0; i < n; ++i) nadd[i] = nadd[i] - add[i] * k;
+    for (int i = 0; i < n; ++i) nadd[i] = fmaf(-add[i], k, nadd[i]);
     /* standardise(add) then standardise(residuals) */
     for (int v = 0; v < 2; ++v) {
         float* vec = v ? nadd : add;

@@ -79,3 +79,23 @@ def assert_ld_close(got: dict, exp: dict, *, tol=TOL, wse_budget=0.001, label=""
         bad = np.flatnonzero(err > lim)
         assert bad.size == 0, (f"{label} {k}: {bad.size} out of tolerance, worst |d|={err.max():.3g} "
                                f"at {np.flatnonzero(keep)[np.flatnonzero(m)[bad[:5]]]}")
+
+
+def rare_variant_set(n_org: int, n_snp: int = 400, seed: int = 5):
+    """PLINK rows + cM positions of a chromosome where every other SNP is rare (MAF 1e-4 .. 3e-3, most
+    without a hom-minor call) and a quarter of the SNPs have A1 as the minor allele (PLINK's default): at
+    N % 4 == 0 those have het + hom-A2 calls only — a constant dominance coding whose fp32 residual in the
+    reference is rounding noise."""
+    from nldsc_amd import synth
+    rng = np.random.default_rng(seed)
+    M, N = n_snp, n_org
+    maf = np.where(np.arange(M) % 2 == 0, 10 ** rng.uniform(-4, np.log10(3e-3), M), rng.uniform(0.05, 0.5, M))
+    g = np.empty((M, N), np.int8)
+    for j in range(M):
+        a = (rng.random(N) < maf[j]).astype(np.int8) + (rng.random(N) < maf[j]).astype(np.int8)
+        if j % 4 == 0:
+            a = 2 - a  # minor allele = A1
+        a[rng.random(N) < 0.01] = -1
+        g[j] = a
+    pos = np.cumsum(rng.exponential(0.05, M))
+    return synth.pack_bed_rows(g), pos

@@ -43,13 +43,20 @@ EXACT = ("i8", "f4")  # integer Gram paths: exact up to the fp64 epilogue
 @pytest.mark.parametrize("mode", sorted(MODES))
 @pytest.mark.parametrize("name", SETS)
 def test_golden_sets_vs_oracle_and_f64(engine, name, mode):
-    got, meta, orc, f64, _, _ = run_set(engine, name, flags=MODES[mode])
-    record(f"golden_{name}_{mode}", dict(vs_oracle=max_errors(got, orc), vs_f64=max_errors(got, f64)))
+    """Default run (rare variants' residuals replayed in the reference's fp32 arithmetic) against the oracle;
+    FLAG_EXACT_RARE run against the fp64 truth, tightly."""
+    ref, meta, orc, f64, _, bed = run_set(engine, name, flags=MODES[mode])
+    got, *_ = run_set(engine, name, flags=MODES[mode] | _lib_flag("FLAG_EXACT_RARE"))
+    record(f"golden_{name}_{mode}", dict(vs_oracle=max_errors(ref, orc), vs_f64=max_errors(got, f64)))
     # MAF: the same fp32 formula from integer counts -> bit-exact
     np.testing.assert_array_equal(got["maf"], f64["maf"])
-    np.testing.assert_array_equal(got["maf"], orc["maf"])
+    np.testing.assert_array_equal(ref["maf"], orc["maf"])
     assert_ld_close(got, f64, label=f"{name} vs f64")
-    assert_ld_close(got, orc, label=f"{name} vs oracle")
+    assert_ld_close(ref, orc, label=f"{name} vs oracle")
+    cnt = O.code_counts(bed, meta["n_snp"], meta["n_org"])
+    rep = (cnt[:, [0, 2, 3]].min(1) <= 16) & ~np.isnan(orc["residuals_std"])
+    assert rep.any()
+    np.testing.assert_array_equal(ref["residuals_std"][rep], orc["residuals_std"][rep])
     # tighter against the fp64 restatement: the GPU path differs only by fp32 lookup values and
     # 2048-sample fp32 MFMA chains
     m = ~np.isnan(f64["l2"])
@@ -168,7 +175,9 @@ def test_random_small_configs_vs_f64(engine, seed, mode):
     w = float(rng.choice([0.05, 0.5, 1.0, 100.0]))
     maf, std_thr, rsq = float(rng.choice([0.0, 0.01, 0.05])), float(rng.choice([0.0, 1e-5])), 0.5 / max(M, 11)
     engine.load_bed_bytes(synth.bed_bytes(rows), M, N)
-    got = engine.run(w, maf, std_thr, rsq, pos, flags=MODES[mode])
+    # tiny N % 4 == 0 cohorts often have SNPs without hom-A1 calls: compared with the exact truth, so the
+    # exact residual (test_rare_variants_reference_residual covers the reference's fp32 one)
+    got = engine.run(w, maf, std_thr, rsq, pos, flags=MODES[mode] | _lib_flag("FLAG_EXACT_RARE"))
     exp = O.run_f64(rows, N, w, maf, std_thr, rsq, pos)
     tol = dict(l2=(1e-4, 1e-5), l2d=(1e-5, 1e-5), residuals_std=(1e-12, 1e-10), maf=(0.0, 0.0))
     if mode in EXACT:
@@ -318,8 +327,9 @@ def test_c2_shape_additive_only_vs_oracle(engine, c2_slice, mode):
     sub = {k: v[t] for k, v in got.items()}
     np.testing.assert_array_equal(sub["l2_ws"], truth["l2_ws"])
     np.testing.assert_allclose(sub["l2"], truth["l2"], rtol=1e-4, atol=1e-3)
-    if mode in EXACT:
-        assert np.max(np.abs(sub["l2"] - truth["l2"])) < 1e-9
+    if mode in EXACT:  # exact vectors for the rare variants too (by default they are the reference's fp32 ones)
+        ex = engine.run(*d["args"], pos, flags=MODES[mode] | _lib.FLAG_ADDITIVE_ONLY | _lib.FLAG_EXACT_RARE)
+        assert np.max(np.abs(ex["l2"][t] - truth["l2"])) < 1e-9
 
 
 def test_f4_gram_is_bitwise_the_int8_gram(engine):
@@ -398,7 +408,7 @@ def test_heavy_maf_failure_both_schedule_paths(engine, order):
     exp = O.run_f64(rows, N, 1.0, 0.2, 1e-5, 0.01, pos)
     assert np.isnan(exp["l2"]).sum() > M // 5  # many SNPs fail MAF 0.2
     for mode in EXACT:
-        got = engine.run(1.0, 0.2, 1e-5, 0.01, pos, flags=MODES[mode])
+        got = engine.run(1.0, 0.2, 1e-5, 0.01, pos, flags=MODES[mode] | _lib_flag("FLAG_EXACT_RARE"))
         assert_ld_close(got, exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
                                            maf=(0.0, 0.0)), label=f"{order} {mode}")
 
@@ -479,7 +489,8 @@ def test_gpu_schedule_matches_host_schedule(engine, seed):
             os.environ["NLDSC_GPU_PLAN"] = g
             with Engine(0) as e:
                 e.load_bed_bytes(synth.bed_bytes(rows), M, N)
-                out[g] = [(e.run(*args, own=o, flags=MODES["f4"]), e.timings()["band_items"]) for o in owns]
+                out[g] = [(e.run(*args, own=o, flags=MODES["f4"] | _lib_flag("FLAG_EXACT_RARE")),
+                           e.timings()["band_items"]) for o in owns]
     finally:
         if old is None:
             os.environ.pop("NLDSC_GPU_PLAN", None)
@@ -526,9 +537,9 @@ def test_allele_orientation_is_invisible(name):
         for o in ("1", "0"):
             os.environ["NLDSC_ORIENT"] = o
             for mode in ("f4", "i8", "f32"):
-                with Engine(0) as e:
+                with Engine(0) as e:  # swapped rare SNPs may lack hom-A1 calls: exact residuals vs the truth
                     e.load_bed_bytes(b"\x6c\x1b\x01" + swapped.tobytes(), M, N)
-                    out[o, mode] = e.run(*args, flags=MODES[mode])
+                    out[o, mode] = e.run(*args, flags=MODES[mode] | _lib_flag("FLAG_EXACT_RARE"))
     finally:
         if old is None:
             os.environ.pop("NLDSC_ORIENT", None)
@@ -561,9 +572,52 @@ def test_missing_free_blocks_skip_m_products(engine, N):
     pos = synth.positions_cm(spec)
     args = (1.0, 0.01, 1e-5, 1.0 / M, pos)
     engine.load_bed_bytes(synth.bed_bytes(rows), M, N)
-    f4 = engine.run(*args, flags=MODES["f4"])
-    i8 = engine.run(*args, flags=MODES["i8"])
+    xr = _lib_flag("FLAG_EXACT_RARE")
+    f4 = engine.run(*args, flags=MODES["f4"] | xr)
+    i8 = engine.run(*args, flags=MODES["i8"] | xr)
     same_gram(f4, i8, f"N={N}")
     exp = O.run_f64(rows, N, *args)
     assert_ld_close(f4, exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
                                       maf=(0.0, 0.0)), label=f"missing-free blocks N={N}")
+
+
+@pytest.mark.parametrize("mode", sorted(MODES))
+@pytest.mark.parametrize("n_org,strict", [(50_000, False), (50_001, True), (50_001, False), (315_599, False)])
+def test_rare_variants_reference_residual(engine, mode, n_org, strict):
+    """Rare variants (<= 16 calls in a genotype class): by default the engine replays the reference's fp32
+    residual (reference_residual_kernel), so their residual std is bit-identical to the oracle's and the
+    noise-dominated residuals enter WSD / L2D as in the reference — in particular SNPs with het + hom-A2
+    calls only (A1 minor, no hom-minor call: an exactly constant residual the reference reports as noise),
+    which exist at N % 4 == 0 or in the strict order (the reference's order at N % 4 != 0 reads a hom-A1
+    padding pair in every row).  With FLAG_EXACT_RARE the engine reports the exact residual and equals
+    the fp64 truth."""
+    from conftest import rare_variant_set
+    from nldsc_amd import _lib
+    rows, pos = rare_variant_set(n_org)
+    M = rows.shape[0]
+    bed = b"\x6c\x1b\x01" + rows.tobytes()
+    oflags = O.NO_COPIES | (O.STRICT_ORDER if strict else 0)
+    args = (1.0, 1e-5, 1e-5, 1.0 / M, pos)
+    orc = O.run_c(bed, M, n_org, *args, flags=oflags)
+    cnt = O.code_counts(bed, M, n_org, strict=strict)
+    passed = ~np.isnan(orc["residuals_std"])
+    constant = (cnt[:, 0] == 0) & (cnt[:, 2] > 0) & (cnt[:, 3] > 0) & passed
+    replayed = (cnt[:, [0, 2, 3]].min(1) <= 16) & passed
+    assert (constant.sum() > 50) == (n_org % 4 == 0 or strict) and replayed.sum() > 90
+    base = MODES[mode] | (_lib.FLAG_STRICT_PLINK_ORDER if strict else 0)
+    engine.load_bed_bytes(bed, M, n_org)
+    got = engine.run(*args, flags=base)
+    record(f"rare_{n_org}_{'strict' if strict else 'compat'}_{mode}",
+           dict(constant_residual=int(constant.sum()), replayed=int(replayed.sum()),
+                constant_above_std_thr=int((orc["residuals_std"][constant] > 1e-5).sum()),
+                gpu_vs_oracle=max_errors(got, orc)))
+    np.testing.assert_array_equal(got["residuals_std"][replayed], orc["residuals_std"][replayed])
+    assert_ld_close(got, orc, label=f"rare N={n_org} {mode}")
+    exact = engine.run(*args, flags=base | _lib.FLAG_EXACT_RARE)
+    truth = O.run_f64(rows, n_org, *args, strict=strict)
+    assert (exact["residuals_std"][constant] == 0).all()
+    tol = dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10), maf=(0.0, 0.0)) \
+        if mode in EXACT else None
+    assert_ld_close(exact, truth, **({"tol": tol} if tol else {}), label=f"rare exact N={n_org} {mode}")
+    if constant.any():
+        assert (got["l2d_ws"] != exact["l2d_ws"]).any()  # the noise residuals are counted by default
