@@ -123,6 +123,7 @@ struct nldsc_engine {
     DevBuf<float2> lut;
     DevBuf<nldsc::SnpConst> cst;
     DevBuf<uint8_t> sflags;
+    DevBuf<uint8_t> blk_rep;  // per 32-SNP block: holds a rare variant with replayed fp32 vectors (KC items)
     DevBuf<double> pos, maf, rstd, l2_acc, l2d_acc, l2, l2d;
     DevBuf<int4> items;
     // host scratch
@@ -441,6 +442,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     HIPCHK(e->lut.ensure((size_t)Mpad * 4));
     HIPCHK(e->cst.ensure((size_t)Mpad));
     HIPCHK(e->sflags.ensure((size_t)Mpad));
+    HIPCHK(e->blk_rep.ensure((size_t)nblk));
     HIPCHK(e->pos.ensure((size_t)M));
     HIPCHK(e->maf.ensure((size_t)M));
     HIPCHK(e->rstd.ensure((size_t)M));
@@ -490,10 +492,11 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->oriented ? e->flip.p : nullptr, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->cst.p,
                                    e->sflags.p, e->maf.p, e->rstd.p, st));
     // rare variants: the reference's fp32 residual replayed (its sums assume N < 2^23)
-    if (N < (1 << 23) && !(p->flags & NLDSC_FLAG_EXACT_RARE))
+    const bool replay = N < (1 << 23) && !(p->flags & NLDSC_FLAG_EXACT_RARE);
+    if (replay)
         HIPCHK(nldsc::launch_reference_residuals(e->bed.p, row_bytes, N, strict, e->counts.p,
                                                  e->oriented ? e->flip.p : nullptr, M, p->std_thr, e->cst.p, e->lut.p,
-                                                 e->sflags.p, e->rstd.p, st));
+                                                 e->sflags.p, e->rstd.p, e->blk_rep.p, st));
     HIPCHK(hipEventRecord(e->ev[2], st));
 
     // ---- window replay + schedule ----
@@ -583,12 +586,13 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         if (use_f4)
             HIPCHK(nldsc::launch_band_f4(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p,
                                          e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr,
-                                         own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true, st));
+                                         own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true,
+                                         replay ? e->blk_rep.p : nullptr, st));
         else if (use_i8)
             HIPCHK(nldsc::launch_band_i8(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p,
                                          e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
                                          (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
-                                         e->ws_acc.p, true, st));
+                                         e->ws_acc.p, true, replay ? e->blk_rep.p : nullptr, st));
         else
             HIPCHK(nldsc::launch_band(dom, 2, n_items, geno, pitch_words, n_it,
                                       e->lut.p, e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,

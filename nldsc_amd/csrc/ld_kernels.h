@@ -38,7 +38,7 @@ hipError_t launch_snp_stats(const int* counts, const uint8_t* flip, const double
 constexpr int REF_RESIDUAL_MIN_CLASS = 16;
 hipError_t launch_reference_residuals(const uint8_t* img, int row_bytes, int n_org, bool strict, const int* counts,
                                      const uint8_t* flip, int n_snp, double std_thr, SnpConst* cst, float2* lut,
-                                     uint8_t* sflags, double* rstd_out, hipStream_t st);
+                                     uint8_t* sflags, double* rstd_out, uint8_t* blk_rep, hipStream_t st);
 // after a load: swap 00 <-> 11 in rows (and saved last bytes) with more hom-A2 than hom-A1 calls; flip[j] = 1
 hipError_t launch_orient_rows(uint8_t* img, uint8_t* last, int n_snp, int row_bytes, uint8_t* flip, hipStream_t st);
 // exact left pointers L from the all-pass replay's A and the device MAF flags (sorted positions)
@@ -57,16 +57,19 @@ hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int
 hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
-                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st);
+                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
+                          hipStream_t st);
 // K-loop chunks (128 samples each) per fp32 accumulation segment of the fp4 path: rows longer than this
 // (N > 2^19) run the segmented kernel, which folds the fp32 Gram into int32 after every segment
 constexpr int F4_SEG_CHUNKS = 4096;
-// exact path on fp4 MFMAs (N < 2^27), items (I, J0, nc <= max_nc, 0); max_nc must be 1 when
-// n_it > F4_SEG_CHUNKS
+// exact path on fp4 MFMAs (N < 2^27), items (I, J0, 1, 0) (max_nc must be 1).  blk_rep (or nullptr): per 32-SNP
+// block, 1 if a SNP carries replayed fp32 vectors (ka / kr != 0): its items run in a second launch (the exact
+// kernels' KC instantiation)
 hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
-                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st);
+                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
+                          hipStream_t st);
 hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2d_acc, const int* ws_acc, int n_snp,
                            int own_lo, int own_hi, bool dom, double* l2, double* l2d, int* ws3, hipStream_t st);
 hipError_t launch_synth_bed(uint8_t* rows, int n_snp, int n_org, int nb, const float* thr, float rho, float missing,

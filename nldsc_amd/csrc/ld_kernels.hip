@@ -444,7 +444,8 @@ __global__ void __launch_bounds__(64) reference_residual_kernel(const uint8_t* _
                                                                 const uint8_t* __restrict__ flip, int n_snp,
                                                                 double std_thr, SnpConst* __restrict__ cst,
                                                                 float2* __restrict__ lut, uint8_t* __restrict__ sflags,
-                                                                double* __restrict__ rstd_out) {
+                                                                double* __restrict__ rstd_out,
+                                                                uint8_t* __restrict__ blk_rep) {
 #pragma clang fp contract(off)
     const int j = blockIdx.x;
     if (j >= n_snp || !(sflags[j] & 1)) return;  // MAF-failed or unused: no residual
@@ -493,6 +494,7 @@ __global__ void __launch_bounds__(64) reference_residual_kernel(const uint8_t* _
     const float sd_a = (float)sqrt((double)var_a);
     if ((threadIdx.x & 63) != 0) return;
     rstd_out[j] = (double)sd;
+    blk_rep[j >> 5] = 1;  // its band items take the KC epilogue
     SnpConst K = cst[j];
     float2* L = lut + (size_t)j * 4;
     // stored codes 00, 10, 11 (slots 0, 2, 3 of the tables) and their call counts; missing is slot 1
@@ -945,7 +947,7 @@ __device__ __forceinline__ int xcd_slot(int b, int n) {
 // MB: the Gram is in the missing basis {x, h, m} (fp4 path): gxo holds x.m, gox m.x, goo m.m, goh m.h,
 // gho h.m, and `kslots` is the number of individual slots (n_org; the other slots are all-zero in every
 // plane); o = 1 - m over the individual slots.
-template <bool DOM, class Acc, bool MB = false>
+template <bool DOM, class Acc, bool MB = false, bool KC = false>
 __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpConst* cst, double* s_l2, double* s_l2d,
                                               int* s_wsa, int* s_wsd, int* s_wse, int rb, int cb, bool diag, int i,
                                               int h, const Acc& gxx, const Acc& gxo, const Acc& gox, const Acc& goo,
@@ -973,8 +975,10 @@ __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpCons
             const double xo = MB ? ki.X - 0.5 * ((double)gxo[r] - mm) : (double)gxo[r];
             const double ox = MB ? kj.X - 0.5 * ((double)gox[r] - mm) : (double)gox[r];
             const double oo = MB ? ki.Ob + kj.Ob - kslots + mm : mm;
-            const double aa = (xx - kj.mu * xo - ki.mu * (ox - kj.mu * oo)) / (ki.sa * kj.sa) + kj.ka * ki.SA +
-                              ki.ka * (kj.SA + kj.ka * n_org);
+            // KC: the item holds a replayed rare variant (ka / kr terms; kept out of the common path, whose
+            // registers are all taken)
+            const double aa = (xx - kj.mu * xo - ki.mu * (ox - kj.mu * oo)) / (ki.sa * kj.sa) +
+                              (KC ? kj.ka * ki.SA + ki.ka * (kj.SA + kj.ka * n_org) : 0.0);
             const double r2 = r2_adjusted(aa, n_org);
             if (nij) { atomicAdd(&s_l2[si], r2); atomicAdd(&s_wsa[si], 1); }
             if (nji) { atomicAdd(&s_l2[sj], r2); atomicAdd(&s_wsa[sj], 1); }
@@ -984,7 +988,7 @@ __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpCons
                     const double oh = MB ? kj.H - (double)goh[r] : (double)goh[r];
                     const double ar = (2.0 * xh - kj.beta * xx - kj.c * xo -
                                        ki.mu * (2.0 * oh - kj.beta * ox - kj.c * oo)) / (ki.sa * kj.s) +
-                                      kj.kr * ki.SA + ki.ka * (kj.SR + kj.kr * n_org);
+                                      (KC ? kj.kr * ki.SA + ki.ka * (kj.SR + kj.kr * n_org) : 0.0);
                     const double rd = r2_adjusted(ar, n_org);
                     atomicAdd(&s_l2d[si], rd); atomicAdd(&s_wsd[si], 1);
                     if (rd > rsq_thr) atomicAdd(&s_wse[si], 1);
@@ -994,7 +998,7 @@ __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpCons
                     const double ho = MB ? ki.H - (double)gho[r] : (double)gho[r];
                     const double ra = (2.0 * hx - ki.beta * xx - ki.c * ox -
                                        kj.mu * (2.0 * ho - ki.beta * xo - ki.c * oo)) / (ki.s * kj.sa) +
-                                      ki.kr * kj.SA + kj.ka * (ki.SR + ki.kr * n_org);
+                                      (KC ? ki.kr * kj.SA + kj.ka * (ki.SR + ki.kr * n_org) : 0.0);
                     const double rd = r2_adjusted(ra, n_org);
                     atomicAdd(&s_l2d[sj], rd); atomicAdd(&s_wsd[sj], 1);
                     if (rd > rsq_thr) atomicAdd(&s_wse[sj], 1);
@@ -1002,6 +1006,17 @@ __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpCons
             }
         }
     }
+}
+
+// Items holding a rare variant whose vectors are the reference's fp32 ones (ka / kr != 0: blk_rep[block] = 1,
+// set by reference_residual_kernel) need the epilogue's ka / kr terms, which the common epilogue has no
+// registers left for: they run in a second launch of the kernel instantiated with KC = true, and the KC = false
+// launch skips them.  blk_rep == nullptr: no replayed SNP (KC = false only).
+template <bool KC>
+__device__ __forceinline__ bool skip_item(const uint8_t* blk_rep, int4 it) {
+    if (!KC && blk_rep == nullptr) return false;
+    const bool rep = blk_rep[it.x] | blk_rep[it.y];
+    return KC ? !rep : rep;
 }
 
 struct BandI8Lds {
@@ -1012,7 +1027,7 @@ struct BandI8Lds {
 };
 
 // NC column blocks J0 .. J0+NC-1 share the row decode; DIAG0: block 0 is the diagonal (J0 == I).
-template <bool DOM, int NC, bool DIAG0>
+template <bool DOM, int NC, bool DIAG0, bool KC>
 __device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const uint32_t* __restrict__ geno,
                                              int pitch_words, int n_it, const SnpConst* __restrict__ cst,
                                              const double* __restrict__ pos, const int* __restrict__ Lw,
@@ -1108,8 +1123,9 @@ __device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const
     // ---- fused epilogue (fp64): standardised dots from the integer Gram, r2adj, masks, sums ----
 #pragma unroll
     for (int b = 0; b < NC; ++b)
-        pair_epilogue<DOM>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * b, DIAG0 && b == 0, i,
-                           h, gxx[b], gxo[b], gox[b], goo[b], gxh[b], goh[b], ghx[b], gho[b], ld_wind, n_org, rsq_thr);
+        pair_epilogue<DOM, i32x16, false, KC>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * b,
+                                              DIAG0 && b == 0, i, h, gxx[b], gxo[b], gox[b], goo[b], gxh[b], goh[b],
+                                              ghx[b], gho[b], ld_wind, n_org, rsq_thr);
     __syncthreads();
     for (int s = lane; s < NS; s += 64) {
         const int g = sh.info[s].g;
@@ -1126,24 +1142,23 @@ __device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const
     }
 }
 
-// WPS: waves per SIMD the register allocation must allow (NC=1 bodies fit 2, NC=2 bodies need 1).
-template <bool DOM, int WPS>
-__global__ void __launch_bounds__(64, WPS) band_i8_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
-                                                        const SnpConst* __restrict__ cst, const int4* __restrict__ items,
-                                                        const double* __restrict__ pos, const int* __restrict__ Lw,
-                                                        const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
-                                                        int n_snp, double ld_wind, double n_org, double rsq_thr,
-                                                        int own_lo, int own_hi, double* __restrict__ l2_acc,
-                                                        double* __restrict__ l2d_acc, int* __restrict__ ws_acc,
-                                                        int xcd) {
+// One block pair per item (the engine plans single column blocks for the exact paths), 2 waves / SIMD.
+template <bool DOM, bool KC>
+__global__ void __launch_bounds__(64, 2) band_i8_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
+                                                      const SnpConst* __restrict__ cst, const int4* __restrict__ items,
+                                                      const double* __restrict__ pos, const int* __restrict__ Lw,
+                                                      const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
+                                                      int n_snp, double ld_wind, double n_org, double rsq_thr,
+                                                      int own_lo, int own_hi, double* __restrict__ l2_acc,
+                                                      double* __restrict__ l2d_acc, int* __restrict__ ws_acc,
+                                                      int xcd, const uint8_t* __restrict__ blk_rep) {
     __shared__ BandI8Lds sh;
     const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
-#define NLDSC_BODY(NC_, DIAG_)                                                                                        \
-    band_i8_body<DOM, NC_, DIAG_>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,  \
-                                  rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc)
-    const bool diag = it.y == it.x;
-    if (WPS == 1 && it.z == 2) { if (diag) NLDSC_BODY(2, true); else NLDSC_BODY(2, false); }
-    else { if (diag) NLDSC_BODY(1, true); else NLDSC_BODY(1, false); }
+    if (skip_item<KC>(blk_rep, it)) return;
+#define NLDSC_BODY(DIAG_)                                                                                             \
+    band_i8_body<DOM, 1, DIAG_, KC>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,\
+                                    rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc)
+    if (it.y == it.x) NLDSC_BODY(true); else NLDSC_BODY(false);
 #undef NLDSC_BODY
 }
 
@@ -1209,7 +1224,7 @@ __device__ __forceinline__ f32x16v mfma_f4(const i32x4& a, const i32x4& b, const
 // samples each, so a segment adds at most 16 * 128 * SEG <= 2^23 to an entry and the fp32 accumulators stay
 // exact integers); after each segment the fp32 Gram is folded into int32 entries (add+dom) or its multiples
 // of 2^16 move to packed 16-bit counters (additive-only), exact while every entry is <= 16N < 2^31.
-template <bool DOM, int NC, bool DIAG0, int SEG = 0>
+template <bool DOM, int NC, bool DIAG0, int SEG, bool KC>
 __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const uint32_t* __restrict__ geno,
                                              int pitch_words, int n_it, const SnpConst* __restrict__ cst,
                                              const double* __restrict__ pos, const int* __restrict__ Lw,
@@ -1339,9 +1354,9 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         }
 #pragma unroll
         for (int c = 0; c < NC; ++c)
-            pair_epilogue<DOM, f32x16v, true>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * c,
-                                              DIAG0 && c == 0, i, h, gxx[c], gxo[c], gox[c], goo[c], gxh[c], goh[c],
-                                              ghx[c], gho[c], ld_wind, n_org, rsq_thr, n_org);
+            pair_epilogue<DOM, f32x16v, true, KC>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * c,
+                                                  DIAG0 && c == 0, i, h, gxx[c], gxo[c], gox[c], goo[c], gxh[c],
+                                                  goh[c], ghx[c], gho[c], ld_wind, n_org, rsq_thr, n_org);
     } else {
         static_assert(NC == 1, "segmented K loop: one column block");
         i32x16 ixx = {}, ixo = {}, iox = {}, ioo = {}, ixh = {}, ioh = {}, ihx = {}, iho = {};
@@ -1395,8 +1410,8 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
 #pragma unroll
             for (int r = 0; r < 16; ++r) iox[r] = tri[i * 33 + (r & 3) + 8 * (r >> 2) + 4 * h];
         }
-        pair_epilogue<DOM, i32x16, true>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32, DIAG0, i, h,
-                                         ixx, ixo, iox, ioo, ixh, ioh, ihx, iho, ld_wind, n_org, rsq_thr, n_org);
+        pair_epilogue<DOM, i32x16, true, KC>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32, DIAG0, i,
+                                             h, ixx, ixo, iox, ioo, ixh, ioh, ihx, iho, ld_wind, n_org, rsq_thr, n_org);
     }
     __syncthreads();
     for (int s = lane; s < NS; s += 64) {
@@ -1414,26 +1429,24 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     }
 }
 
-// WPS 2: single block-pair items; WPS 1: items of up to 2 column blocks (1 wave per SIMD, the
-// 2 x 128 accumulator registers in AGPRs).
-template <bool DOM, int WPS, int SEG = 0>
+// One block pair per item.  WPS 2, except the segmented add+dom kernel (its int32 fold registers need 1).
+template <bool DOM, int WPS, int SEG, bool KC>
 __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
                                                         const SnpConst* __restrict__ cst, const int4* __restrict__ items,
                                                         const double* __restrict__ pos, const int* __restrict__ Lw,
                                                         const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
                                                         int n_snp, double ld_wind, double n_org, double rsq_thr,
                                                         int own_lo, int own_hi, double* __restrict__ l2_acc,
-                                                        double* __restrict__ l2d_acc, int* __restrict__ ws_acc, int xcd) {
+                                                        double* __restrict__ l2d_acc, int* __restrict__ ws_acc, int xcd,
+                                                        const uint8_t* __restrict__ blk_rep) {
     __shared__ BandI8Lds sh;
     __shared__ float tr[32 * 33];
     const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
-#define NLDSC_BODY(NC_, DIAG_)                                                                                        \
-    band_f4_body<DOM, NC_, DIAG_, SEG>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind,   \
-                                       n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, tr)
-    const bool diag = it.y == it.x;
-    if constexpr (SEG > 0) { if (diag) NLDSC_BODY(1, true); else NLDSC_BODY(1, false); }
-    else if (WPS == 1 && it.z == 2) { if (diag) NLDSC_BODY(2, true); else NLDSC_BODY(2, false); }
-    else { if (diag) NLDSC_BODY(1, true); else NLDSC_BODY(1, false); }
+    if (skip_item<KC>(blk_rep, it)) return;
+#define NLDSC_BODY(DIAG_)                                                                                             \
+    band_f4_body<DOM, 1, DIAG_, SEG, KC>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind,  \
+                                         n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, tr)
+    if (it.y == it.x) NLDSC_BODY(true); else NLDSC_BODY(false);
 #undef NLDSC_BODY
 }
 
@@ -1548,10 +1561,12 @@ hipError_t launch_snp_stats(const int* counts, const uint8_t* flip, const double
 
 hipError_t launch_reference_residuals(const uint8_t* img, int row_bytes, int n_org, bool strict, const int* counts,
                                      const uint8_t* flip, int n_snp, double std_thr, SnpConst* cst, float2* lut,
-                                     uint8_t* sflags, double* rstd_out, hipStream_t st) {
+                                     uint8_t* sflags, double* rstd_out, uint8_t* blk_rep, hipStream_t st) {
     if (n_snp <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(blk_rep, 0, (size_t)(n_snp + 31) / 32, st);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(reference_residual_kernel, dim3(n_snp), dim3(64), 0, st, img, row_bytes, n_org, (int)strict,
-                       counts, flip, n_snp, std_thr, cst, lut, sflags, rstd_out);
+                       counts, flip, n_snp, std_thr, cst, lut, sflags, rstd_out, blk_rep);
     return hipGetLastError();
 }
 
@@ -1605,14 +1620,16 @@ hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int
 hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
-                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st) {
+                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
+                          hipStream_t st) {
     if (n_items <= 0) return hipSuccess;
-#define NLDSC_BAND(DOM_, WPS_)                                                                                      \
-    hipLaunchKernelGGL((band_i8_kernel<DOM_, WPS_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, cst,   \
+    if (max_nc != 1) return hipErrorInvalidValue;  // single block-pair items
+#define NLDSC_BAND(DOM_, KC_)                                                                                       \
+    hipLaunchKernelGGL((band_i8_kernel<DOM_, KC_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, cst,    \
                        items, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, \
-                       ws_acc, xcd ? 1 : 0)
-    if (dom) { if (max_nc == 2) NLDSC_BAND(true, 1); else NLDSC_BAND(true, 2); }
-    else { if (max_nc == 2) NLDSC_BAND(false, 1); else NLDSC_BAND(false, 2); }
+                       ws_acc, xcd ? 1 : 0, blk_rep)
+    if (dom) NLDSC_BAND(true, false); else NLDSC_BAND(false, false);
+    if (blk_rep) { if (dom) NLDSC_BAND(true, true); else NLDSC_BAND(false, true); }
 #undef NLDSC_BAND
     return hipGetLastError();
 }
@@ -1620,17 +1637,22 @@ hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* gen
 hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
-                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, hipStream_t st) {
+                          int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
+                          hipStream_t st) {
     if (n_items <= 0) return hipSuccess;
-    if (n_it > F4_SEG_CHUNKS && max_nc != 1) return hipErrorInvalidValue;  // segmented kernel: single blocks only
-#define NLDSC_BAND(DOM_, WPS_, SEG_)                                                                                \
-    hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, \
-                       cst, items, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc,     \
-                       l2d_acc, ws_acc, xcd ? 1 : 0)
+    if (max_nc != 1) return hipErrorInvalidValue;  // single block-pair items
+#define NLDSC_BAND(DOM_, WPS_, SEG_, KC_)                                                                           \
+    hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_, KC_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words,  \
+                       n_it, cst, items, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi,       \
+                       l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep)
+#define NLDSC_PICK(KC_)                                                                                              \
+    if (n_it > F4_SEG_CHUNKS) { if (dom) NLDSC_BAND(true, 1, F4_SEG_CHUNKS, KC_); else NLDSC_BAND(false, 2, F4_SEG_CHUNKS, KC_); } \
+    else if (dom) NLDSC_BAND(true, 2, 0, KC_);                                                                       \
+    else NLDSC_BAND(false, 2, 0, KC_)
     // segmented kernel: the add+dom variant needs more than 256 registers (2 waves / SIMD would spill)
-    if (n_it > F4_SEG_CHUNKS) { if (dom) NLDSC_BAND(true, 1, F4_SEG_CHUNKS); else NLDSC_BAND(false, 2, F4_SEG_CHUNKS); }
-    else if (dom) { if (max_nc == 2) NLDSC_BAND(true, 1, 0); else NLDSC_BAND(true, 2, 0); }
-    else { if (max_nc == 2) NLDSC_BAND(false, 1, 0); else NLDSC_BAND(false, 2, 0); }
+    NLDSC_PICK(false);
+    if (blk_rep) { NLDSC_PICK(true); }
+#undef NLDSC_PICK
 #undef NLDSC_BAND
     return hipGetLastError();
 }

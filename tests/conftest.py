@@ -51,6 +51,15 @@ def max_errors(got: dict, exp: dict) -> dict:
     return out
 
 
+def progress(msg: str) -> None:
+    """Append a line to gpurun_out/progress.log (GPU boxes): long fixtures show they are alive."""
+    d = os.path.join(REPO, "gpurun_out")
+    if os.path.isdir(d):
+        import time
+        with open(os.path.join(d, "progress.log"), "a") as fh:
+            fh.write(f"{time.strftime('%H:%M:%S')} {msg}\n")
+
+
 def record(name: str, payload: dict) -> None:
     """Write measured parity numbers to gpurun_out/ when it exists (GPU box runs)."""
     d = os.path.join(REPO, "gpurun_out")

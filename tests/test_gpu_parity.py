@@ -10,7 +10,7 @@ import sys
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, REPO, assert_ld_close, golden_sets, load_set, max_errors, record
+from conftest import GOLDEN, REPO, assert_ld_close, golden_sets, load_set, max_errors, progress, record
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -205,7 +205,9 @@ def c3_slice(engine):
     bed = buf.cpu().numpy().tobytes()
     args = (1.0, 1e-4, 1e-5, 1.0 / M)
     t = c3_targets(M)
+    progress("c3 fixture: oracle")
     exp = O.run_c(bed, M, N, *args, pos, targets=t, flags=O.NO_COPIES)
+    progress("c3 fixture: fp64 truth")
     rows = np.frombuffer(bed, np.uint8, offset=3).reshape(M, -1)
     truth = O.run_f64_targets(rows, N, *args, pos, t, bed=bed)
     yield dict(buf=buf, pos=pos, N=N, M=M, args=args, t=t, exp=exp, truth=truth)
@@ -242,7 +244,8 @@ def c5_slice(engine):
     """C5 shape (BASELINE.json configs[4], imputed genome): N = 315 599, no missing calls (hard calls), bp
     positions at 288 bp per SNP (2.88 Gb / 10 M SNPs, duplicates from integer rounding), --ld-wind-kb 1000:
     ~6 900 neighbours per SNP, so the plan's tiled wide-band item order and the missing-free 3-of-8 fp4
-    products run at full N.  12 000 SNPs (3.5 Mb); oracle + fp64 truth at 64 targets."""
+    products run at full N.  12 000 SNPs (3.5 Mb); oracle + fp64 truth at 40 targets (each one's window is
+    ~14 000 fp32 dots of 315 599 samples in the oracle)."""
     from nldsc_amd import synth
     N, M = 315_599, 12_000
     buf, pos = synth.device_bed(M, N, seed=21, length_cm=288.0 * M, missing=0.0)
@@ -250,16 +253,19 @@ def c5_slice(engine):
     bed = buf.cpu().numpy().tobytes()
     args = (1.0e6, 1e-4, 1e-5, 1.0 / M)
     t = set()
-    for b in range(180, 192):  # mid-chromosome band, full windows
+    for b in range(180, 186):  # mid-chromosome band, full windows: both edges of 6 blocks
         t.update(32 * b + k for k in (0, 1, 30, 31))
-    t.update({0, 1, 31, 32, 3000, 3001, 3039, 3040})    # left end: one-sided windows; within one window of it
-    t.update({M - 1, M - 2, M - 32, M - 33, 9000, 9031, 9032, 9063})
+    t.update({0, 1, 31, 32})                             # left end: one-sided windows
+    t.update({M - 1, M - 2, M - 32, M - 33})             # right end
     for k in range(8):
         t.add(4000 + 331 * k)                            # interior SNPs at various block offsets
     t = np.array(sorted(t), np.int32)
+    progress(f"c5 fixture: oracle at {len(t)} targets")
     exp = O.run_c(bed, M, N, *args, pos, targets=t, flags=O.NO_COPIES)
+    progress("c5 fixture: fp64 truth")
     rows = np.frombuffer(bed, np.uint8, offset=3).reshape(M, -1)
     truth = O.run_f64_targets(rows, N, *args, pos, t, bed=bed)
+    progress("c5 fixture: done")
     yield dict(buf=buf, pos=pos, N=N, M=M, args=args, t=t, exp=exp, truth=truth)
 
 
@@ -275,7 +281,7 @@ def test_c5_shape_1000kb_vs_oracle(engine, c5_slice, mode):
     record(f"c5_shape_{mode}", dict(n_org=N, n_snp=M, targets=t.tolist(), band_items=tim["band_items"],
                                     mean_window=float(got["l2_ws"].mean()), gpu_vs_oracle=max_errors(sub, exp),
                                     gpu_vs_truth=max_errors(sub, truth), oracle_vs_truth=max_errors(exp, truth)))
-    assert len(t) >= 64
+    assert len(t) >= 40
     assert got["l2_ws"][M // 2] > 6000  # ~6 900 neighbours mid-chromosome
     assert_ld_close(sub, truth, label="C5 shape vs fp64 truth")
     assert_ld_close(sub, exp, label="C5 shape vs oracle")
