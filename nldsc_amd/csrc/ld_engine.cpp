@@ -450,7 +450,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     HIPCHK(e->Rw.ensure((size_t)M));
     HIPCHK(e->l2_acc.ensure((size_t)M));
     HIPCHK(e->l2d_acc.ensure((size_t)M));
-    HIPCHK(e->ws_acc.ensure((size_t)M * 3));
+    HIPCHK(e->ws_acc.ensure((size_t)M * 4));  // WSA, WSD, WSDE, non-finite flags
     HIPCHK(e->l2.ensure((size_t)M));
     HIPCHK(e->l2d.ensure((size_t)M));
     HIPCHK(e->ws3.ensure((size_t)M * 3));
@@ -565,7 +565,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     }
     HIPCHK(hipMemsetAsync(e->l2_acc.p, 0, sizeof(double) * M, st));
     HIPCHK(hipMemsetAsync(e->l2d_acc.p, 0, sizeof(double) * M, st));
-    HIPCHK(hipMemsetAsync(e->ws_acc.p, 0, sizeof(int) * 3 * (size_t)M, st));
+    HIPCHK(hipMemsetAsync(e->ws_acc.p, 0, sizeof(int) * 4 * (size_t)M, st));
     auto t_host1 = std::chrono::steady_clock::now();
 
     HIPCHK(hipEventRecord(e->ev[3], st));

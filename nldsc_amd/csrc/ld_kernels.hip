@@ -680,6 +680,19 @@ __global__ void plan_emit_kernel(const int2* __restrict__ rows, int nblk, const 
     }
 }
 
+// Per-SNP sums across work items: every item adds its partial sums (fp64, per 32-SNP block) as fixed-point
+// integers (2^-44 units; |partial| <= 32, a SNP's total < 2^19) with 64-bit integer atomics, so the total does not
+// depend on the order in which items finish and L2 / L2D are bit-reproducible run to run (fp64 atomics are not).
+// Non-finite partials (windows poisoned by an all-missing SNP) set a flag instead (nanf: bit 1 L2, bit 2 L2D).
+constexpr double ACC_SCALE = 17592186044416.0;  // 2^44
+__device__ __forceinline__ void acc_fixed(double* acc, int* nanf, int bit, double v) {
+    if (!isfinite(v)) {
+        atomicOr(nanf, bit);
+        return;
+    }
+    atomicAdd(reinterpret_cast<unsigned long long*>(acc), (unsigned long long)__double2ll_rn(v * ACC_SCALE));
+}
+
 // ------------------------------------------------------------------------------------------
 // 3. band correlation kernel
 // ------------------------------------------------------------------------------------------
@@ -873,11 +886,11 @@ __device__ __forceinline__ void band_body(BandLds& sh, const int4 it, const uint
         const int g = info[s].g;
         if (g < own_lo || g >= own_hi || g >= n_snp) continue;
         if (s_wsa[s]) {
-            unsafeAtomicAdd(&l2_acc[g], s_l2[s]);
+            acc_fixed(&l2_acc[g], &ws_acc[3 * (size_t)n_snp + g], 1, s_l2[s]);
             atomicAdd(&ws_acc[g], s_wsa[s]);
         }
         if (DOM && s_wsd[s]) {
-            unsafeAtomicAdd(&l2d_acc[g], s_l2d[s]);
+            acc_fixed(&l2d_acc[g], &ws_acc[3 * (size_t)n_snp + g], 2, s_l2d[s]);
             atomicAdd(&ws_acc[(size_t)n_snp + g], s_wsd[s]);
             if (s_wse[s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + g], s_wse[s]);
         }
@@ -1131,11 +1144,11 @@ __device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const
         const int g = sh.info[s].g;
         if (g < own_lo || g >= own_hi || g >= n_snp) continue;
         if (sh.wsa[s]) {
-            unsafeAtomicAdd(&l2_acc[g], sh.l2[s]);
+            acc_fixed(&l2_acc[g], &ws_acc[3 * (size_t)n_snp + g], 1, sh.l2[s]);
             atomicAdd(&ws_acc[g], sh.wsa[s]);
         }
         if (DOM && sh.wsd[s]) {
-            unsafeAtomicAdd(&l2d_acc[g], sh.l2d[s]);
+            acc_fixed(&l2d_acc[g], &ws_acc[3 * (size_t)n_snp + g], 2, sh.l2d[s]);
             atomicAdd(&ws_acc[(size_t)n_snp + g], sh.wsd[s]);
             if (sh.wse[s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + g], sh.wse[s]);
         }
@@ -1418,11 +1431,11 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         const int g = sh.info[s].g;
         if (g < own_lo || g >= own_hi || g >= n_snp) continue;
         if (sh.wsa[s]) {
-            unsafeAtomicAdd(&l2_acc[g], sh.l2[s]);
+            acc_fixed(&l2_acc[g], &ws_acc[3 * (size_t)n_snp + g], 1, sh.l2[s]);
             atomicAdd(&ws_acc[g], sh.wsa[s]);
         }
         if (DOM && sh.wsd[s]) {
-            unsafeAtomicAdd(&l2d_acc[g], sh.l2d[s]);
+            acc_fixed(&l2d_acc[g], &ws_acc[3 * (size_t)n_snp + g], 2, sh.l2d[s]);
             atomicAdd(&ws_acc[(size_t)n_snp + g], sh.wsd[s]);
             if (sh.wse[s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + g], sh.wse[s]);
         }
@@ -1461,8 +1474,11 @@ __global__ void finalize_kernel(const int* __restrict__ Lw, const double* __rest
     if (g >= own_hi) return;
     const double qnan = __builtin_nan("");
     if (Lw[g] >= 0) {  // computed SNP (ldscalc.h:49-54)
-        l2[g] = 1.0 + l2_acc[g];
-        l2d[g] = dom ? l2d_acc[g] : qnan;
+        const int nanf = ws_acc[3 * (size_t)n_snp + g];
+        const long long a = reinterpret_cast<const long long*>(l2_acc)[g];
+        const long long d = reinterpret_cast<const long long*>(l2d_acc)[g];
+        l2[g] = (nanf & 1) ? qnan : 1.0 + (double)a / ACC_SCALE;
+        l2d[g] = dom && !(nanf & 2) ? (double)d / ACC_SCALE : qnan;
         ws3[g] = ws_acc[g];
         ws3[(size_t)n_snp + g] = dom ? ws_acc[(size_t)n_snp + g] : -1;
         ws3[2 * (size_t)n_snp + g] = dom ? ws_acc[2 * (size_t)n_snp + g] : -1;

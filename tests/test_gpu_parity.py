@@ -85,7 +85,7 @@ def test_sharded_runs_assemble_to_full(engine, name):
         if full[k].dtype.kind == "i":
             np.testing.assert_array_equal(parts[k], full[k], err_msg=k)
         else:
-            np.testing.assert_allclose(parts[k], full[k], rtol=1e-12, atol=1e-13, err_msg=k)
+            np.testing.assert_allclose(parts[k], full[k], rtol=1e-12, atol=3e-12, err_msg=k)
 
 
 def test_strict_plink_order(engine):
@@ -104,7 +104,7 @@ def test_additive_only(engine):
     from nldsc_amd import _lib
     full, *_ = run_set(engine, "n1002")
     got, *_ = run_set(engine, "n1002", flags=_lib.FLAG_ADDITIVE_ONLY)
-    np.testing.assert_allclose(got["l2"], full["l2"], rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(got["l2"], full["l2"], rtol=1e-12, atol=3e-12)
     np.testing.assert_array_equal(got["l2_ws"], full["l2_ws"])
     assert np.isnan(got["l2d"]).all()
     assert (got["l2d_ws"] == -1).all() and (got["l2d_wse"] == -1).all()
@@ -233,10 +233,10 @@ def test_full_size_block_edges_vs_oracle(engine, c3_slice, mode):
             assert np.max(np.abs(sub[k] - truth[k])) < 1e-8, k
     assert_ld_close(sub, exp, label="N=315599")
     assert (got["l2_ws"] > 100).all() and np.isfinite(got["l2"]).all()
+    # bit-reproducible: per-SNP sums across items are fixed-point integer atomics (order-independent)
     again = engine.run(*d["args"], pos, flags=MODES[mode])
-    np.testing.assert_array_equal(again["l2_ws"], got["l2_ws"])
-    np.testing.assert_array_equal(again["l2d_wse"], got["l2d_wse"])
-    np.testing.assert_allclose(again["l2"], got["l2"], rtol=1e-13)
+    for k in got:
+        np.testing.assert_array_equal(again[k], got[k], err_msg=k)
 
 
 @pytest.fixture(scope="module")
@@ -291,6 +291,9 @@ def test_c5_shape_1000kb_vs_oracle(engine, c5_slice, mode):
         for k in ("l2_ws", "l2d_ws", "l2d_wse"):
             np.testing.assert_array_equal(sub[k], truth[k], err_msg=k)
     assert np.isfinite(got["l2"]).all() and (got["l2_ws"] > 2000).all()
+    again = engine.run(*d["args"], pos, flags=MODES[mode])
+    for k in got:  # bit-reproducible run to run
+        np.testing.assert_array_equal(again[k], got[k], err_msg=k)
 
 
 @pytest.fixture(scope="module")
@@ -383,7 +386,7 @@ def test_segmented_f4_gram_is_bitwise_the_int8_gram(engine, N):
         same_gram(a, b, f"N={N}")
         c = engine.run(*args, flags=MODES["f4"] | _lib_flag("FLAG_ADDITIVE_ONLY"))
         np.testing.assert_array_equal(c["l2_ws"], a["l2_ws"])
-        np.testing.assert_allclose(c["l2"], a["l2"], rtol=1e-13, atol=1e-14)
+        np.testing.assert_allclose(c["l2"], a["l2"], rtol=1e-13, atol=3e-12)
 
 
 def same_gram(a, b, label):
@@ -391,7 +394,8 @@ def same_gram(a, b, label):
         np.testing.assert_array_equal(a[k], b[k], err_msg=f"{label} {k}")
     for k in ("l2", "l2d"):
         np.testing.assert_array_equal(np.isnan(a[k]), np.isnan(b[k]), err_msg=f"{label} {k}")
-        np.testing.assert_allclose(a[k], b[k], rtol=1e-13, atol=1e-14, equal_nan=True, err_msg=f"{label} {k}")
+        # the per-item partial sums enter the per-SNP totals in 2^-44 fixed point: <= ~40 quanta apart
+        np.testing.assert_allclose(a[k], b[k], rtol=1e-13, atol=3e-12, equal_nan=True, err_msg=f"{label} {k}")
 
 
 @pytest.mark.parametrize("order", ["sorted", "unsorted"])
@@ -465,7 +469,7 @@ def test_halo_loaded_shards_assemble_to_full(engine, tmp_path):
     for k in ("l2_ws", "l2d_ws", "l2d_wse", "maf", "residuals_std"):
         np.testing.assert_array_equal(got[k], full[k], err_msg=k)
     for k in ("l2", "l2d"):
-        np.testing.assert_allclose(got[k], full[k], rtol=1e-12, atol=1e-13, equal_nan=True, err_msg=k)
+        np.testing.assert_allclose(got[k], full[k], rtol=1e-12, atol=3e-12, equal_nan=True, err_msg=k)
 
 
 @pytest.mark.parametrize("seed", range(6))
