@@ -59,7 +59,8 @@ def format_scores(bim: BIMFile, ld, *, extra: bool = False) -> bytes:
     from .. import _lib
     cols = (bim.chr.reset_index(drop=True), bim.snp.reset_index(drop=True), bim.bp.reset_index(drop=True))
     n = len(cols[0])
-    if any(c.dtype.kind not in "iuO" for c in cols) or len(ld.l2) != n:
+    # pandas prints a null object cell (e.g. a SNP id read as NaN: 'NA', 'NULL') as an empty field, str() as 'nan'
+    if any(c.dtype.kind not in "iuO" or c.isna().any() for c in cols) or len(ld.l2) != n:
         buf = make_output(bim, ld, extra=extra).to_csv(sep="\t", index=False, float_format="%.5f")
         return buf.encode()
     text = [list(map(str, c.tolist())) for c in cols]  # what pandas prints for int64 / object cells

@@ -115,11 +115,13 @@ def test_native_tsv_writer_is_byte_identical_to_pandas(tmp_path):
     from nldsc_amd.ldscore.routine import format_scores, make_output
     rng = np.random.default_rng(3)
     n = 5000
-    for chrom in ("7", "X"):
+    for chrom in ("7", "X", "NA-ids"):
         path = tmp_path / f"t{chrom}.bim"
         with open(path, "w") as fh:
             for i in range(n):
-                fh.write(f"{chrom}\trs{i}\t{i * 0.001:.6f}\t{1000 + 37 * i}\tA\tG\n")
+                # pandas' default na_values read SNP ids such as 'NA' / 'NULL' as NaN (an object column with nulls)
+                snp = ("NA" if i % 7 == 0 else "NULL" if i % 11 == 0 else f"rs{i}") if chrom == "NA-ids" else f"rs{i}"
+                fh.write(f"{chrom if chrom != 'NA-ids' else '3'}\t{snp}\t{i * 0.001:.6f}\t{1000 + 37 * i}\tA\tG\n")
         bim = BIMFile(str(path))
 
         class LD:
