@@ -617,8 +617,9 @@ def test_rare_variants_reference_residual(engine, mode, n_org, strict):
     base = MODES[mode] | (_lib.FLAG_STRICT_PLINK_ORDER if strict else 0)
     engine.load_bed_bytes(bed, M, n_org)
     got = engine.run(*args, flags=base)
+    stats_ms = engine.timings()["stats_ms"]  # includes the replay kernel
     record(f"rare_{n_org}_{'strict' if strict else 'compat'}_{mode}",
-           dict(constant_residual=int(constant.sum()), replayed=int(replayed.sum()),
+           dict(constant_residual=int(constant.sum()), replayed=int(replayed.sum()), stats_ms=stats_ms,
                 constant_above_std_thr=int((orc["residuals_std"][constant] > 1e-5).sum()),
                 gpu_vs_oracle=max_errors(got, orc)))
     np.testing.assert_array_equal(got["residuals_std"][replayed], orc["residuals_std"][replayed])
