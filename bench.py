@@ -192,6 +192,9 @@ def main():
                          "position-sharded over the GPUs (strong scaling, what the BASELINE metric reads: chr1 at "
                          "1/2/4/8 GPUs)")
     ap.add_argument("--split", action="store_true", help=argparse.SUPPRESS)  # the default since round 2
+    ap.add_argument("--rehearse", default=None, metavar="R/N",
+                    help="one process on one GPU doing exactly what rank R of an N-GPU strong-scaling run does "
+                         "(its owned range + halo resident, its share of the chromosome), without the gather")
     ap.add_argument("--no-file", action="store_true",
                     help="skip the wall clock from a PLINK file (rank 0, N = 1: the synthetic .bed written to "
                          "$TMPDIR, then _ldscore.calculate timed from the file)")
@@ -233,7 +236,12 @@ def main():
     N, M = args.n_org, args.n_snp
     flags = (_lib.FLAG_ADDITIVE_ONLY if args.additive_only else 0) | getattr(_lib, PATHS[args.path][0])
     t = time.perf_counter()
-    split = world > 1 and not args.weak
+    s_rank, s_world = rank, world
+    if args.rehearse:
+        if world > 1:
+            raise SystemExit("--rehearse is a single-process mode")
+        s_rank, s_world = (int(x) for x in args.rehearse.split("/"))
+    split = s_world > 1 and not args.weak
     buf, pos = synth.device_bed(M, N, seed=7 if split else 7 + rank, length_cm=args.length_cm,
                                 missing=args.missing, device=local)
     eng = Engine(local)
@@ -241,8 +249,8 @@ def main():
     if split:
         # --split: ONE chromosome position-sharded over the ranks (strong scaling): rank g keeps only its
         # owned SNP range plus one window of halo rows resident and computes the owned SNPs
-        from nldsc_amd.distributed import gather_ranges, halo_range, shard_ranges
-        lo, hi = shard_ranges(pos, args.window_cm, world)[rank]
+        from nldsc_amd.distributed import gather_ranges, gather_spans, halo_range, shard_ranges
+        lo, hi = shard_ranges(pos, args.window_cm, s_world)[s_rank]
         a, b = halo_range(pos, args.window_cm, (lo, hi))
         nb = (N + 3) // 4
         sl = torch.cat([buf[:3], buf[3 + a * nb:3 + b * nb]])
@@ -251,6 +259,7 @@ def main():
         own, own_rel, pos = (lo, hi), (lo - a, hi - a), pos[a:b]
         full_local = {k: np.empty(M, np.float64 if k in ("l2", "l2d", "maf", "residuals_std") else np.int32)
                       for k in ("l2", "l2d", "maf", "residuals_std", "l2_ws", "l2d_ws", "l2d_wse")}
+        spans = gather_spans(own, device=coll) if world > 1 else None  # the sharding is fixed across steps
     else:
         eng.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
     bed_host = None
@@ -272,7 +281,8 @@ def main():
             for k, v in full_local.items():
                 v[own[0]:own[1]] = out[k][own_rel[0]:own_rel[1]]
             tg = time.perf_counter()
-            gather_ranges(full_local, own, M, device=coll)
+            if world > 1:
+                gather_ranges(full_local, own, M, device=coll, spans=spans)
             tim["gather_ms"] = 1e3 * (time.perf_counter() - tg)
             return tim
         out = eng.run(w, args.maf, args.std_thr, rsq, pos, flags=flags, out=out)
@@ -357,6 +367,8 @@ def main():
             "ms_per_step": 1e3 * t_max / args.steps,
             "higher_is_better": True,
             "scaling": "strong" if split else "weak",
+            **({"rehearsal": f"rank {s_rank} of {s_world} on one GPU (no gather): its owned SNPs / time"}
+               if args.rehearse else {}),
             "vs_baseline": None,
             "dtype": dtype,
             "data": "synthetic (GPU-generated PLINK .bed, AR(1) haplotypes, %g%% missing calls; %s)"

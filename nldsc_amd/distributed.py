@@ -79,33 +79,44 @@ def assign_units(work: Sequence[float], world: int) -> list[list[int]]:
     return out
 
 
-def gather_ranges(local: dict, own: tuple[int, int], n_snp: int, *, device=None) -> dict | None:
-    """Gather every rank's owned slice of the result table; the full table on rank 0, None elsewhere."""
+def gather_spans(own: tuple[int, int], *, device=None) -> list[tuple[int, int]]:
+    """Every rank's owned range (one small all_gather; constant for a given sharding, so callers that gather
+    repeatedly compute it once)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    span = torch.tensor([own[0], own[1]], dtype=torch.int64, device=device)
+    spans = torch.empty(world * 2, dtype=torch.int64, device=device)  # flat: gloo's shape rule
+    dist.all_gather_into_tensor(spans, span)
+    return [(int(a), int(b)) for a, b in spans.view(world, 2).cpu().tolist()]
+
+
+def gather_ranges(local: dict, own: tuple[int, int], n_snp: int, *, device=None,
+                  spans: list[tuple[int, int]] | None = None) -> dict | None:
+    """Gather every rank's owned slice of the result table; the full table on rank 0, None elsewhere.
+    One all_gather of a [world, 7, width] fp64 block (RCCL over xGMI with device tensors, gloo on CPU)."""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(), dist.get_rank()
+    spans = gather_spans(own, device=device) if spans is None else spans
     lo, hi = own
     n_own = hi - lo
-    span = torch.tensor([lo, hi], dtype=torch.int64, device=device)
-    spans = [torch.empty_like(span) for _ in range(world)]
-    dist.all_gather(spans, span)
-    width = max(int(s[1] - s[0]) for s in spans)
-    tab = np.full((len(RESULT_KEYS), max(width, 1)), np.nan)
+    width = max(max(b - a for a, b in spans), 1)
+    tab = np.full((len(RESULT_KEYS), width), np.nan)
     for k, key in enumerate(RESULT_KEYS):
         tab[k, :n_own] = np.asarray(local[key][lo:hi], dtype=np.float64)
     t = torch.from_numpy(tab)
     if device is not None:
-        t = t.to(device)
-    parts = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(parts, t)
+        t = t.to(device, non_blocking=False)
+    out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)  # flat: gloo's shape rule
+    dist.all_gather_into_tensor(out, t.reshape(-1))
     if rank != 0:
         return None
+    arr = out.view((world,) + tuple(t.shape)).cpu().numpy()
     full = empty_result(n_snp)
-    for s, part in zip(spans, parts):
-        a, b = int(s[0]), int(s[1])
-        arr = part.cpu().numpy()
+    for g, (a, b) in enumerate(spans):
         for k, key in enumerate(RESULT_KEYS):
-            v = arr[k, : b - a]
+            v = arr[g, k, : b - a]
             full[key][a:b] = v if full[key].dtype.kind == "f" else v.astype(np.int32)
     return full
 
