@@ -120,6 +120,9 @@ int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, d
 /* Path of the last run: 2 = exact Gram on fp4 MFMAs, 1 = exact Gram on int8 MFMAs, 0 = fp32;
  * *ops_alg_i8 = algorithmic ops of the exact formulation, 2N (2 sum WSA + 2 sum WSD). */
 int nldsc_engine_path(const nldsc_engine* e, int32_t* exact_i8, double* ops_alg_i8);
+/* K-split factor of the last run's fp4 band kernel: the number of K pieces each work item was split into
+ * (1 = single pass; > 1 for launches too small to fill the GPU, e.g. one rank's shard of a chromosome). */
+int nldsc_engine_ksplit(const nldsc_engine* e);
 
 /* Load SNP rows [snp_begin, snp_end) of a .bed file of n_snp_file SNPs as the engine's image
  * (snp_end - snp_begin SNPs; the run then takes the positions of that slice).  Position sharding

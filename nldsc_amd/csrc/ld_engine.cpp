@@ -124,6 +124,9 @@ struct nldsc_engine {
     DevBuf<nldsc::SnpConst> cst;
     DevBuf<uint8_t> sflags;
     DevBuf<uint8_t> blk_rep;  // per 32-SNP block: holds a rare variant with replayed fp32 vectors (KC items)
+    DevBuf<float> gram;       // K-split partial Gram tiles
+    bool ksplit_ok = true;    // $NLDSC_KSPLIT=0 disables the K-split
+    int last_ksplit = 1;
     DevBuf<double> pos, maf, rstd, l2_acc, l2d_acc, l2, l2d;
     DevBuf<int4> items;
     // host scratch
@@ -150,7 +153,7 @@ struct nldsc_engine {
         (void)hipSetDevice(device);
         bed.release(); lastb.release(); flip.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
         ws3.release(); lut.release(); cst.release(); sflags.release(); pos.release(); maf.release(); rstd.release();
-        l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release();
+        l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release(); gram.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         if (ev_plan) (void)hipEventDestroy(ev_plan);
         Ew.release(); plan_counts.release(); plan_meta.release(); plan_rows.release();
@@ -245,6 +248,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
         e->band_mode = std::strcmp(v, "f32") == 0 ? 0 : std::strcmp(v, "i8") == 0 ? 1 : 2;
     if (const char* v = std::getenv("NLDSC_GPU_PLAN")) e->gpu_plan = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_ORIENT")) e->orient = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_KSPLIT")) e->ksplit_ok = std::atoi(v) != 0;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
@@ -582,8 +586,30 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
                                        : blocks * (dom ? 3.0 : 1.0) - (dom ? 1.0 * n_diag : 0.0);
         e->flop_issued = products * 2.0 * BLK * BLK * (double)row_bytes * 4.0;
     }
+    // K-split (f4, unsegmented rows) when the items fill the wave slots (2 per SIMD) in few, partly empty
+    // rounds — a rank's shard of one chromosome — and splitting the K loop in P pieces fills them better
+    // Model: a round of items takes ~0.67 us per K chunk (C3: 2 466 chunks, 1.65 ms per round, 12.7 rounds in
+    // 20.9 ms); the split adds ~64 KiB of partial-tile traffic per piece at ~3 TB/s effective (measured: a 1/8
+    // shard of C3, 3 300 items, band 3.35 -> 3.01 ms; a 1/2 shard, 13 000 items, P = 5 made it 7.5 % slower).
+    int ksplit = 1;
+    if (use_f4 && n_items > 0 && n_it <= nldsc::F4_SEG_CHUNKS && e->ksplit_ok) {
+        const double slots = 8.0 * (double)e->n_cu, t_round = 0.67e-6 * n_it;
+        auto cost = [&](int P) {
+            return std::ceil((double)n_items * P / slots) / P * t_round + (P > 1 ? n_items * P * 65536.0 / 3e12 : 0.0);
+        };
+        double best = cost(1);
+        for (int P = 2; P <= 8 && 2 * P <= n_it; ++P)
+            if (cost(P) < 0.97 * best && (size_t)n_items * P * 32768 <= ((size_t)3 << 30)) { best = cost(P); ksplit = P; }
+    }
+    e->last_ksplit = ksplit;
+    if (ksplit > 1) HIPCHK(e->gram.ensure((size_t)n_items * ksplit * 8192));
     if (n_items > 0) {
-        if (use_f4)
+        if (use_f4 && ksplit > 1)
+            HIPCHK(nldsc::launch_band_f4_split(dom, ksplit, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p,
+                                               e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N,
+                                               p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p,
+                                               replay ? e->blk_rep.p : nullptr, e->gram.p, st));
+        else if (use_f4)
             HIPCHK(nldsc::launch_band_f4(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p,
                                          e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr,
                                          own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true,
@@ -664,6 +690,8 @@ int nldsc_engine_path(const nldsc_engine* e, int32_t* exact_i8, double* ops_alg_
     if (ops_alg_i8) *ops_alg_i8 = e->ops_alg_i8;
     return NLDSC_OK;
 }
+
+int nldsc_engine_ksplit(const nldsc_engine* e) { return e ? e->last_ksplit : NLDSC_E_ARG; }
 
 int nldsc_ld_calculate(const nldsc_ld_params* p, nldsc_ld_result* r, char* err, size_t errlen) {
     if (!p || !r || !p->bedfile) return set_err(err, errlen, NLDSC_E_ARG, "NULL argument");

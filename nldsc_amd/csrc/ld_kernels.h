@@ -70,6 +70,13 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
                           hipStream_t st);
+// the same with the K loop split in P pieces (small launches: better filled wave slots): partial Gram tiles to
+// `gram` (n_items * P * 8192 floats), then an epilogue kernel (unsegmented rows, n_it <= F4_SEG_CHUNKS)
+hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* geno, int pitch_words, int n_it,
+                                const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
+                                const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr,
+                                int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc,
+                                const uint8_t* blk_rep, float* gram, hipStream_t st);
 hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2d_acc, const int* ws_acc, int n_snp,
                            int own_lo, int own_hi, bool dom, double* l2, double* l2d, int* ws3, hipStream_t st);
 hipError_t launch_synth_bed(uint8_t* rows, int n_snp, int n_org, int nb, const float* thr, float rho, float missing,

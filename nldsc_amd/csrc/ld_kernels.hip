@@ -1237,14 +1237,17 @@ __device__ __forceinline__ f32x16v mfma_f4(const i32x4& a, const i32x4& b, const
 // samples each, so a segment adds at most 16 * 128 * SEG <= 2^23 to an entry and the fp32 accumulators stay
 // exact integers); after each segment the fp32 Gram is folded into int32 entries (add+dom) or its multiples
 // of 2^16 move to packed 16-bit counters (additive-only), exact while every entry is <= 16N < 2^31.
-template <bool DOM, int NC, bool DIAG0, int SEG, bool KC>
+// PART: K-split partial mode (small launches, see band_f4_part_kernel): run chunks [t_lo, t_hi) only and store
+// the 8 fp32 Gram tiles to `part` (exact integers) instead of running the epilogue.
+template <bool DOM, int NC, bool DIAG0, int SEG, bool KC, bool PART = false>
 __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const uint32_t* __restrict__ geno,
                                              int pitch_words, int n_it, const SnpConst* __restrict__ cst,
                                              const double* __restrict__ pos, const int* __restrict__ Lw,
                                              const int* __restrict__ Rw, const uint8_t* __restrict__ sflags,
                                              int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                                              int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
-                                             int* __restrict__ ws_acc, float* tr) {
+                                             int* __restrict__ ws_acc, float* tr, int t_lo = 0, int t_hi = 0,
+                                             float* __restrict__ part = nullptr) {
     constexpr int NS = 32 * (1 + NC);
     const int lane = threadIdx.x & 63;
     const int i = lane & 31, h = lane >> 5;
@@ -1356,7 +1359,19 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         else if (cm) kloop(std::false_type{}, std::true_type{}, t_lo, t_hi);
         else kloop(std::false_type{}, std::false_type{}, t_lo, t_hi);
     };
-    if constexpr (SEG == 0) {
+    if constexpr (PART) {
+        static_assert(SEG == 0 && NC == 1, "K-split: unsegmented single blocks");
+        run(t_lo, t_hi);
+        const f32x16v* tiles[8] = {&gxx[0], &gxo[0], &gox[0], &goo[0], &gxh[0], &goh[0], &ghx[0], &gho[0]};
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            float4* dst = reinterpret_cast<float4*>(part + t * 1024 + lane * 16);
+            const f32x16v v = *tiles[t];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dst[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        }
+        return;
+    } else if constexpr (SEG == 0) {
         run(0, n_it);
         if constexpr (DIAG0) {  // m.x(a, b) = x.m(b, a): lane (i, h) register r holds (row si(r), column i)
 #pragma unroll
@@ -1461,6 +1476,106 @@ __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __rest
                                          n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, tr)
     if (it.y == it.x) NLDSC_BODY(true); else NLDSC_BODY(false);
 #undef NLDSC_BODY
+}
+
+// K-split for small launches (a rank's shard of one chromosome: ~3 300 items for 2 048 wave slots leave the
+// second round of items 60 % full).  Unit u = item * P + piece runs K chunks [piece n_it / P, (piece + 1) n_it / P)
+// (even-aligned) and stores its 8 Gram tiles (32 KiB) to gram + u * 8192; band_f4_epi_kernel adds the P partial
+// tiles of each item in piece order — integers below 2^24 (N < 2^19), so the fp32 sums are exact and equal to the
+// single-pass Gram — and runs the usual epilogue.
+template <bool DOM>
+__global__ void __launch_bounds__(64, 2) band_f4_part_kernel(const uint32_t* __restrict__ geno, int pitch_words,
+                                                           int n_it, const SnpConst* __restrict__ cst,
+                                                           const int4* __restrict__ items,
+                                                           const double* __restrict__ pos, const int* __restrict__ Lw,
+                                                           const int* __restrict__ Rw,
+                                                           const uint8_t* __restrict__ sflags, int n_snp, int P,
+                                                           float* __restrict__ gram) {
+    __shared__ BandI8Lds sh;
+    __shared__ float tr[32 * 33];
+    const int u = xcd_slot(blockIdx.x, gridDim.x), item = u / P, piece = u % P;
+    const int4 it = items[item];
+    const int t_lo = (int)(((long long)piece * n_it / P) & ~1LL);
+    const int t_hi = piece == P - 1 ? n_it : (int)(((long long)(piece + 1) * n_it / P) & ~1LL);
+    float* part = gram + (size_t)u * 8192;
+#define NLDSC_BODY(DIAG_)                                                                                             \
+    band_f4_body<DOM, 1, DIAG_, 0, false, true>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp,     \
+                                                0.0, 0.0, 0.0, 0, 0, nullptr, nullptr, nullptr, tr, t_lo, t_hi, part)
+    if (it.y == it.x) NLDSC_BODY(true); else NLDSC_BODY(false);
+#undef NLDSC_BODY
+}
+
+template <bool DOM, bool KC>
+__global__ void __launch_bounds__(64, 2) band_f4_epi_kernel(const SnpConst* __restrict__ cst,
+                                                          const int4* __restrict__ items,
+                                                          const double* __restrict__ pos, const int* __restrict__ Lw,
+                                                          const int* __restrict__ Rw,
+                                                          const uint8_t* __restrict__ sflags, int n_snp,
+                                                          double ld_wind, double n_org, double rsq_thr, int own_lo,
+                                                          int own_hi, double* __restrict__ l2_acc,
+                                                          double* __restrict__ l2d_acc, int* __restrict__ ws_acc,
+                                                          const uint8_t* __restrict__ blk_rep, int P,
+                                                          const float* __restrict__ gram) {
+    __shared__ BandI8Lds sh;
+    __shared__ float tr[32 * 33];
+    const int4 it = items[blockIdx.x];
+    if (skip_item<KC>(blk_rep, it)) return;
+    const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
+    const int I = it.x, J = it.y;
+    const bool diag = I == J;
+    for (int s = lane; s < 64; s += 64) {
+        const int g = s < 32 ? I * 32 + s : J * 32 + (s & 31);
+        SnpSlot si;
+        si.g = g;
+        if (g < n_snp) {
+            si.pos = pos[g]; si.L = Lw[g]; si.R = Rw[g]; si.fl = sflags[g];
+        } else {
+            si.pos = 0.0; si.L = -1; si.R = -2; si.fl = 0;
+        }
+        sh.info[s] = si;
+        sh.cst[s] = cst[g];
+        sh.l2[s] = 0.0; sh.l2d[s] = 0.0;
+        sh.wsa[s] = 0; sh.wsd[s] = 0; sh.wse[s] = 0;
+    }
+    f32x16v g8[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) g8[t] = f32x16v{};
+    const float* src = gram + (size_t)blockIdx.x * P * 8192 + lane * 16;
+    for (int p = 0; p < P; ++p)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const float4* q = reinterpret_cast<const float4*>(src + (size_t)p * 8192 + t * 1024);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 v = q[k];
+                g8[t][4 * k] += v.x; g8[t][4 * k + 1] += v.y; g8[t][4 * k + 2] += v.z; g8[t][4 * k + 3] += v.w;
+            }
+        }
+    __syncthreads();
+    if (diag) {  // m.x(a, b) = x.m(b, a)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tr[((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + i] = g8[1][r];
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) g8[2][r] = tr[i * 33 + (r & 3) + 8 * (r >> 2) + 4 * h];
+    }
+    pair_epilogue<DOM, f32x16v, true, KC>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32, diag, i, h,
+                                          g8[0], g8[1], g8[2], g8[3], g8[4], g8[5], g8[6], g8[7], ld_wind, n_org,
+                                          rsq_thr, n_org);
+    __syncthreads();
+    for (int s = lane; s < 64; s += 64) {
+        const int g = sh.info[s].g;
+        if (g < own_lo || g >= own_hi || g >= n_snp) continue;
+        if (sh.wsa[s]) {
+            acc_fixed(&l2_acc[g], &ws_acc[3 * (size_t)n_snp + g], 1, sh.l2[s]);
+            atomicAdd(&ws_acc[g], sh.wsa[s]);
+        }
+        if (DOM && sh.wsd[s]) {
+            acc_fixed(&l2d_acc[g], &ws_acc[3 * (size_t)n_snp + g], 2, sh.l2d[s]);
+            atomicAdd(&ws_acc[(size_t)n_snp + g], sh.wsd[s]);
+            if (sh.wse[s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + g], sh.wse[s]);
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1647,6 +1762,27 @@ hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* gen
     if (dom) NLDSC_BAND(true, false); else NLDSC_BAND(false, false);
     if (blk_rep) { if (dom) NLDSC_BAND(true, true); else NLDSC_BAND(false, true); }
 #undef NLDSC_BAND
+    return hipGetLastError();
+}
+
+hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* geno, int pitch_words, int n_it,
+                                const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
+                                const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr,
+                                int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc,
+                                const uint8_t* blk_rep, float* gram, hipStream_t st) {
+    if (n_items <= 0) return hipSuccess;
+    if (n_it > F4_SEG_CHUNKS || P < 1 || 2 * P > n_it) return hipErrorInvalidValue;
+    const dim3 grid_p((unsigned)n_items * (unsigned)P);
+    if (dom) hipLaunchKernelGGL((band_f4_part_kernel<true>), grid_p, dim3(64), 0, st, geno, pitch_words, n_it, cst,
+                                items, pos, Lw, Rw, sflags, n_snp, P, gram);
+    else hipLaunchKernelGGL((band_f4_part_kernel<false>), grid_p, dim3(64), 0, st, geno, pitch_words, n_it, cst,
+                            items, pos, Lw, Rw, sflags, n_snp, P, gram);
+#define NLDSC_EPI(DOM_, KC_)                                                                                        \
+    hipLaunchKernelGGL((band_f4_epi_kernel<DOM_, KC_>), dim3(n_items), dim3(64), 0, st, cst, items, pos, Lw, Rw,    \
+                       sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, blk_rep, P, gram)
+    if (dom) NLDSC_EPI(true, false); else NLDSC_EPI(false, false);
+    if (blk_rep) { if (dom) NLDSC_EPI(true, true); else NLDSC_EPI(false, true); }
+#undef NLDSC_EPI
     return hipGetLastError();
 }
 

@@ -98,7 +98,8 @@ class Engine:
         d.update(flop_alg=flop.value, flop_issued=issued.value, pairs=pairs.value, band_items=nl.value)
         ex, ops = ctypes.c_int32(), ctypes.c_double()
         self._L.nldsc_engine_path(self._h, ctypes.byref(ex), ctypes.byref(ops))
-        d.update(exact_i8=ex.value > 0, path={0: "f32", 1: "i8", 2: "f4"}[ex.value], ops_alg_i8=ops.value)
+        d.update(exact_i8=ex.value > 0, path={0: "f32", 1: "i8", 2: "f4"}[ex.value], ops_alg_i8=ops.value,
+                 ksplit=self._L.nldsc_engine_ksplit(self._h))
         return d
 
 

@@ -632,3 +632,41 @@ def test_rare_variants_reference_residual(engine, mode, n_org, strict):
     assert_ld_close(exact, truth, **({"tol": tol} if tol else {}), label=f"rare exact N={n_org} {mode}")
     if constant.any():
         assert (got["l2d_ws"] != exact["l2d_ws"]).any()  # the noise residuals are counted by default
+
+
+@pytest.mark.parametrize("N,M,dom", [(20_001, 1500, True), (20_001, 1500, False), (4096, 700, True)])
+def test_ksplit_equals_single_pass(engine, N, M, dom):
+    """Launches too small to fill the GPU (a rank's shard) split every item's K loop into P pieces whose exact
+    integer Gram tiles are summed by an epilogue kernel: every output is bitwise the single-pass one
+    ($NLDSC_KSPLIT=0), and both equal the fp64 truth."""
+    import os
+
+    from nldsc_amd import synth
+    from nldsc_amd.engine import Engine
+    spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=6.0, seed=N + M, missing=0.02)
+    rows = synth.pack_bed_rows(synth.genotypes(spec))
+    pos = synth.positions_cm(spec)
+    flags = MODES["f4"] | _lib_flag("FLAG_EXACT_RARE") | (0 if dom else _lib_flag("FLAG_ADDITIVE_ONLY"))
+    args = (1.0, 0.01, 1e-5, 1.0 / M, pos)
+    engine.load_bed_bytes(synth.bed_bytes(rows), M, N)
+    got = engine.run(*args, flags=flags)
+    assert engine.timings()["ksplit"] > 1
+    old = os.environ.get("NLDSC_KSPLIT")
+    os.environ["NLDSC_KSPLIT"] = "0"
+    try:
+        with Engine(0) as e:
+            e.load_bed_bytes(synth.bed_bytes(rows), M, N)
+            ref = e.run(*args, flags=flags)
+            assert e.timings()["ksplit"] == 1
+    finally:
+        if old is None:
+            os.environ.pop("NLDSC_KSPLIT")
+        else:
+            os.environ["NLDSC_KSPLIT"] = old
+    for k in got:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    exp = O.run_f64(rows, N, *args)
+    if not dom:
+        exp = dict(exp, l2d=np.full(M, np.nan), l2d_ws=np.full(M, -1, np.int32), l2d_wse=np.full(M, -1, np.int32))
+    assert_ld_close(got, exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
+                                       maf=(0.0, 0.0)), label=f"ksplit N={N}")
