@@ -110,6 +110,8 @@ struct nldsc_engine {
     hipEvent_t ev_pos = nullptr;        // positions uploaded (the schedule's only input)
     hipEvent_t ev[6] = {};
     hipEvent_t ev_plan = nullptr;  // GPU plan counters landed in h_meta
+    hipEvent_t ev_stats = nullptr;   // SNP constants and replay flags written (the replay's inputs)
+    hipEvent_t ev_replay = nullptr;  // replayed constants written (the KC launch and finalize wait on it)
     // resident .bed image
     DevBuf<uint8_t> bed;
     DevBuf<uint8_t> lastb;  // each row's original last byte (the per-run count kernel masks a copy of it)
@@ -126,6 +128,7 @@ struct nldsc_engine {
     DevBuf<uint8_t> blk_rep;  // per 32-SNP block: holds a rare variant with replayed fp32 vectors (KC items)
     DevBuf<float> gram;       // K-split partial Gram tiles
     bool ksplit_ok = true;    // $NLDSC_KSPLIT=0 disables the K-split
+    bool replay_overlap = true;  // $NLDSC_REPLAY_OVERLAP=0 runs the rare-variant replay in line on the main stream
     int last_ksplit = 1;
     DevBuf<double> pos, maf, rstd, l2_acc, l2d_acc, l2, l2d;
     DevBuf<int4> items;
@@ -160,6 +163,8 @@ struct nldsc_engine {
         if (stream) (void)hipStreamDestroy(stream);
         if (plan_stream) (void)hipStreamDestroy(plan_stream);
         if (ev_pos) (void)hipEventDestroy(ev_pos);
+        if (ev_stats) (void)hipEventDestroy(ev_stats);
+        if (ev_replay) (void)hipEventDestroy(ev_replay);
     }
 };
 
@@ -249,6 +254,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_GPU_PLAN")) e->gpu_plan = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_ORIENT")) e->orient = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_KSPLIT")) e->ksplit_ok = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_REPLAY_OVERLAP")) e->replay_overlap = std::atoi(v) != 0;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
@@ -260,6 +266,8 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     for (auto& ev : e->ev)
         if (he == hipSuccess) he = hipEventCreate(&ev);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_plan, hipEventDisableTiming);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_stats, hipEventDisableTiming);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_replay, hipEventDisableTiming);
     if (he != hipSuccess) {
         delete e;
         return set_err(err, errlen, NLDSC_E_HIP, "HIP error %s creating stream/events", hipGetErrorString(he));
@@ -495,12 +503,21 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     HIPCHK(hipEventRecord(e->ev[1], st));
     HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->oriented ? e->flip.p : nullptr, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->cst.p,
                                    e->sflags.p, e->maf.p, e->rstd.p, st));
-    // rare variants: the reference's fp32 residual replayed (its sums assume N < 2^23)
+    // rare variants: the reference's fp32 residual replayed (its sums assume N < 2^23).  The flags go first on
+    // the main stream; the replay itself (a few long sequential sums) runs on the plan stream beside the band
+    // launch for the items without a replayed SNP, and only the KC launch and finalize wait for it.
     const bool replay = N < (1 << 23) && !(p->flags & NLDSC_FLAG_EXACT_RARE);
-    if (replay)
+    if (replay) {
+        HIPCHK(nldsc::launch_replay_flags(e->counts.p, e->oriented ? e->flip.p : nullptr, e->sflags.p, M,
+                                          e->blk_rep.p, st));
+        hipStream_t rs = e->replay_overlap ? e->plan_stream : st;
+        HIPCHK(hipEventRecord(e->ev_stats, st));
+        HIPCHK(hipStreamWaitEvent(rs, e->ev_stats, 0));
         HIPCHK(nldsc::launch_reference_residuals(e->bed.p, row_bytes, N, strict, e->counts.p,
                                                  e->oriented ? e->flip.p : nullptr, M, p->std_thr, e->cst.p, e->lut.p,
-                                                 e->sflags.p, e->rstd.p, e->blk_rep.p, st));
+                                                 e->sflags.p, e->rstd.p, rs));
+        HIPCHK(hipEventRecord(e->ev_replay, rs));
+    }
     HIPCHK(hipEventRecord(e->ev[2], st));
 
     // ---- window replay + schedule ----
@@ -603,24 +620,34 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     }
     e->last_ksplit = ksplit;
     if (ksplit > 1) HIPCHK(e->gram.ensure((size_t)n_items * ksplit * 8192));
-    if (n_items > 0) {
+    // which = 1: the launch for the items without a replayed SNP (beside the replay), 2: the KC launch after it
+    const uint8_t* blk_rep = replay ? e->blk_rep.p : nullptr;
+    auto launch_band_path = [&](int which) -> hipError_t {
         if (use_f4 && ksplit > 1)
-            HIPCHK(nldsc::launch_band_f4_split(dom, ksplit, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p,
+            return nldsc::launch_band_f4_split(dom, ksplit, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p,
                                                e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N,
                                                p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p,
-                                               replay ? e->blk_rep.p : nullptr, e->gram.p, st));
-        else if (use_f4)
-            HIPCHK(nldsc::launch_band_f4(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p,
+                                               blk_rep, e->gram.p, which, st);
+        if (use_f4)
+            return nldsc::launch_band_f4(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p,
                                          e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr,
-                                         own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true,
-                                         replay ? e->blk_rep.p : nullptr, st));
-        else if (use_i8)
-            HIPCHK(nldsc::launch_band_i8(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p,
-                                         e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
-                                         (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
-                                         e->ws_acc.p, true, replay ? e->blk_rep.p : nullptr, st));
-        else
-            HIPCHK(nldsc::launch_band(dom, 2, n_items, geno, pitch_words, n_it,
+                                         own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true, blk_rep,
+                                         which, st);
+        return nldsc::launch_band_i8(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p, e->pos.p,
+                                     e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin,
+                                     own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true, blk_rep, which, st);
+    };
+    if (n_items > 0 && (use_f4 || use_i8)) {
+        HIPCHK(launch_band_path(1));
+        if (replay) {
+            HIPCHK(hipStreamWaitEvent(st, e->ev_replay, 0));
+            HIPCHK(launch_band_path(2));
+        }
+    } else if (replay) {
+        HIPCHK(hipStreamWaitEvent(st, e->ev_replay, 0));  // the fp32 path reads the replayed tables everywhere
+    }
+    if (n_items > 0 && !use_f4 && !use_i8) {
+        HIPCHK(nldsc::launch_band(dom, 2, n_items, geno, pitch_words, n_it,
                                       e->lut.p, e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
                                       (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                       e->ws_acc.p, st));

@@ -36,9 +36,12 @@ hipError_t launch_snp_stats(const int* counts, const uint8_t* flip, const double
 // residual std, residual-pass flag bit 2, exact constants and fp32 table of the reference's fp32 residual,
 // replayed in its arithmetic (ld_kernels.hip reference_residual_kernel)
 constexpr int REF_RESIDUAL_MIN_CLASS = 16;
+// blk_rep[block] = 1 for blocks holding such SNPs (cheap; first), then the replay itself (long, few waves)
+hipError_t launch_replay_flags(const int* counts, const uint8_t* flip, const uint8_t* sflags, int n_snp,
+                              uint8_t* blk_rep, hipStream_t st);
 hipError_t launch_reference_residuals(const uint8_t* img, int row_bytes, int n_org, bool strict, const int* counts,
                                      const uint8_t* flip, int n_snp, double std_thr, SnpConst* cst, float2* lut,
-                                     uint8_t* sflags, double* rstd_out, uint8_t* blk_rep, hipStream_t st);
+                                     uint8_t* sflags, double* rstd_out, hipStream_t st);
 // after a load: swap 00 <-> 11 in rows (and saved last bytes) with more hom-A2 than hom-A1 calls; flip[j] = 1
 hipError_t launch_orient_rows(uint8_t* img, uint8_t* last, int n_snp, int row_bytes, uint8_t* flip, hipStream_t st);
 // exact left pointers L from the all-pass replay's A and the device MAF flags (sorted positions)
@@ -58,25 +61,25 @@ hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
-                          hipStream_t st);
+                          int which, hipStream_t st);
 // K-loop chunks (128 samples each) per fp32 accumulation segment of the fp4 path: rows longer than this
 // (N > 2^19) run the segmented kernel, which folds the fp32 Gram into int32 after every segment
 constexpr int F4_SEG_CHUNKS = 4096;
 // exact path on fp4 MFMAs (N < 2^27), items (I, J0, 1, 0) (max_nc must be 1).  blk_rep (or nullptr): per 32-SNP
 // block, 1 if a SNP carries replayed fp32 vectors (ka / kr != 0): its items run in a second launch (the exact
-// kernels' KC instantiation)
+// kernels' KC instantiation).  which: 1 the main launch (items of other blocks), 2 the KC launch, 3 both
 hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
-                          hipStream_t st);
+                          int which, hipStream_t st);
 // the same with the K loop split in P pieces (small launches: better filled wave slots): partial Gram tiles to
 // `gram` (n_items * P * 8192 floats), then an epilogue kernel (unsegmented rows, n_it <= F4_SEG_CHUNKS)
 hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                                 const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                                 const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr,
                                 int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc,
-                                const uint8_t* blk_rep, float* gram, hipStream_t st);
+                                const uint8_t* blk_rep, float* gram, int which, hipStream_t st);
 hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2d_acc, const int* ws_acc, int n_snp,
                            int own_lo, int own_hi, bool dom, double* l2, double* l2d, int* ws3, hipStream_t st);
 hipError_t launch_synth_bed(uint8_t* rows, int n_snp, int n_org, int nb, const float* thr, float rho, float missing,

@@ -439,20 +439,34 @@ __device__ float ref_mean_finish(int n, float acc, int first, float* sh) {
     return (sh[first] + sh[first + 1]) / (float)n;
 }
 
+// the SNPs the replay handles: MAF-passing, observed, at most REF_RESIDUAL_MIN_CLASS calls in a genotype class
+__device__ __forceinline__ bool replayed_snp(const int* counts, const uint8_t* flip, const uint8_t* sflags, int j) {
+    if (!(sflags[j] & 1)) return false;  // MAF-failed or unused: no residual
+    const int s0 = counts[4 * (size_t)j], c1 = counts[4 * (size_t)j + 1], s2 = counts[4 * (size_t)j + 2];
+    (void)flip;  // the class counts do not depend on the stored orientation
+    return s0 + c1 + s2 > 0 && min(s0, min(c1, s2)) <= REF_RESIDUAL_MIN_CLASS;
+}
+
+// per 32-SNP block: does it hold a replayed SNP?  Cheap and first, so that the band launch for the other items
+// (KC = false) can run while reference_residual_kernel's long sequential sums run beside it.
+__global__ void replay_flags_kernel(const int* __restrict__ counts, const uint8_t* __restrict__ flip,
+                                    const uint8_t* __restrict__ sflags, int n_snp, uint8_t* __restrict__ blk_rep) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n_snp && replayed_snp(counts, flip, sflags, j)) blk_rep[j >> 5] = 1;
+}
+
 __global__ void __launch_bounds__(64) reference_residual_kernel(const uint8_t* __restrict__ img, int row_bytes,
                                                                 int n_org, int strict, const int* __restrict__ counts,
                                                                 const uint8_t* __restrict__ flip, int n_snp,
                                                                 double std_thr, SnpConst* __restrict__ cst,
                                                                 float2* __restrict__ lut, uint8_t* __restrict__ sflags,
-                                                                double* __restrict__ rstd_out,
-                                                                uint8_t* __restrict__ blk_rep) {
+                                                                double* __restrict__ rstd_out) {
 #pragma clang fp contract(off)
     const int j = blockIdx.x;
-    if (j >= n_snp || !(sflags[j] & 1)) return;  // MAF-failed or unused: no residual
+    if (j >= n_snp || !replayed_snp(counts, flip, sflags, j)) return;
     const int s0 = counts[4 * (size_t)j], c1 = counts[4 * (size_t)j + 1], s2 = counts[4 * (size_t)j + 2];
     const bool fj = flip != nullptr && flip[j];
     const int c0 = fj ? s2 : s0, c2 = fj ? s0 : s2;
-    if (c0 + c1 + c2 == 0 || min(c0, min(c1, c2)) > REF_RESIDUAL_MIN_CLASS) return;
     __shared__ uint32_t buf[REF_CHUNK / 4];
     __shared__ float2 tab[4 * 256];
     __shared__ float sh[72];
@@ -494,7 +508,6 @@ __global__ void __launch_bounds__(64) reference_residual_kernel(const uint8_t* _
     const float sd_a = (float)sqrt((double)var_a);
     if ((threadIdx.x & 63) != 0) return;
     rstd_out[j] = (double)sd;
-    blk_rep[j >> 5] = 1;  // its band items take the KC epilogue
     SnpConst K = cst[j];
     float2* L = lut + (size_t)j * 4;
     // stored codes 00, 10, 11 (slots 0, 2, 3 of the tables) and their call counts; missing is slot 1
@@ -1690,14 +1703,22 @@ hipError_t launch_snp_stats(const int* counts, const uint8_t* flip, const double
     return hipGetLastError();
 }
 
-hipError_t launch_reference_residuals(const uint8_t* img, int row_bytes, int n_org, bool strict, const int* counts,
-                                     const uint8_t* flip, int n_snp, double std_thr, SnpConst* cst, float2* lut,
-                                     uint8_t* sflags, double* rstd_out, uint8_t* blk_rep, hipStream_t st) {
+hipError_t launch_replay_flags(const int* counts, const uint8_t* flip, const uint8_t* sflags, int n_snp,
+                              uint8_t* blk_rep, hipStream_t st) {
     if (n_snp <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(blk_rep, 0, (size_t)(n_snp + 31) / 32, st);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(replay_flags_kernel, dim3((n_snp + 255) / 256), dim3(256), 0, st, counts, flip, sflags, n_snp,
+                       blk_rep);
+    return hipGetLastError();
+}
+
+hipError_t launch_reference_residuals(const uint8_t* img, int row_bytes, int n_org, bool strict, const int* counts,
+                                     const uint8_t* flip, int n_snp, double std_thr, SnpConst* cst, float2* lut,
+                                     uint8_t* sflags, double* rstd_out, hipStream_t st) {
+    if (n_snp <= 0) return hipSuccess;
     hipLaunchKernelGGL(reference_residual_kernel, dim3(n_snp), dim3(64), 0, st, img, row_bytes, n_org, (int)strict,
-                       counts, flip, n_snp, std_thr, cst, lut, sflags, rstd_out, blk_rep);
+                       counts, flip, n_snp, std_thr, cst, lut, sflags, rstd_out);
     return hipGetLastError();
 }
 
@@ -1752,15 +1773,15 @@ hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
-                          hipStream_t st) {
+                          int which, hipStream_t st) {
     if (n_items <= 0) return hipSuccess;
     if (max_nc != 1) return hipErrorInvalidValue;  // single block-pair items
 #define NLDSC_BAND(DOM_, KC_)                                                                                       \
     hipLaunchKernelGGL((band_i8_kernel<DOM_, KC_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words, n_it, cst,    \
                        items, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, \
                        ws_acc, xcd ? 1 : 0, blk_rep)
-    if (dom) NLDSC_BAND(true, false); else NLDSC_BAND(false, false);
-    if (blk_rep) { if (dom) NLDSC_BAND(true, true); else NLDSC_BAND(false, true); }
+    if (which & 1) { if (dom) NLDSC_BAND(true, false); else NLDSC_BAND(false, false); }
+    if (blk_rep && (which & 2)) { if (dom) NLDSC_BAND(true, true); else NLDSC_BAND(false, true); }
 #undef NLDSC_BAND
     return hipGetLastError();
 }
@@ -1769,10 +1790,11 @@ hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* ge
                                 const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                                 const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr,
                                 int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc,
-                                const uint8_t* blk_rep, float* gram, hipStream_t st) {
+                                const uint8_t* blk_rep, float* gram, int which, hipStream_t st) {
     if (n_items <= 0) return hipSuccess;
     if (n_it > F4_SEG_CHUNKS || P < 1 || 2 * P > n_it) return hipErrorInvalidValue;
     const dim3 grid_p((unsigned)n_items * (unsigned)P);
+    if (!(which & 1)) goto kc;  // the partial tiles of every item come from the main launch
     if (dom) hipLaunchKernelGGL((band_f4_part_kernel<true>), grid_p, dim3(64), 0, st, geno, pitch_words, n_it, cst,
                                 items, pos, Lw, Rw, sflags, n_snp, P, gram);
     else hipLaunchKernelGGL((band_f4_part_kernel<false>), grid_p, dim3(64), 0, st, geno, pitch_words, n_it, cst,
@@ -1781,7 +1803,8 @@ hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* ge
     hipLaunchKernelGGL((band_f4_epi_kernel<DOM_, KC_>), dim3(n_items), dim3(64), 0, st, cst, items, pos, Lw, Rw,    \
                        sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, blk_rep, P, gram)
     if (dom) NLDSC_EPI(true, false); else NLDSC_EPI(false, false);
-    if (blk_rep) { if (dom) NLDSC_EPI(true, true); else NLDSC_EPI(false, true); }
+kc:
+    if (blk_rep && (which & 2)) { if (dom) NLDSC_EPI(true, true); else NLDSC_EPI(false, true); }
 #undef NLDSC_EPI
     return hipGetLastError();
 }
@@ -1790,7 +1813,7 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
-                          hipStream_t st) {
+                          int which, hipStream_t st) {
     if (n_items <= 0) return hipSuccess;
     if (max_nc != 1) return hipErrorInvalidValue;  // single block-pair items
 #define NLDSC_BAND(DOM_, WPS_, SEG_, KC_)                                                                           \
@@ -1802,8 +1825,8 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
     else if (dom) NLDSC_BAND(true, 2, 0, KC_);                                                                       \
     else NLDSC_BAND(false, 2, 0, KC_)
     // segmented kernel: the add+dom variant needs more than 256 registers (2 waves / SIMD would spill)
-    NLDSC_PICK(false);
-    if (blk_rep) { NLDSC_PICK(true); }
+    if (which & 1) { NLDSC_PICK(false); }
+    if (blk_rep && (which & 2)) { NLDSC_PICK(true); }
 #undef NLDSC_PICK
 #undef NLDSC_BAND
     return hipGetLastError();
