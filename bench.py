@@ -42,6 +42,24 @@ PATHS = {
 }
 
 
+def band_kernel_name(variant: str, dom: bool, default: str) -> str:
+    """The band kernel that ran (Engine.timings()['band_kernel']) as rocprof names it, with what it issues."""
+    d = "true" if dom else "false"
+    names = {
+        "f4_2x2": f"band_f4_t2_kernel<{d}, 4, false> (4-wave workgroups over 2x2 block pairs sharing their strips "
+                  "through LDS, global_load_lds ring; v_mfma_scale_f32_32x32x64_f8f6f4, e2m1 operands, exact integer "
+                  "Gram in fp32)",
+        "f4_routed": f"band_f4_t2_kernel<{d}, 4, false> for missing-free 2x2 super-items (4-wave workgroups sharing "
+                     f"their strips through LDS) + band_f4_kernel<{d}, 2, 0, false> for the rest (one wave per 32x32 "
+                     "block pair); v_mfma_scale_f32_32x32x64_f8f6f4, e2m1 operands, exact integer Gram in fp32",
+        "f4": f"band_f4_kernel<{d}, 2, 0, false> (one wave per 32x32 block pair; v_mfma_scale_f32_32x32x64_f8f6f4, "
+              "e2m1 operands, exact integer Gram in fp32)",
+        "f4_ksplit": f"band_f4_part_kernel<{d}> + band_f4_epi_kernel (K-split; v_mfma_scale_f32_32x32x64_f8f6f4)",
+        "f4_seg": f"band_f4_kernel<{d}, ., 4096, false> (segmented K loop; v_mfma_scale_f32_32x32x64_f8f6f4)",
+    }
+    return names.get(variant, default.replace("<true>", f"<{d}>"))
+
+
 def kernel_source_sha16() -> str:
     """Fingerprint of the kernels' source (a PMC summary counts only for the kernels it was measured on)."""
     import hashlib
@@ -72,9 +90,11 @@ def pmc_traffic(kernel_key: str, n_org: int, n_snp: int, missing: float):
         if doc.get("kernels_source_sha16") != sha:
             stale = stale or os.path.relpath(path, REPO)
             continue
-        for name, k in doc.get("kernels", {}).items():
-            if name.startswith(kernel_key):
-                return k["traffic_bytes"], os.path.relpath(path, REPO)
+        keys = [kernel_key] if isinstance(kernel_key, str) else list(kernel_key)
+        found = [k["traffic_bytes"] for name, k in doc.get("kernels", {}).items()
+                 if any(name.startswith(key + "<") or name == key for key in keys)]
+        if found:  # (the routed fp4 band: both kernels' bytes per launch pair)
+            return float(sum(found)), os.path.relpath(path, REPO)
     return None, (f"no PMC summary of the current kernels (source sha {sha}); newest for this workload: {stale}"
                   if stale else "no PMC summary for this workload")
 
@@ -329,6 +349,7 @@ def main():
         flop = tims[-1]["flop_alg"]
         path = tims[-1]["path"]
         _, peak, unit, kname, dtype = PATHS[path]
+        kname = band_kernel_name(tims[-1].get("band_kernel", path), not args.additive_only, kname)
         # roofline on SURVEY.md §8(d3)'s basis for every path: FLOP_alg = 2N(1/2 sumWSA + sumWSD) (the reference
         # formulation's multiply-adds) over the band kernel's time, against the dense MFMA peak of the dtype
         # that ran.  The exact paths issue more: 8 integer Gram entries per pair (frac_8_product_basis).
@@ -344,7 +365,9 @@ def main():
                         ops_8_product_definition="2N(4*(1/2)sumWSA + 2*sumWSD): the exact formulation's 8 integer "
                                                  "Gram entries per pair (vv, vm, mv, mm additive; vh, mh, hv, hm "
                                                  "dominance), skipped products of missing-free blocks included")
-        traffic, traffic_src = pmc_traffic(kname.split("<")[0], N, M, args.missing)
+        traffic, traffic_src = pmc_traffic(
+            ("band_f4_t2_kernel", "band_f4_kernel") if tims[-1].get("band_kernel") == "f4_routed" else kname.split("<")[0],
+            N, M, args.missing)
         roof.update(traffic=traffic, traffic_source=traffic_src,
                     algorithmic_bytes_per_launch=eng.n_snp * 4 * ((((N + 3) // 4) + 31) // 32 * 8),
                     avg_launch_ms=band_ms,

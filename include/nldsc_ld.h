@@ -123,6 +123,19 @@ int nldsc_engine_path(const nldsc_engine* e, int32_t* exact_i8, double* ops_alg_
 /* K-split factor of the last run's fp4 band kernel: the number of K pieces each work item was split into
  * (1 = single pass; > 1 for launches too small to fill the GPU, e.g. one rank's shard of a chromosome). */
 int nldsc_engine_ksplit(const nldsc_engine* e);
+/* Band kernel of the last run: NLDSC_BAND_F32 (fp32 MFMA GEMM), NLDSC_BAND_I8, NLDSC_BAND_F4 (one wave per
+ * 32x32 block pair), NLDSC_BAND_F4_SEG (rows above 2^19 samples), NLDSC_BAND_F4_KSPLIT, NLDSC_BAND_F4_2X2
+ * (4-wave workgroups over 2x2 block pairs sharing their strips through LDS), NLDSC_BAND_F4_ROUTED (the default
+ * for sorted non-negative positions: missing-free 2x2 super-items in the 2x2 workgroups, the rest in the
+ * single-block kernel).  All exact paths give bitwise the same results. */
+#define NLDSC_BAND_F32 0
+#define NLDSC_BAND_I8 1
+#define NLDSC_BAND_F4 2
+#define NLDSC_BAND_F4_SEG 3
+#define NLDSC_BAND_F4_KSPLIT 4
+#define NLDSC_BAND_F4_2X2 5
+#define NLDSC_BAND_F4_ROUTED 6
+int nldsc_engine_band_kernel(const nldsc_engine* e);
 
 /* Load SNP rows [snp_begin, snp_end) of a .bed file of n_snp_file SNPs as the engine's image
  * (snp_end - snp_begin SNPs; the run then takes the positions of that slice).  Position sharding

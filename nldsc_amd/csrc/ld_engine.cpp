@@ -130,6 +130,11 @@ struct nldsc_engine {
     bool ksplit_ok = true;    // $NLDSC_KSPLIT=0 disables the K-split
     bool replay_overlap = true;  // $NLDSC_REPLAY_OVERLAP=0 runs the rare-variant replay in line on the main stream
     int last_ksplit = 1;
+    // fp4 band kernels on the GPU plan ($NLDSC_T2): 1 (default) missing-free super-items in the 2 x 2 block-pair
+    // workgroups, the rest in the single-block kernel; 2 everything in the 2 x 2 workgroups; 0 single-block only
+    int t2_mode = 1;
+    DevBuf<uint8_t> blk_miss;
+    int last_band_kernel = NLDSC_BAND_F4;
     DevBuf<double> pos, maf, rstd, l2_acc, l2d_acc, l2, l2d;
     DevBuf<int4> items;
     // host scratch
@@ -140,8 +145,9 @@ struct nldsc_engine {
     HostPinned h_meta;   // GPU plan counters (items, diagonal items)
     HostPinned h_pos;    // pinned copy of the positions (the upload does not stall this thread)
     HostPinned h_res;    // pinned landing buffer of the result copies (DMA, then host copies out)
-    DevBuf<int> Ew, plan_counts, plan_meta;
-    DevBuf<int2> plan_rows;
+    DevBuf<int> Ew, plan_counts, plan_meta, plan_counts2;
+    DevBuf<int2> plan_rows, plan_rows2;
+    DevBuf<int4> items2;  // super-items of the 2 x 2 kernel
     bool gpu_plan = true;  // band schedule on the GPU for non-negative sorted positions (NLDSC_GPU_PLAN=0: host)
     // timings of the last run
     double ms[6] = {0, 0, 0, 0, 0, 0};
@@ -160,6 +166,7 @@ struct nldsc_engine {
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         if (ev_plan) (void)hipEventDestroy(ev_plan);
         Ew.release(); plan_counts.release(); plan_meta.release(); plan_rows.release();
+        plan_counts2.release(); plan_rows2.release(); items2.release(); blk_miss.release();
         if (stream) (void)hipStreamDestroy(stream);
         if (plan_stream) (void)hipStreamDestroy(plan_stream);
         if (ev_pos) (void)hipEventDestroy(ev_pos);
@@ -255,6 +262,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_ORIENT")) e->orient = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_KSPLIT")) e->ksplit_ok = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_REPLAY_OVERLAP")) e->replay_overlap = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_T2")) e->t2_mode = std::max(0, std::min(2, std::atoi(v)));
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
@@ -472,14 +480,47 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     const bool sorted = nldsc::positions_sorted(p->positions, M);
     const bool gpu_plan = e->gpu_plan && sorted && max_nc == 1 &&
                           std::all_of(p->positions, p->positions + M, [](double x) { return x >= 0.0; });
+    // the 2 x 2 block-pair workgroups: fp4, unsegmented rows, GPU plan, and no K-split (choose_ksplit below)
+    const bool t2_cand = e->t2_mode > 0 && gpu_plan && use_f4 && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 2;
+    const bool routed = e->t2_mode == 1;
+    // K-split (f4, unsegmented rows) when the items fill the wave slots (2 per SIMD) in few, partly empty
+    // rounds — a rank's shard of one chromosome — and splitting the K loop in P pieces fills them better
+    // Model: a round of items takes ~0.67 us per K chunk (C3: 2 466 chunks, 1.65 ms per round, 12.7 rounds in
+    // 20.9 ms); the split adds ~64 KiB of partial-tile traffic per piece at ~3 TB/s effective (measured: a 1/8
+    // shard of C3, 3 300 items, band 3.35 -> 3.01 ms; a 1/2 shard, 13 000 items, P = 5 made it 7.5 % slower).
+    auto choose_ksplit = [&](int n_items) {
+        int ksplit = 1;
+        if (use_f4 && n_items > 0 && n_it <= nldsc::F4_SEG_CHUNKS && e->ksplit_ok) {
+            const double slots = 8.0 * (double)e->n_cu, t_round = 0.67e-6 * n_it;
+            auto cost = [&](int P) {
+                return std::ceil((double)n_items * P / slots) / P * t_round +
+                       (P > 1 ? n_items * P * 65536.0 / 3e12 : 0.0);
+            };
+            double best = cost(1);
+            for (int P = 2; P <= 8 && 2 * P <= n_it; ++P)
+                if (cost(P) < 0.97 * best && (size_t)n_items * P * 32768 <= ((size_t)3 << 30)) {
+                    best = cost(P);
+                    ksplit = P;
+                }
+        }
+        return ksplit;
+    };
+    int ksplit = 1;
+    bool use_t2 = false;
+    int n_items2 = 0;
     if (gpu_plan) {
         const size_t n_t = (size_t)(nblk + 15) / 16;
         HIPCHK(e->Aw.ensure((size_t)M));
         HIPCHK(e->Ew.ensure((size_t)M));
         HIPCHK(e->plan_rows.ensure((size_t)nblk));
         HIPCHK(e->plan_counts.ensure(n_t * n_t));
-        HIPCHK(e->plan_meta.ensure(4));
-        HIPCHK(e->h_meta.ensure(4 * sizeof(int)));
+        HIPCHK(e->plan_meta.ensure(8));  // [0, 4) single-block plan, [4, 8) super-item plan
+        HIPCHK(e->h_meta.ensure(8 * sizeof(int)));
+        if (t2_cand) {
+            const size_t nblk2 = (size_t)(nblk + 1) / 2, n_t2 = (nblk2 + 15) / 16;
+            HIPCHK(e->plan_rows2.ensure(nblk2));
+            HIPCHK(e->plan_counts2.ensure(n_t2 * n_t2));
+        }
     }
 
     auto t_start = std::chrono::steady_clock::now();
@@ -493,7 +534,10 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         HIPCHK(hipStreamWaitEvent(e->plan_stream, e->ev_pos, 0));
         HIPCHK(nldsc::launch_plan(e->pos.p, M, p->ld_wind, own_begin, own_end, e->Aw.p, e->Ew.p, e->Rw.p,
                                   e->plan_rows.p, e->plan_counts.p, e->plan_meta.p, e->plan_stream));
-        HIPCHK(hipMemcpyAsync(e->h_meta.p, e->plan_meta.p, 4 * sizeof(int), hipMemcpyDeviceToHost, e->plan_stream));
+        if (t2_cand)
+            HIPCHK(nldsc::launch_plan_super(M, e->plan_rows.p, e->plan_rows2.p, e->plan_counts2.p, e->plan_meta.p + 4,
+                                            e->plan_stream));
+        HIPCHK(hipMemcpyAsync(e->h_meta.p, e->plan_meta.p, 8 * sizeof(int), hipMemcpyDeviceToHost, e->plan_stream));
         HIPCHK(hipEventRecord(e->ev_plan, e->plan_stream));
     }
     // non-individual slots read as missing (0x55) for the int8 / fp32 kernels, as 00 (all fp4 planes zero) for fp4
@@ -529,9 +573,23 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         const int* meta = reinterpret_cast<const int*>(e->h_meta.p);
         n_items = meta[1];
         n_diag = meta[2];
-        HIPCHK(e->items.ensure(std::max<size_t>((size_t)n_items, 1)));
-        if (n_items > 0)
-            HIPCHK(nldsc::launch_plan_emit(M, e->plan_rows.p, e->plan_meta.p, e->plan_counts.p, e->items.p, st));
+        ksplit = choose_ksplit(n_items);
+        use_t2 = t2_cand && ksplit == 1 && n_items > 0;
+        if (use_t2) {
+            n_items2 = meta[5];
+            HIPCHK(e->items2.ensure(std::max<size_t>((size_t)n_items2, 1)));
+            HIPCHK(nldsc::launch_plan_emit_super(M, e->plan_rows2.p, e->plan_meta.p + 4, e->plan_counts2.p,
+                                                 e->items2.p, st));
+        }
+        if (use_t2 && routed) {
+            HIPCHK(e->blk_miss.ensure((size_t)nblk));
+            HIPCHK(nldsc::launch_block_missing(e->sflags.p, M, e->blk_miss.p, st));
+        }
+        if (!use_t2 || routed) {
+            HIPCHK(e->items.ensure(std::max<size_t>((size_t)n_items, 1)));
+            if (n_items > 0)
+                HIPCHK(nldsc::launch_plan_emit(M, e->plan_rows.p, e->plan_meta.p, e->plan_counts.p, e->items.p, st));
+        }
         HIPCHK(nldsc::launch_left_pointers(e->Aw.p, e->sflags.p, e->pos.p, M, e->Lw.p, st));
     } else {
     e->h_L.resize(M);
@@ -583,6 +641,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     if (bI) HIPCHK(hipMemcpyAsync(e->items.p, e->h_stage.p + 2 * bL, bI, hipMemcpyHostToDevice, st));
     n_items = (int)e->h_items.size();
     for (const nldsc::PlanItem& it : e->h_items) n_diag += it.x == it.y;
+    ksplit = choose_ksplit(n_items);
     }
     HIPCHK(hipMemsetAsync(e->l2_acc.p, 0, sizeof(double) * M, st));
     HIPCHK(hipMemsetAsync(e->l2d_acc.p, 0, sizeof(double) * M, st));
@@ -597,32 +656,30 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
         double blocks = 0;
         if (gpu_plan) blocks = n_items;
         else for (const nldsc::PlanItem& it : e->h_items) blocks += it.z;
-        // (the fp4 kernel also skips m.x on diagonal blocks: the transpose of x.m)
-        const double products = use_i8 ? blocks * (dom ? 8.0 : 4.0) - (dom ? 2.0 * n_diag : 0.0)
+        // (the single-block fp4 kernel also skips m.x on diagonal blocks: the transpose of x.m; the 2 x 2
+        // workgroups issue every product)
+        const double products = use_t2 && !routed ? blocks * (dom ? 8.0 : 4.0)
+                              : use_i8 ? blocks * (dom ? 8.0 : 4.0) - (dom ? 2.0 * n_diag : 0.0)
                                          - (use_f4 ? 1.0 * n_diag : 0.0)
                                        : blocks * (dom ? 3.0 : 1.0) - (dom ? 1.0 * n_diag : 0.0);
         e->flop_issued = products * 2.0 * BLK * BLK * (double)row_bytes * 4.0;
     }
-    // K-split (f4, unsegmented rows) when the items fill the wave slots (2 per SIMD) in few, partly empty
-    // rounds — a rank's shard of one chromosome — and splitting the K loop in P pieces fills them better
-    // Model: a round of items takes ~0.67 us per K chunk (C3: 2 466 chunks, 1.65 ms per round, 12.7 rounds in
-    // 20.9 ms); the split adds ~64 KiB of partial-tile traffic per piece at ~3 TB/s effective (measured: a 1/8
-    // shard of C3, 3 300 items, band 3.35 -> 3.01 ms; a 1/2 shard, 13 000 items, P = 5 made it 7.5 % slower).
-    int ksplit = 1;
-    if (use_f4 && n_items > 0 && n_it <= nldsc::F4_SEG_CHUNKS && e->ksplit_ok) {
-        const double slots = 8.0 * (double)e->n_cu, t_round = 0.67e-6 * n_it;
-        auto cost = [&](int P) {
-            return std::ceil((double)n_items * P / slots) / P * t_round + (P > 1 ? n_items * P * 65536.0 / 3e12 : 0.0);
-        };
-        double best = cost(1);
-        for (int P = 2; P <= 8 && 2 * P <= n_it; ++P)
-            if (cost(P) < 0.97 * best && (size_t)n_items * P * 32768 <= ((size_t)3 << 30)) { best = cost(P); ksplit = P; }
-    }
     e->last_ksplit = ksplit;
+    e->last_band_kernel = use_t2 ? (routed ? NLDSC_BAND_F4_ROUTED : NLDSC_BAND_F4_2X2) : !use_f4 ? (use_i8 ? NLDSC_BAND_I8 : NLDSC_BAND_F32)
+                        : ksplit > 1 ? NLDSC_BAND_F4_KSPLIT : n_it > nldsc::F4_SEG_CHUNKS ? NLDSC_BAND_F4_SEG
+                        : NLDSC_BAND_F4;
     if (ksplit > 1) HIPCHK(e->gram.ensure((size_t)n_items * ksplit * 8192));
     // which = 1: the launch for the items without a replayed SNP (beside the replay), 2: the KC launch after it
     const uint8_t* blk_rep = replay ? e->blk_rep.p : nullptr;
     auto launch_band_path = [&](int which) -> hipError_t {
+        const uint8_t* miss = use_t2 && routed ? e->blk_miss.p : nullptr;
+        if (use_t2) {
+            hipError_t r = nldsc::launch_band_f4_t2(dom, n_items2, geno, pitch_words, n_it, e->cst.p, e->items2.p,
+                                                    e->plan_rows.p, nblk, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
+                                                    p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p,
+                                                    e->l2d_acc.p, e->ws_acc.p, true, blk_rep, miss, which, st);
+            if (r != hipSuccess || !routed) return r;
+        }
         if (use_f4 && ksplit > 1)
             return nldsc::launch_band_f4_split(dom, ksplit, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p,
                                                e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N,
@@ -632,7 +689,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
             return nldsc::launch_band_f4(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p,
                                          e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr,
                                          own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true, blk_rep,
-                                         which, st);
+                                         which, st, miss);
         return nldsc::launch_band_i8(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p, e->pos.p,
                                      e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin,
                                      own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true, blk_rep, which, st);
@@ -719,6 +776,7 @@ int nldsc_engine_path(const nldsc_engine* e, int32_t* exact_i8, double* ops_alg_
 }
 
 int nldsc_engine_ksplit(const nldsc_engine* e) { return e ? e->last_ksplit : NLDSC_E_ARG; }
+int nldsc_engine_band_kernel(const nldsc_engine* e) { return e ? e->last_band_kernel : NLDSC_E_ARG; }
 
 int nldsc_ld_calculate(const nldsc_ld_params* p, nldsc_ld_result* r, char* err, size_t errlen) {
     if (!p || !r || !p->bedfile) return set_err(err, errlen, NLDSC_E_ARG, "NULL argument");

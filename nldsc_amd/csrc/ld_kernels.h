@@ -72,7 +72,7 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
-                          int which, hipStream_t st);
+                          int which, hipStream_t st, const uint8_t* blk_miss = nullptr);
 // the same with the K loop split in P pieces (small launches: better filled wave slots): partial Gram tiles to
 // `gram` (n_items * P * 8192 floats), then an epilogue kernel (unsegmented rows, n_it <= F4_SEG_CHUNKS)
 hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* geno, int pitch_words, int n_it,
@@ -80,6 +80,24 @@ hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* ge
                                 const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr,
                                 int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc,
                                 const uint8_t* blk_rep, float* gram, int which, hipStream_t st);
+// 2 x 2 block-pair workgroups (unsegmented rows, gpu plan): super-items (I2, J2, 1, 0) over row / column
+// super-blocks of two 32-SNP blocks, planned from the single-block rows (launch_plan) by launch_plan_super (meta2
+// as meta; counts2 capacity ceil(nblk2/16)^2) and launch_plan_emit_super; the kernel reads `rows` (nblk) to skip the
+// block pairs the single-block plan does not hold
+constexpr int T2_STAGES = 4;  // LDS ring stages (2 chunks each) of band_f4_t2_kernel
+hipError_t launch_plan_super(int n, const int2* rows, int2* rows2, int* counts2, int* meta2, hipStream_t st);
+hipError_t launch_plan_emit_super(int n, const int2* rows2, const int* meta2, const int* offsets2, int4* items2,
+                                  hipStream_t st);
+hipError_t launch_band_f4_t2(bool dom, int n_items2, const uint32_t* geno, int pitch_words, int n_it,
+                             const SnpConst* cst, const int4* items2, const int2* rows, int nblk, const double* pos,
+                             const int* Lw, const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind,
+                             double n_org, double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
+                             int* ws_acc, bool xcd, const uint8_t* blk_rep, const uint8_t* blk_miss, int which,
+                             hipStream_t st);
+// blk_miss[b] = block b holds a missing call.  Passed to both fp4 kernels (unsegmented rows) it routes the
+// super-items: missing-free ones to the 2 x 2 kernel (operand-feed bound at 3 products per K step, where sharing
+// the strips pays), the block pairs of the others to the single-block kernel (MFMA bound at 8 products)
+hipError_t launch_block_missing(const uint8_t* sflags, int n_snp, uint8_t* blk_miss, hipStream_t st);
 hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2d_acc, const int* ws_acc, int n_snp,
                            int own_lo, int own_hi, bool dom, double* l2, double* l2d, int* ws3, hipStream_t st);
 hipError_t launch_synth_bed(uint8_t* rows, int n_snp, int n_org, int nb, const float* thr, float rho, float missing,

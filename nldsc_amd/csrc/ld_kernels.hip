@@ -1470,6 +1470,15 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     }
 }
 
+// Routing between the two fp4 kernels (blk_miss[b] = block b holds a missing call): a super-item whose four
+// blocks are all missing-free (3 products per K step: operand-feed bound) runs in the 2 x 2 kernel, the block pairs
+// of every other super-item (8 products: MFMA bound, where the single-block kernel is faster) in the single-block
+// kernel.  Both kernels evaluate this predicate on the same clamped blocks, so every block pair runs exactly once.
+__device__ __forceinline__ bool t2_routed(const uint8_t* blk_miss, int I2, int J2, int nblk) {
+    return !(blk_miss[2 * I2] | blk_miss[min(2 * I2 + 1, nblk - 1)] | blk_miss[2 * J2] |
+             blk_miss[min(2 * J2 + 1, nblk - 1)]);
+}
+
 // One block pair per item.  WPS 2, except the segmented add+dom kernel (its int32 fold registers need 1).
 template <bool DOM, int WPS, int SEG, bool KC>
 __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
@@ -1479,16 +1488,218 @@ __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __rest
                                                         int n_snp, double ld_wind, double n_org, double rsq_thr,
                                                         int own_lo, int own_hi, double* __restrict__ l2_acc,
                                                         double* __restrict__ l2d_acc, int* __restrict__ ws_acc, int xcd,
-                                                        const uint8_t* __restrict__ blk_rep) {
+                                                        const uint8_t* __restrict__ blk_rep,
+                                                        const uint8_t* __restrict__ blk_miss) {
     __shared__ BandI8Lds sh;
     __shared__ float tr[32 * 33];
     const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
     if (skip_item<KC>(blk_rep, it)) return;
+    // blk_miss: the 2 x 2 kernel runs the missing-free super-items
+    if (blk_miss != nullptr && t2_routed(blk_miss, it.x >> 1, it.y >> 1, (n_snp + 31) >> 5)) return;
 #define NLDSC_BODY(DIAG_)                                                                                             \
     band_f4_body<DOM, 1, DIAG_, SEG, KC>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind,  \
                                          n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, tr)
     if (it.y == it.x) NLDSC_BODY(true); else NLDSC_BODY(false);
 #undef NLDSC_BODY
+}
+
+// ---- 2 x 2 block-pair workgroups: the operand feed ----
+
+// One workgroup of 4 waves per super-item (I2, J2) of the band: wave w computes the block pair
+// (2 I2 + w / 2, 2 J2 + w % 2) when the plan needs it (rows[rb] = the needed column offsets of row block rb,
+// plan_rows_kernel).  The four 32-SNP strips (row blocks 2 I2, 2 I2 + 1, column blocks 2 J2, 2 J2 + 1; only the
+// first two on a diagonal super-item) go global -> LDS once per workgroup by global_load_lds, 1 KiB per strip and
+// chunk, lane-linear in the (i, h) order the waves read them, through a ring of S two-chunk stages with S - 1
+// stages in flight across the barriers (counted vmcnt, raw s_barrier): every strip byte fetched feeds two block
+// pairs instead of one.  Diagonal block pairs issue all products (no transpose through LDS).
+constexpr int T2_SLOTS = 128;  // LDS slot tables: 0-63 the two row blocks, 64-127 the two column blocks
+template <int S>
+struct T2Lds {
+    uint4 stage[S][4][2][64];  // [buffer][strip][chunk of the stage][lane (i + 32 h)]
+    SnpSlot info[T2_SLOTS];
+    SnpConst cst[T2_SLOTS];
+    // per-SNP sums per wave: each block pair's partial sums are formed exactly as the single-block kernel forms
+    // them (one wave, the same epilogue), so the fixed-point totals are bitwise that kernel's
+    double l2[4][T2_SLOTS], l2d[4][T2_SLOTS];
+    int wsa[4][T2_SLOTS], wsd[4][T2_SLOTS], wse[4][T2_SLOTS];
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    // s_waitcnt encoding (gfx9): vmcnt[3:0] | expcnt[6:4] = 7 | lgkmcnt[11:8] = 15 | vmcnt[5:4] at [15:14]
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// the products of one K step for one block pair (band_f4_body's mfmas_v with one column block, no diagonal skip)
+template <bool DOM, bool RM, bool CM>
+__device__ __forceinline__ void f4_step(const F4Frag& a, const F4Frag& b, f32x16v& gxx, f32x16v& gxo, f32x16v& gox,
+                                        f32x16v& goo, f32x16v& gxh, f32x16v& goh, f32x16v& ghx, f32x16v& gho) {
+    gxx = mfma_f4(a.x, b.x, gxx);
+    if (CM) gxo = mfma_f4(a.x, b.o, gxo);
+    if (DOM) gxh = mfma_f4(a.x, b.h, gxh);
+    if (RM) gox = mfma_f4(a.o, b.x, gox);
+    if (DOM) ghx = mfma_f4(a.h, b.x, ghx);
+    if (RM && CM) goo = mfma_f4(a.o, b.o, goo);
+    if (DOM && RM) goh = mfma_f4(a.o, b.h, goh);
+    if (DOM && CM) gho = mfma_f4(a.h, b.o, gho);
+    constexpr int n_mfma = 1 + CM + RM + (RM && CM) + (DOM ? 2 + RM + CM : 0);
+    constexpr int n_valu = 2 * 9 + 2 * 9;  // the next step's two decodes
+#pragma unroll
+    for (int m = 0; m < n_mfma; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, (n_valu + n_mfma - 1) / n_mfma, 0);
+    }
+}
+
+template <bool DOM, int S, bool KC>
+__global__ void __launch_bounds__(256, 2) band_f4_t2_kernel(
+    const uint32_t* __restrict__ geno, int pitch_words, int n_it, const SnpConst* __restrict__ cst,
+    const int4* __restrict__ items, const int2* __restrict__ rows, int nblk, const double* __restrict__ pos,
+    const int* __restrict__ Lw, const int* __restrict__ Rw, const uint8_t* __restrict__ sflags, int n_snp,
+    double ld_wind, double n_org, double rsq_thr, int own_lo, int own_hi, double* __restrict__ l2_acc,
+    double* __restrict__ l2d_acc, int* __restrict__ ws_acc, int xcd, const uint8_t* __restrict__ blk_rep,
+    const uint8_t* __restrict__ blk_miss) {
+    static_assert(S >= 2, "ring of at least two stages");
+    __shared__ T2Lds<S> sh;
+    const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
+    const int I2 = it.x, J2 = it.y;
+    // strip blocks (a block past the end, odd nblk, is clamped: its block pairs are not needed)
+    const int b0 = 2 * I2, b1 = min(2 * I2 + 1, nblk - 1), b2 = 2 * J2, b3 = min(2 * J2 + 1, nblk - 1);
+    if (KC || blk_rep != nullptr) {  // a super-item with a replayed SNP runs whole in the KC launch
+        const bool rep = blk_rep[b0] | blk_rep[b1] | blk_rep[b2] | blk_rep[b3];
+        if (KC ? !rep : rep) return;
+    }
+    if (blk_miss != nullptr && !t2_routed(blk_miss, I2, J2, nblk)) return;  // the single-block kernel's
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
+    if (tid < T2_SLOTS) {
+        const int blk = (tid < 64 ? 2 * I2 : 2 * J2) + ((tid >> 5) & 1);
+        const int g = blk * 32 + (tid & 31);
+        SnpSlot si;
+        si.g = g;
+        if (g < n_snp) {
+            si.pos = pos[g]; si.L = Lw[g]; si.R = Rw[g]; si.fl = sflags[g];
+        } else {
+            si.pos = 0.0; si.L = -1; si.R = -2; si.fl = 0;
+        }
+        sh.info[tid] = si;
+        sh.cst[tid] = blk < nblk ? cst[g] : SnpConst{};
+    }
+    for (int s = lane; s < T2_SLOTS; s += 64) {
+        sh.l2[w][s] = 0.0; sh.l2d[w][s] = 0.0;
+        sh.wsa[w][s] = 0; sh.wsd[w][s] = 0; sh.wse[w][s] = 0;
+    }
+    const int rb = 2 * I2 + (w >> 1), cb = 2 * J2 + (w & 1);
+    bool need = rb < nblk && cb < nblk;
+    if (need) {
+        const int2 r = rows[rb];
+        need = cb - rb >= r.x && cb - rb <= r.y;
+    }
+    const bool dsup = I2 == J2;  // diagonal super-item: the column strips are the row strips
+    const int sA = w >> 1, sB = dsup ? (w & 1) : 2 + (w & 1);
+    const int my_blk = w == 0 ? b0 : w == 1 ? b1 : w == 2 ? b2 : b3;
+    const bool loads = !(dsup && w >= 2);
+    const uint4* src = reinterpret_cast<const uint4*>(geno + (size_t)(my_blk * 32 + i) * (size_t)pitch_words) + h;
+    const int n_st = n_it >> 1;  // two-chunk stages (rows are padded to 64 bytes)
+    // stage t (clamped to the last: the surplus loads of the tail land in buffers no one reads again) -> buffer t % S
+    // (inline asm: hipcc's own LDS-DMA tracking cannot tell the ring buffers apart and would wait vmcnt(0) before
+    // every stage's first ds_read; the counted waits below order them instead)
+    auto issue = [&](int t) {
+        const int tc = min(t, n_st - 1);
+        if (loads) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const uint32_t dst = __builtin_amdgcn_readfirstlane(
+                    (uint32_t)(size_t)(__attribute__((address_space(3))) void*)&sh.stage[t % S][w][c][0]);
+                uint32_t keep;
+                asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                             "s_mov_b32 m0, %0"
+                             : "=&s"(keep)
+                             : "v"(src + 4 * tc + 2 * c), "s"(dst)
+                             : "memory");
+            }
+        }
+    };
+    __syncthreads();  // slot tables written; nothing in flight yet
+    const bool rm = __any(lane < 32 && (sh.info[32 * sA + lane].fl & 4));
+    const bool cm = __any(lane < 32 && (sh.info[64 + 32 * (w & 1) + lane].fl & 4));
+#pragma unroll
+    for (int t = 0; t < S - 1; ++t) issue(t);
+
+    f32x16v gxx = {}, gxo = {}, gox = {}, goo = {}, gxh = {}, goh = {}, ghx = {}, gho = {};
+    auto kloop = [&](auto RMc, auto CMc, auto ACTc) {
+        constexpr bool RM = decltype(RMc)::value, CM = decltype(CMc)::value, ACT = decltype(ACTc)::value;
+        for (int t = 0; t < n_st; ++t) {
+            wait_vmcnt<2 * (S - 2)>();  // this wave's loads of stage t have landed
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // every wave's have, and every wave is done with buffer (t - 1) % S
+            asm volatile("" ::: "memory");
+            issue(t + S - 1);
+            if constexpr (ACT) {
+                const uint4* A = &sh.stage[t % S][sA][0][0];
+                const uint4* B = &sh.stage[t % S][sB][0][0];
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const uint4 a = A[c * 64 + lane], b = B[c * 64 + lane];
+                    const F4Frag a0 = decode_f4(a.x, a.y), f0 = decode_f4(b.x, b.y);
+                    f4_step<DOM, RM, CM>(a0, f0, gxx, gxo, gox, goo, gxh, goh, ghx, gho);
+                    const F4Frag a1 = decode_f4(a.z, a.w), f1 = decode_f4(b.z, b.w);
+                    f4_step<DOM, RM, CM>(a1, f1, gxx, gxo, gox, goo, gxh, goh, ghx, gho);
+                }
+            }
+        }
+    };
+    if (!need) kloop(std::false_type{}, std::false_type{}, std::false_type{});
+    else if (rm && cm) kloop(std::true_type{}, std::true_type{}, std::true_type{});
+    else if (rm) kloop(std::true_type{}, std::false_type{}, std::true_type{});
+    else if (cm) kloop(std::false_type{}, std::true_type{}, std::true_type{});
+    else kloop(std::false_type{}, std::false_type{}, std::true_type{});
+    wait_vmcnt<0>();  // the tail's surplus loads
+    if (!need) return;  // no barrier follows
+    pair_epilogue<DOM, f32x16v, true, KC>(sh.info, sh.cst, sh.l2[w], sh.l2d[w], sh.wsa[w], sh.wsd[w], sh.wse[w],
+                                          32 * sA, 64 + 32 * (w & 1), rb == cb, i, h, gxx, gxo, gox, goo, gxh, goh,
+                                          ghx, gho, ld_wind, n_org, rsq_thr, n_org);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // this wave's 64 slots: its row block (lanes 0-31) and column block (lanes 32-63)
+    const int s = h ? 64 + 32 * (w & 1) + i : 32 * sA + i, g = sh.info[s].g;
+    if (g >= own_lo && g < own_hi && g < n_snp) {
+        if (sh.wsa[w][s]) {
+            acc_fixed(&l2_acc[g], &ws_acc[3 * (size_t)n_snp + g], 1, sh.l2[w][s]);
+            atomicAdd(&ws_acc[g], sh.wsa[w][s]);
+        }
+        if (DOM && sh.wsd[w][s]) {
+            acc_fixed(&l2d_acc[g], &ws_acc[3 * (size_t)n_snp + g], 2, sh.l2d[w][s]);
+            atomicAdd(&ws_acc[(size_t)n_snp + g], sh.wsd[w][s]);
+            if (sh.wse[w][s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + g], sh.wse[w][s]);
+        }
+    }
+}
+
+// blk_miss[b] = 1 if block b holds a SNP with a missing call (flag bit 2) — zeroed before
+__global__ void block_missing_kernel(const uint8_t* __restrict__ sflags, int n_snp, uint8_t* __restrict__ blk_miss) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n_snp && (sflags[j] & 4)) blk_miss[j >> 5] = 1;
+}
+
+// super-item rows: per row super-block I2 (row blocks 2 I2, 2 I2 + 1) the super-column offsets [d0, d1] covering both
+// blocks' needed columns; meta[0] = max d1 + 1, meta[2] = diagonal super-items (plan_count / scan / emit then run on
+// these rows as on the single-block ones)
+__global__ void plan_rows2_kernel(const int2* __restrict__ rows, int nblk, int2* __restrict__ rows2,
+                                  int* __restrict__ meta) {
+    const int I2 = blockIdx.x * blockDim.x + threadIdx.x, nblk2 = (nblk + 1) / 2;
+    if (I2 >= nblk2) return;
+    int lo = INT_MAX, hi = -1;
+    for (int b = 2 * I2; b < min(nblk, 2 * I2 + 2); ++b) {
+        const int2 r = rows[b];
+        if (r.x <= r.y) { lo = min(lo, b + r.x); hi = max(hi, b + r.y); }
+    }
+    const int2 r2 = hi >= 0 ? make_int2((lo >> 1) - I2, (hi >> 1) - I2) : make_int2(1, 0);
+    rows2[I2] = r2;
+    if (r2.x <= r2.y) {
+        atomicMax(&meta[0], r2.y + 1);
+        if (r2.x == 0) atomicAdd(&meta[2], 1);
+    }
 }
 
 // K-split for small launches (a rank's shard of one chromosome: ~3 300 items for 2 048 wave slots leave the
@@ -1786,6 +1997,50 @@ hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* gen
     return hipGetLastError();
 }
 
+hipError_t launch_plan_super(int n, const int2* rows, int2* rows2, int* counts2, int* meta2, hipStream_t st) {
+    const int nblk = (n + 31) / 32, nblk2 = (nblk + 1) / 2;
+    hipError_t e = hipMemsetAsync(meta2, 0, 4 * sizeof(int), st);
+    if (e != hipSuccess || n <= 0) return e;
+    hipLaunchKernelGGL(plan_rows2_kernel, dim3((nblk2 + 255) / 256), dim3(256), 0, st, rows, nblk, rows2, meta2);
+    hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, counts2);
+    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts2, nblk2, meta2);
+    return hipGetLastError();
+}
+
+hipError_t launch_block_missing(const uint8_t* sflags, int n_snp, uint8_t* blk_miss, hipStream_t st) {
+    if (n_snp <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(blk_miss, 0, (size_t)(n_snp + 31) / 32, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(block_missing_kernel, dim3((n_snp + 255) / 256), dim3(256), 0, st, sflags, n_snp, blk_miss);
+    return hipGetLastError();
+}
+
+hipError_t launch_plan_emit_super(int n, const int2* rows2, const int* meta2, const int* offsets2, int4* items2,
+                                  hipStream_t st) {
+    const int nblk2 = ((n + 31) / 32 + 1) / 2;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, offsets2, items2);
+    return hipGetLastError();
+}
+
+hipError_t launch_band_f4_t2(bool dom, int n_items2, const uint32_t* geno, int pitch_words, int n_it,
+                             const SnpConst* cst, const int4* items2, const int2* rows, int nblk, const double* pos,
+                             const int* Lw, const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind,
+                             double n_org, double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
+                             int* ws_acc, bool xcd, const uint8_t* blk_rep, const uint8_t* blk_miss, int which,
+                             hipStream_t st) {
+    if (n_items2 <= 0) return hipSuccess;
+    if (n_it > F4_SEG_CHUNKS || n_it < 2 || (n_it & 1)) return hipErrorInvalidValue;
+#define NLDSC_BAND(DOM_, KC_)                                                                                       \
+    hipLaunchKernelGGL((band_f4_t2_kernel<DOM_, T2_STAGES, KC_>), dim3(n_items2), dim3(256), 0, st, geno,           \
+                       pitch_words, n_it, cst, items2, rows, nblk, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,      \
+                       rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss)
+    if (which & 1) { if (dom) NLDSC_BAND(true, false); else NLDSC_BAND(false, false); }
+    if (blk_rep && (which & 2)) { if (dom) NLDSC_BAND(true, true); else NLDSC_BAND(false, true); }
+#undef NLDSC_BAND
+    return hipGetLastError();
+}
+
 hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                                 const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                                 const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr,
@@ -1813,13 +2068,14 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
-                          int which, hipStream_t st) {
+                          int which, hipStream_t st, const uint8_t* blk_miss) {
     if (n_items <= 0) return hipSuccess;
     if (max_nc != 1) return hipErrorInvalidValue;  // single block-pair items
+    if (blk_miss != nullptr && n_it > F4_SEG_CHUNKS) return hipErrorInvalidValue;  // routing: unsegmented rows only
 #define NLDSC_BAND(DOM_, WPS_, SEG_, KC_)                                                                           \
     hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_, KC_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words,  \
                        n_it, cst, items, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi,       \
-                       l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep)
+                       l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss)
 #define NLDSC_PICK(KC_)                                                                                              \
     if (n_it > F4_SEG_CHUNKS) { if (dom) NLDSC_BAND(true, 1, F4_SEG_CHUNKS, KC_); else NLDSC_BAND(false, 2, F4_SEG_CHUNKS, KC_); } \
     else if (dom) NLDSC_BAND(true, 2, 0, KC_);                                                                       \

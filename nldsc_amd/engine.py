@@ -13,6 +13,9 @@ import numpy as np
 
 from . import _lib
 
+# nldsc_engine_band_kernel codes (include/nldsc_ld.h NLDSC_BAND_*)
+BAND_KERNELS = {0: "f32", 1: "i8", 2: "f4", 3: "f4_seg", 4: "f4_ksplit", 5: "f4_2x2", 6: "f4_routed"}
+
 
 class Engine:
     def __init__(self, device: int = -1, lib_path: str | None = None):
@@ -99,7 +102,8 @@ class Engine:
         ex, ops = ctypes.c_int32(), ctypes.c_double()
         self._L.nldsc_engine_path(self._h, ctypes.byref(ex), ctypes.byref(ops))
         d.update(exact_i8=ex.value > 0, path={0: "f32", 1: "i8", 2: "f4"}[ex.value], ops_alg_i8=ops.value,
-                 ksplit=self._L.nldsc_engine_ksplit(self._h))
+                 ksplit=self._L.nldsc_engine_ksplit(self._h),
+                 band_kernel=BAND_KERNELS.get(self._L.nldsc_engine_band_kernel(self._h), "?"))
         return d
 
 

@@ -670,3 +670,84 @@ def test_ksplit_equals_single_pass(engine, N, M, dom):
         exp = dict(exp, l2d=np.full(M, np.nan), l2d_ws=np.full(M, -1, np.int32), l2d_wse=np.full(M, -1, np.int32))
     assert_ld_close(got, exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
                                        maf=(0.0, 0.0)), label=f"ksplit N={N}")
+
+
+def _env_run(var, value, fn):
+    old = os.environ.get(var)
+    os.environ[var] = value
+    try:
+        return fn()
+    finally:
+        if old is None:
+            os.environ.pop(var)
+        else:
+            os.environ[var] = old
+
+
+T2_CASES = {
+    # (N, M, length cM, window cM, missing, dom, own, rare): odd block counts, narrow and wide bands, missing-free
+    # blocks (3 products) beside blocks with missing calls, an owned sub-range, additive only, replayed rare
+    # variants (the KC launch)
+    "odd_blocks_narrow": (4099, 990, 30.0, 0.3, 0.02, True, None, False),
+    "wide_band": (2053, 1500, 4.0, 1.0, 0.01, True, None, False),
+    "missing_free": (6000, 1100, 8.0, 1.0, 0.0, True, None, False),
+    "additive_only": (4096, 1025, 8.0, 1.0, 0.02, False, None, False),
+    "owned_range": (3001, 1400, 10.0, 1.0, 0.02, True, (333, 1001), False),
+    "rare_replay": (50_001, 400, None, 1.0, None, True, None, True),
+    # missing calls in every third block only: the routed default splits the band between both kernels
+    "mixed_blocks": (5003, 1300, 8.0, 1.0, "mixed", True, None, False),
+}
+
+
+@pytest.mark.parametrize("t2", ["2", "1"])
+@pytest.mark.parametrize("case", sorted(T2_CASES))
+def test_2x2_workgroups_bitwise_single_block(engine, case, t2):
+    """The 2 x 2 block-pair workgroups (LDS-shared strips) — for every super-item ($NLDSC_T2=2) or, the default,
+    for the missing-free ones with the rest routed to the single-block kernel ($NLDSC_T2=1) — give bitwise the
+    single-block kernel's results ($NLDSC_T2=0): each wave forms its block pair's partial sums exactly as the
+    single-block kernel does; both match the fp64 truth."""
+    from conftest import rare_variant_set
+    from nldsc_amd import synth
+    from nldsc_amd.engine import Engine
+    N, M, length, wind, missing, dom, own, rare = T2_CASES[case]
+    if rare:
+        rows, pos = rare_variant_set(N)
+        M = len(pos)
+    else:
+        spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=length, seed=N + M,
+                               missing=0.0 if missing == "mixed" else missing)
+        g = synth.genotypes(spec)
+        if missing == "mixed":
+            rng = np.random.default_rng(M)
+            for b in range(0, (M + 31) // 32, 3):
+                j = 32 * b + rng.integers(0, min(32, M - 32 * b))
+                g[j, rng.choice(N, 20, replace=False)] = -1
+        rows = synth.pack_bed_rows(g)
+        pos = synth.positions_cm(spec)
+    # (the fp64-truth comparison needs the exact rare-variant residuals; the rare case keeps the replay: KC launch)
+    flags = MODES["f4"] | (0 if dom else _lib_flag("FLAG_ADDITIVE_ONLY")) | (0 if rare else _lib_flag("FLAG_EXACT_RARE"))
+    args = (wind, 1e-5, 1e-5, 1.0 / M, pos)
+
+    def fresh(kernel):  # engines read $NLDSC_* when created; these launches are small enough for the K-split
+        with Engine(0) as e:
+            e.load_bed_bytes(synth.bed_bytes(rows), M, N)
+            r = e.run(*args, flags=flags, own=own)
+            assert e.timings()["band_kernel"] == kernel
+            return r
+    got = _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", t2, lambda: fresh(
+        {"2": "f4_2x2", "1": "f4_routed"}[t2])))
+    ref = _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", "0", lambda: fresh("f4")))
+    for k in got:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{case} {k}")
+    if rare:
+        return  # the replayed residuals are the reference's fp32 ones, not the fp64 truth
+    exp = O.run_f64(rows, N, *args)
+    if own is not None:
+        lo, hi = own
+        exp = {k: v[lo:hi] for k, v in exp.items()}
+        got = {k: v[lo:hi] for k, v in got.items()}
+    if not dom:
+        n = len(next(iter(exp.values())))
+        exp = dict(exp, l2d=np.full(n, np.nan), l2d_ws=np.full(n, -1, np.int32), l2d_wse=np.full(n, -1, np.int32))
+    assert_ld_close(got, exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
+                                       maf=(0.0, 0.0)), label=f"2x2 {case} T2={t2}")
