@@ -130,9 +130,12 @@ struct nldsc_engine {
     bool ksplit_ok = true;    // $NLDSC_KSPLIT=0 disables the K-split
     bool replay_overlap = true;  // $NLDSC_REPLAY_OVERLAP=0 runs the rare-variant replay in line on the main stream
     int last_ksplit = 1;
+    int last_round_items = 0;
     // fp4 band kernels on the GPU plan ($NLDSC_T2): 1 (default) missing-free super-items in the 2 x 2 block-pair
     // workgroups, the rest in the single-block kernel; 2 everything in the 2 x 2 workgroups; 0 single-block only
     int t2_mode = 1;
+    // single-block fp4 band in launches of one round of wave slots ($NLDSC_BAND_ROUNDS=0: one launch)
+    bool band_rounds = true;
     DevBuf<uint8_t> blk_miss;
     int last_band_kernel = NLDSC_BAND_F4;
     DevBuf<double> pos, maf, rstd, l2_acc, l2d_acc, l2, l2d;
@@ -263,6 +266,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_KSPLIT")) e->ksplit_ok = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_REPLAY_OVERLAP")) e->replay_overlap = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_T2")) e->t2_mode = std::max(0, std::min(2, std::atoi(v)));
+    if (const char* v = std::getenv("NLDSC_BAND_ROUNDS")) e->band_rounds = std::atoi(v) != 0;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
@@ -669,6 +673,15 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
                         : ksplit > 1 ? NLDSC_BAND_F4_KSPLIT : n_it > nldsc::F4_SEG_CHUNKS ? NLDSC_BAND_F4_SEG
                         : NLDSC_BAND_F4;
     if (ksplit > 1) HIPCHK(e->gram.ensure((size_t)n_items * ksplit * 8192));
+    // Unsegmented single-block fp4 items go in launches of one round of the wave slots each (2 per SIMD): the items
+    // of a launch start together and, all of equal length, stay at nearby K offsets, so the waves on one XCD that
+    // share a strip (the plan's 16 x 16 tiles) read it from that XCD's L2.  In one launch of all items the waves
+    // drift apart and most strip bytes come from beyond L2 again (C3: 68 -> 14 GB per band, the clock 1.90 -> 2.02
+    // GHz; band -2 to -3 % after the launch tails).  Only for launches of several rounds.
+    const int slots = 8 * e->n_cu;
+    const int round_items =
+        use_f4 && ksplit == 1 && e->band_rounds && n_it <= nldsc::F4_SEG_CHUNKS && n_items >= 4 * slots ? slots : 0;
+    e->last_round_items = round_items;
     // which = 1: the launch for the items without a replayed SNP (beside the replay), 2: the KC launch after it
     const uint8_t* blk_rep = replay ? e->blk_rep.p : nullptr;
     auto launch_band_path = [&](int which) -> hipError_t {
@@ -689,7 +702,7 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
             return nldsc::launch_band_f4(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p,
                                          e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr,
                                          own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true, blk_rep,
-                                         which, st, miss);
+                                         which, st, miss, round_items);
         return nldsc::launch_band_i8(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p, e->pos.p,
                                      e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin,
                                      own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true, blk_rep, which, st);
@@ -776,6 +789,7 @@ int nldsc_engine_path(const nldsc_engine* e, int32_t* exact_i8, double* ops_alg_
 }
 
 int nldsc_engine_ksplit(const nldsc_engine* e) { return e ? e->last_ksplit : NLDSC_E_ARG; }
+int nldsc_engine_band_round_items(const nldsc_engine* e) { return e ? e->last_round_items : NLDSC_E_ARG; }
 int nldsc_engine_band_kernel(const nldsc_engine* e) { return e ? e->last_band_kernel : NLDSC_E_ARG; }
 
 int nldsc_ld_calculate(const nldsc_ld_params* p, nldsc_ld_result* r, char* err, size_t errlen) {

@@ -1601,7 +1601,8 @@ __global__ void __launch_bounds__(256, 2) band_f4_t2_kernel(
     const bool loads = !(dsup && w >= 2);
     const uint4* src = reinterpret_cast<const uint4*>(geno + (size_t)(my_blk * 32 + i) * (size_t)pitch_words) + h;
     const int n_st = n_it >> 1;  // two-chunk stages (rows are padded to 64 bytes)
-    // stage t (clamped to the last: the surplus loads of the tail land in buffers no one reads again) -> buffer t % S
+    // stage t (clamped to the last: the surplus loads of the tail rewrite the last stage's bytes into buffers no one
+    // reads again) -> buffer t % S
     // (inline asm: hipcc's own LDS-DMA tracking cannot tell the ring buffers apart and would wait vmcnt(0) before
     // every stage's first ds_read; the counted waits below order them instead)
     auto issue = [&](int t) {
@@ -1624,28 +1625,45 @@ __global__ void __launch_bounds__(256, 2) band_f4_t2_kernel(
     const bool rm = __any(lane < 32 && (sh.info[32 * sA + lane].fl & 4));
     const bool cm = __any(lane < 32 && (sh.info[64 + 32 * (w & 1) + lane].fl & 4));
 #pragma unroll
-    for (int t = 0; t < S - 1; ++t) issue(t);
+    for (int t = 0; t < S; ++t) issue(t);
 
     f32x16v gxx = {}, gxo = {}, gox = {}, goo = {}, gxh = {}, goh = {}, ghx = {}, gho = {};
+    // Stage t is read from LDS into registers one stage ahead (during stage t - 1's MFMAs), so no ds_read latency
+    // sits in front of a stage's first products.  At the barrier of iteration t every wave has stage t + 1 landed
+    // and has finished reading stage t (its reads were waited for before the barrier), so buffer t % S takes stage
+    // t + S right after it: S - 1 stages in flight, one in registers.
+    auto read_stage = [&](int t, uint4 (&a)[2], uint4 (&b)[2]) {
+        const uint4* A = &sh.stage[t % S][sA][0][0];
+        const uint4* B = &sh.stage[t % S][sB][0][0];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) { a[c] = A[c * 64 + lane]; b[c] = B[c * 64 + lane]; }
+    };
     auto kloop = [&](auto RMc, auto CMc, auto ACTc) {
         constexpr bool RM = decltype(RMc)::value, CM = decltype(CMc)::value, ACT = decltype(ACTc)::value;
+        uint4 ra[2], rb[2];
+        wait_vmcnt<2 * (S - 1)>();  // stage 0 landed (this wave's loads)
+        __builtin_amdgcn_s_barrier();  // every wave's
+        asm volatile("" ::: "memory");
+        if constexpr (ACT) read_stage(0, ra, rb);
         for (int t = 0; t < n_st; ++t) {
-            wait_vmcnt<2 * (S - 2)>();  // this wave's loads of stage t have landed
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();  // every wave's have, and every wave is done with buffer (t - 1) % S
+            wait_vmcnt<2 * (S - 2)>();  // this wave's loads of stage t + 1 have landed
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // its reads of stage t are in registers
+            __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
-            issue(t + S - 1);
+            issue(t + S);
             if constexpr (ACT) {
-                const uint4* A = &sh.stage[t % S][sA][0][0];
-                const uint4* B = &sh.stage[t % S][sB][0][0];
+                uint4 na[2], nb[2];
+                read_stage(t + 1, na, nb);  // past the last stage: a buffer of surplus bytes, never used
+                __builtin_amdgcn_sched_barrier(0);  // issued here, ahead of the products (the scheduler sinks them)
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
-                    const uint4 a = A[c * 64 + lane], b = B[c * 64 + lane];
-                    const F4Frag a0 = decode_f4(a.x, a.y), f0 = decode_f4(b.x, b.y);
+                    const F4Frag a0 = decode_f4(ra[c].x, ra[c].y), f0 = decode_f4(rb[c].x, rb[c].y);
                     f4_step<DOM, RM, CM>(a0, f0, gxx, gxo, gox, goo, gxh, goh, ghx, gho);
-                    const F4Frag a1 = decode_f4(a.z, a.w), f1 = decode_f4(b.z, b.w);
+                    const F4Frag a1 = decode_f4(ra[c].z, ra[c].w), f1 = decode_f4(rb[c].z, rb[c].w);
                     f4_step<DOM, RM, CM>(a1, f1, gxx, gxo, gox, goo, gxh, goh, ghx, gho);
                 }
+#pragma unroll
+                for (int c = 0; c < 2; ++c) { ra[c] = na[c]; rb[c] = nb[c]; }
             }
         }
     };
@@ -2068,13 +2086,16 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
-                          int which, hipStream_t st, const uint8_t* blk_miss) {
+                          int which, hipStream_t st, const uint8_t* blk_miss, int round_items) {
     if (n_items <= 0) return hipSuccess;
     if (max_nc != 1) return hipErrorInvalidValue;  // single block-pair items
     if (blk_miss != nullptr && n_it > F4_SEG_CHUNKS) return hipErrorInvalidValue;  // routing: unsegmented rows only
+    // round_items > 0: the items go in launches of that many (one round of the wave slots each), see ld_engine.cpp
+    const int chunk = round_items > 0 ? round_items : n_items;
 #define NLDSC_BAND(DOM_, WPS_, SEG_, KC_)                                                                           \
-    hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_, KC_>), dim3(n_items), dim3(64), 0, st, geno, pitch_words,  \
-                       n_it, cst, items, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi,       \
+    for (int o = 0; o < n_items; o += chunk)                                                                      \
+    hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_, KC_>), dim3(std::min(chunk, n_items - o)), dim3(64), 0, st, geno, pitch_words,  \
+                       n_it, cst, items + o, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi,       \
                        l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss)
 #define NLDSC_PICK(KC_)                                                                                              \
     if (n_it > F4_SEG_CHUNKS) { if (dom) NLDSC_BAND(true, 1, F4_SEG_CHUNKS, KC_); else NLDSC_BAND(false, 2, F4_SEG_CHUNKS, KC_); } \

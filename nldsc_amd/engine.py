@@ -103,7 +103,9 @@ class Engine:
         self._L.nldsc_engine_path(self._h, ctypes.byref(ex), ctypes.byref(ops))
         d.update(exact_i8=ex.value > 0, path={0: "f32", 1: "i8", 2: "f4"}[ex.value], ops_alg_i8=ops.value,
                  ksplit=self._L.nldsc_engine_ksplit(self._h),
-                 band_kernel=BAND_KERNELS.get(self._L.nldsc_engine_band_kernel(self._h), "?"))
+                 band_kernel=BAND_KERNELS.get(self._L.nldsc_engine_band_kernel(self._h), "?"),
+                 band_round_items=(self._L.nldsc_engine_band_round_items(self._h)
+                                   if hasattr(self._L, "nldsc_engine_band_round_items") else 0))
         return d
 
 

@@ -8,7 +8,7 @@ O=gpurun_out/$T
 mkdir -p $O
 for v in "$@"; do
   label=${v%%:*}; rest=${v#*:}; kv=${rest%%:*}; args=${rest#*:}
-  env "$kv" timeout -k 10 300 python bench.py --no-cpu --no-file $args > $O/bench_$label.json 2> $O/bench_$label.err \
+  env ${kv//,/ } timeout -k 10 300 python bench.py --no-cpu --no-file $args > $O/bench_$label.json 2> $O/bench_$label.err \
     || { echo "bench $label failed"; tail $O/bench_$label.err; exit 1; }
   python - "$O/bench_$label.json" "$label" <<'PY'
 import json, sys

@@ -111,6 +111,65 @@ __global__ void __launch_bounds__(64, 2) k16(float* out, int iters, int zero) {
     out[blockIdx.x * 64 + lane] = acc;
 }
 
+
+// decode as the band kernel does: 16 two-bit codes -> v (= code << 1), h, m nibble planes
+__device__ __forceinline__ void dec(uint32_t w, int& x0, int& x1, int& h0, int& h1, int& o0, int& o1) {
+    constexpr uint32_t M = 0x22222222u, K6 = 0x66666666u;
+    const uint32_t s1 = w << 1, s2 = w >> 1, w2 = w >> 2;
+    x0 = (int)(s1 & K6); x1 = (int)(s2 & K6); h0 = (int)(w & M); h1 = (int)(w2 & M);
+    o0 = (int)(s1 & ~w & M); o1 = (int)(s2 & ~w2 & M);
+}
+__device__ __forceinline__ Fr decf(uint32_t wa, uint32_t wb) {
+    int x0, x1, x2, x3, h0, h1, h2, h3, o0, o1, o2, o3;
+    dec(wa, x0, x1, h0, h1, o0, o1); dec(wb, x2, x3, h2, h3, o2, o3);
+    Fr f; f.v = i32x4{x0, x1, x2, x3}; f.h = i32x4{h0, h1, h2, h3}; f.m = i32x4{o0, o1, o2, o3};
+    return f;
+}
+__device__ __forceinline__ uint32_t codes(uint32_t seed) {  // 16 genotype-like 2-bit codes
+    uint32_t w = 0;
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t r = hash32(seed * 16 + k) & 1023u;
+        w |= (r < 10 ? 1u : r < 430 ? 2u : r < 520 ? 3u : 0u) << (2 * k);
+    }
+    return w;
+}
+// MODE 1: operands decoded every K step from code words held in registers (rotated per iteration);
+// MODE 2: code words loaded every K step from a 2.5 MB strip pair (L2-resident, all waves share it)
+template <int MODE>
+__global__ void __launch_bounds__(64, 2) k32d(float* out, const uint4* strip, int iters, int words) {
+    const int lane = threadIdx.x;
+    const uint32_t base = (blockIdx.x * 64 + lane) * 16;
+    uint4 ra = make_uint4(codes(base), codes(base + 1), codes(base + 2), codes(base + 3));
+    uint4 rb = make_uint4(codes(base + 4), codes(base + 5), codes(base + 6), codes(base + 7));
+    f32x16 g[8];
+    for (int p = 0; p < 8; ++p) g[p] = f32x16{};
+    int off = lane;
+    uint4 pa = ra, pb = rb, qa = ra, qb = rb;
+    for (int it = 0; it < iters; ++it) {
+        if (MODE == 2) {  // two iterations of prefetch distance
+            ra = pa; rb = pb; pa = qa; pb = qb;
+            qa = strip[off]; qb = strip[off + words];
+            off += 64; if (off >= words) off = lane;
+        } else {
+            ra.x = __builtin_amdgcn_alignbit(ra.x, ra.y, 2); ra.y = __builtin_amdgcn_alignbit(ra.y, ra.z, 2);
+            ra.z = __builtin_amdgcn_alignbit(ra.z, ra.w, 2); ra.w = __builtin_amdgcn_alignbit(ra.w, ra.x, 2);
+            rb.x = __builtin_amdgcn_alignbit(rb.x, rb.y, 2); rb.y = __builtin_amdgcn_alignbit(rb.y, rb.z, 2);
+            rb.z = __builtin_amdgcn_alignbit(rb.z, rb.w, 2); rb.w = __builtin_amdgcn_alignbit(rb.w, rb.x, 2);
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const Fr a = s ? decf(ra.z, ra.w) : decf(ra.x, ra.y), b = s ? decf(rb.z, rb.w) : decf(rb.x, rb.y);
+            g[0] = m32(a.v, b.v, g[0]); g[1] = m32(a.v, b.m, g[1]); g[2] = m32(a.v, b.h, g[2]);
+            g[3] = m32(a.m, b.v, g[3]); g[4] = m32(a.h, b.v, g[4]); g[5] = m32(a.m, b.m, g[5]);
+            g[6] = m32(a.m, b.h, g[6]); g[7] = m32(a.h, b.m, g[7]);
+        }
+    }
+    float acc = 0.f;
+    for (int p = 0; p < 8; ++p)
+        for (int r = 0; r < 16; ++r) acc += g[p][r];
+    out[blockIdx.x * 64 + lane] = acc;
+}
+
 int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 2000;
     const int grid = 256 * 8;  // 2 waves per SIMD on every CU
@@ -138,6 +197,41 @@ int main(int argc, char** argv) {
                        flop / (ms * 1e-3) / 1e12);
                 fflush(stdout);
             }
+        }
+    }
+    // decode-fed and load-fed loops: 2 K steps per iteration, so twice the iterations for the same FLOPs
+    const int words = 2 * 78912 / 16 * 32;  // two 32-row strips of a C3 row (uint4 units per strip pair / 2)
+    uint4* strip;
+    hipMalloc(&strip, (size_t)2 * words * sizeof(uint4));
+    hipLaunchKernelGGL(k32d<1>, dim3(1), dim3(64), 0, 0, out, strip, 0, words);  // load the module
+    {
+        uint32_t* h = (uint32_t*)malloc((size_t)2 * words * sizeof(uint4));
+        for (size_t k = 0; k < (size_t)8 * words; ++k) {
+            uint32_t w = 0;
+            for (int j = 0; j < 16; ++j) {
+                uint32_t r = (uint32_t)((k * 16 + j) * 2654435761u) >> 22;
+                w |= (r < 10 ? 1u : r < 430 ? 2u : r < 520 ? 3u : 0u) << (2 * j);
+            }
+            h[k] = w;
+        }
+        hipMemcpy(strip, h, (size_t)2 * words * sizeof(uint4), hipMemcpyHostToDevice);
+        free(h);
+    }
+    for (int rep = 0; rep < 2; ++rep) {
+        for (int mode = 1; mode <= 2; ++mode) {
+            for (int w = 0; w < 6; ++w) {
+                if (w == 3) hipEventRecord(e0);
+                if (mode == 1) k32d<1><<<grid, 64>>>(out, strip, 2 * iters, words);
+                else k32d<2><<<grid, 64>>>(out, strip, 2 * iters, words);
+            }
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms = 0;
+            hipEventElapsedTime(&ms, e0, e1);
+            ms /= 3;
+            printf("{\"shape\": \"32x32x64\", \"data\": \"%s\", \"rep\": %d, \"ms\": %.3f, \"tflops\": %.1f}\n",
+                   mode == 1 ? "decoded in registers" : "decoded from L2 loads", rep, ms, flop / (ms * 1e-3) / 1e12);
+            fflush(stdout);
         }
     }
     return hipGetLastError() != hipSuccess;
