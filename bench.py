@@ -397,9 +397,12 @@ def main():
             "data": "synthetic (GPU-generated PLINK .bed, AR(1) haplotypes, %g%% missing calls; %s)"
                     % (100 * args.missing, "one chromosome split over the GPUs" if split else "one chromosome per GPU"),
             "config": {
-                "workload": (("C3 (BASELINE.json configs[2]): chr1-like N=%d individuals, M=%d SNPs over %.0f cM, "
+                "workload": (("%s: chr1-like N=%d individuals, M=%d SNPs over %.0f cM, "
                               "%s, --ld-wind-cm %g, maf %g, std-thr %g, rsq 1/M" %
-                              (N, M, args.length_cm, "additive only" if args.additive_only else "additive+dominance",
+                              ("C2 (BASELINE.json configs[1])" if N == 50_000 and args.additive_only else
+                               "C3 (BASELINE.json configs[2])" if N == 315_599 and not args.additive_only else
+                               "C3-shaped variant (BASELINE.json configs[2] with N / coding changed)",
+                               N, M, args.length_cm, "additive only" if args.additive_only else "additive+dominance",
                                w, args.maf, args.std_thr)) if args.workload == "c3" else
                              ("C5 slice (BASELINE.json configs[4]: imputed genome, M~10M over 2.88 Gb, --ld-wind-kb "
                               "1000, 8 GPUs): per GPU N=%d individuals, M=%d SNPs over %.0f Mb (1/8 genome at M=1.25M), "
