@@ -68,7 +68,7 @@ def kernel_source_sha16() -> str:
 
 
 def pmc_traffic(kernel_key: str, n_org: int, n_snp: int, missing: float):
-    """HBM-side bytes per launch of `kernel_key` from the committed rocprofv3 PMC summary measured on the same
+    """HBM-side bytes per engine run of `kernel_key` (all its launches) from the committed rocprofv3 PMC summary measured on the same
     workload AND the same kernel source (profiles/*_pmc*.json carrying `kernels_source_sha16`): (bytes, file),
     or (None, reason) when no summary matches the current kernels."""
     import glob
@@ -91,7 +91,7 @@ def pmc_traffic(kernel_key: str, n_org: int, n_snp: int, missing: float):
             stale = stale or os.path.relpath(path, REPO)
             continue
         keys = [kernel_key] if isinstance(kernel_key, str) else list(kernel_key)
-        found = [k["traffic_bytes"] for name, k in doc.get("kernels", {}).items()
+        found = [k.get("traffic_bytes_per_run", k["traffic_bytes"]) for name, k in doc.get("kernels", {}).items()
                  if any(name.startswith(key + "<") or name == key for key in keys)]
         if found:  # (the routed fp4 band: both kernels' bytes per launch pair)
             return float(sum(found)), os.path.relpath(path, REPO)
@@ -371,6 +371,11 @@ def main():
         roof.update(traffic=traffic, traffic_source=traffic_src,
                     algorithmic_bytes_per_launch=eng.n_snp * 4 * ((((N + 3) // 4) + 31) // 32 * 8),
                     avg_launch_ms=band_ms,
+                    launch_note=("the band of one run (all its launches: %d items in launches of %d, one round of "
+                                 "the wave slots each; rocprofv3 lists each launch) timed with HIP events on the "
+                                 "engine stream" % (tims[-1]["band_items"], tims[-1]["band_round_items"])
+                                 if tims[-1].get("band_round_items") else
+                                 "one band launch per run, timed with HIP events on the engine stream"),
                     issued_per_launch=tims[-1]["flop_issued"], work_items=tims[-1]["band_items"],
                     mfma_pipe_frac=tims[-1]["flop_issued"] / t_band / 1e12 / peak,
                     fp32_equivalent_tflops=flop / t_band / 1e12,

@@ -13,7 +13,8 @@
 
 FETCH_SIZE / WRITE_SIZE are in KB; gfx950 reports half of wide streaming reads, so FETCH_SIZE is
 doubled (calibrated by repack_count_kernel, whose corrected fetch equals its .bed input).  Values are
-averaged over the launches of each kernel (per launch).  MFMA busy fraction per SIMD =
+averaged over the launches of each kernel (per launch); `traffic_bytes_per_run` sums a kernel's launches of one
+engine run (the band kernel goes in several launches of one round each).  MFMA busy fraction per SIMD =
 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs); effective clock = GRBM_GUI_ACTIVE / 8 /
 duration (GRBM_GUI_ACTIVE is reported summed over the 8 XCDs).
 """
@@ -60,6 +61,8 @@ def main():
     args = ap.parse_args()
     alg = dict((k, float(v)) for k, v in (a.split("=") for a in args.alg_bytes))
     fetch, write, sq, l2 = (read_counters(os.path.join(args.dir, p)) for p in ("fetch", "write", "sq", "l2"))
+    # engine runs in the profiled command: finalize_kernel runs once per run (the band may take several launches)
+    runs = len(fetch.get("finalize_kernel", {}).get("FETCH_SIZE", [])) or None
     kernels = {}
     for name in sorted(set(fetch) | set(write) | set(sq)):
         if name.startswith("__amd"):
@@ -74,10 +77,14 @@ def main():
              "fetch_bytes_corrected_x2": 2 * f * 1024 if f is not None else None,
              "write_bytes": w * 1024 if w is not None else None}
         k["traffic_bytes"] = (k["fetch_bytes_corrected_x2"] or 0) + (k["write_bytes"] or 0)
+        n_disp = len(fetch.get(name, {}).get("FETCH_SIZE", []))
+        if runs and n_disp:  # per engine run: all launches of this kernel in one run
+            k["dispatches_per_run"] = n_disp / runs
+            k["traffic_bytes_per_run"] = k["traffic_bytes"] * n_disp / runs
         base = name.split("<")[0]
         if base in alg:
             k["algorithmic_bytes"] = alg[base]
-            k["traffic_over_algorithmic"] = k["traffic_bytes"] / alg[base]
+            k["traffic_over_algorithmic"] = k.get("traffic_bytes_per_run", k["traffic_bytes"]) / alg[base]
         k.update(duration_s_pmc_run=dur, grbm_gui_active=g, sq_valu_mfma_busy_cycles=busy, sq_insts_valu=valu)
         if g and busy is not None:
             k["mfma_busy_frac_per_simd"] = busy / (g / N_XCD * N_SIMD)

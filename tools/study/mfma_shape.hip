@@ -170,6 +170,44 @@ __global__ void __launch_bounds__(64, 2) k32d(float* out, const uint4* strip, in
     out[blockIdx.x * 64 + lane] = acc;
 }
 
+// 64 x 32 tile per wave at 1 wave per SIMD: two row fragments share one column fragment's decode (3 decodes per
+// 16 products instead of 2 per 8), operands decoded every K step from code words in registers
+__global__ void __launch_bounds__(64, 1) k64d(float* out, int iters) {
+    const int lane = threadIdx.x;
+    const uint32_t base = (blockIdx.x * 64 + lane) * 16;
+    uint4 ra = make_uint4(codes(base), codes(base + 1), codes(base + 2), codes(base + 3));
+    uint4 rc = make_uint4(codes(base + 8), codes(base + 9), codes(base + 10), codes(base + 11));
+    uint4 rb = make_uint4(codes(base + 4), codes(base + 5), codes(base + 6), codes(base + 7));
+    f32x16 g[2][8];
+    for (int q = 0; q < 2; ++q)
+        for (int p = 0; p < 8; ++p) g[q][p] = f32x16{};
+    for (int it = 0; it < iters; ++it) {
+        ra.x = __builtin_amdgcn_alignbit(ra.x, ra.y, 2); ra.y = __builtin_amdgcn_alignbit(ra.y, ra.z, 2);
+        ra.z = __builtin_amdgcn_alignbit(ra.z, ra.w, 2); ra.w = __builtin_amdgcn_alignbit(ra.w, ra.x, 2);
+        rc.x = __builtin_amdgcn_alignbit(rc.x, rc.y, 2); rc.y = __builtin_amdgcn_alignbit(rc.y, rc.z, 2);
+        rc.z = __builtin_amdgcn_alignbit(rc.z, rc.w, 2); rc.w = __builtin_amdgcn_alignbit(rc.w, rc.x, 2);
+        rb.x = __builtin_amdgcn_alignbit(rb.x, rb.y, 2); rb.y = __builtin_amdgcn_alignbit(rb.y, rb.z, 2);
+        rb.z = __builtin_amdgcn_alignbit(rb.z, rb.w, 2); rb.w = __builtin_amdgcn_alignbit(rb.w, rb.x, 2);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const Fr b = s ? decf(rb.z, rb.w) : decf(rb.x, rb.y);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint4& r = q ? rc : ra;
+                const Fr a = s ? decf(r.z, r.w) : decf(r.x, r.y);
+                g[q][0] = m32(a.v, b.v, g[q][0]); g[q][1] = m32(a.v, b.m, g[q][1]); g[q][2] = m32(a.v, b.h, g[q][2]);
+                g[q][3] = m32(a.m, b.v, g[q][3]); g[q][4] = m32(a.h, b.v, g[q][4]); g[q][5] = m32(a.m, b.m, g[q][5]);
+                g[q][6] = m32(a.m, b.h, g[q][6]); g[q][7] = m32(a.h, b.m, g[q][7]);
+            }
+        }
+    }
+    float acc = 0.f;
+    for (int q = 0; q < 2; ++q)
+        for (int p = 0; p < 8; ++p)
+            for (int r = 0; r < 16; ++r) acc += g[q][p][r];
+    out[blockIdx.x * 64 + lane] = acc;
+}
+
 int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 2000;
     const int grid = 256 * 8;  // 2 waves per SIMD on every CU
@@ -233,6 +271,20 @@ int main(int argc, char** argv) {
                    mode == 1 ? "decoded in registers" : "decoded from L2 loads", rep, ms, flop / (ms * 1e-3) / 1e12);
             fflush(stdout);
         }
+    }
+    for (int rep = 0; rep < 2; ++rep) {  // 64 x 32 tiles: half the waves (1 per SIMD), same FLOPs per launch
+        for (int w = 0; w < 6; ++w) {
+            if (w == 3) hipEventRecord(e0);
+            k64d<<<grid / 2, 64>>>(out, 2 * iters);
+        }
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms = 0;
+        hipEventElapsedTime(&ms, e0, e1);
+        ms /= 3;
+        printf("{\"shape\": \"32x32x64, 64x32 tile per wave\", \"data\": \"decoded in registers\", \"rep\": %d, "
+               "\"ms\": %.3f, \"tflops\": %.1f}\n", rep, ms, flop / (ms * 1e-3) / 1e12);
+        fflush(stdout);
     }
     return hipGetLastError() != hipSuccess;
 }
