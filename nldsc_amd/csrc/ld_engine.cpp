@@ -677,10 +677,13 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     // of a launch start together and, all of equal length, stay at nearby K offsets, so the waves on one XCD that
     // share a strip (the plan's 16 x 16 tiles) read it from that XCD's L2.  In one launch of all items the waves
     // drift apart and most strip bytes come from beyond L2 again (C3: 68 -> 14 GB per band, the clock 1.90 -> 2.02
-    // GHz; band -2 to -3 % after the launch tails).  Only for launches of several rounds.
+    // GHz; band -2 to -4 % after the launch tails).  Only for bands of several rounds, and only for long rows: the
+    // waves of a round also reach their epilogues together, which then no longer overlap another wave's products —
+    // at N = 50 000 (strips of 0.4 MB, L2-resident anyway; epilogue ~1/3 of an item) round launches made the band
+    // 2.8 -> 5.1 ms.
     const int slots = 8 * e->n_cu;
-    const int round_items =
-        use_f4 && ksplit == 1 && e->band_rounds && n_it <= nldsc::F4_SEG_CHUNKS && n_items >= 4 * slots ? slots : 0;
+    const int round_items = use_f4 && ksplit == 1 && e->band_rounds && n_it <= nldsc::F4_SEG_CHUNKS &&
+                            n_it >= 1024 && n_items >= 4 * slots ? slots : 0;
     e->last_round_items = round_items;
     // which = 1: the launch for the items without a replayed SNP (beside the replay), 2: the KC launch after it
     const uint8_t* blk_rep = replay ? e->blk_rep.p : nullptr;
