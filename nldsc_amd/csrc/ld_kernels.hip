@@ -1203,6 +1203,7 @@ __global__ void __launch_bounds__(64, 2) band_i8_kernel(const uint32_t* __restri
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 constexpr int E8M0_ONE = 127;  // block scale 2^0
+constexpr int E8M0_HALF = 126;  // 2^-1
 // VALU instructions interleaved after each MFMA of a full 8-product K step (3, 5, 6 and alternating 4/5
 // measured slower in round 1)
 constexpr int F4_VPM = 4;
@@ -1215,22 +1216,34 @@ struct F4Frag {
 // pairs into the *1 dword (any fixed slot permutation is fine: both operands use it).  The first plane is
 // the code itself moved to nibble bits 2:1 — v = 0 (00 hom A1), 1.0 (01 missing), 2.0 (10 het), 4.0
 // (11 hom A2) = m + 2x — which costs two VALU ops per dword instead of the three of x itself; the
-// epilogue recovers the x products exactly.  h = [b1] and m = [b0 & ~b1] land on bit 1 (1.0).
+// epilogue recovers the x products exactly.  WM (the block holds missing calls): h = [b1] and m = [b0 & ~b1]
+// land on bit 1 (1.0), 9 VALU per word (m is one v_bitop3).  !WM (missing-free block: no m plane): h is taken
+// from the two shifted words at bit 2 (2.0; the MFMAs scale such an h operand by 2^-1 through its E8M0 block
+// scale, see H_SCALE), 6 VALU per word instead of 7.
+template <bool WM>
 __device__ __forceinline__ void decode_f4_word(uint32_t w, int& x0, int& x1, int& h0, int& h1, int& o0, int& o1) {
-    constexpr uint32_t M = 0x22222222u, K6 = 0x66666666u;  // bit 1 / bits 2:1 of every nibble
-    const uint32_t s1 = w << 1, s2 = w >> 1, w2 = w >> 2;
+    constexpr uint32_t M = 0x22222222u, K6 = 0x66666666u, M4 = 0x44444444u;
+    const uint32_t s1 = w << 1, s2 = w >> 1;
     x0 = (int)(s1 & K6);       // even (b1, b0) at bits (1, 0) -> (2, 1)
     x1 = (int)(s2 & K6);       // odd  (b1, b0) at bits (3, 2) -> (2, 1)
-    h0 = (int)(w & M);
-    h1 = (int)(w2 & M);
-    o0 = (int)(s1 & ~w & M);   // m: code 01 -> 0010 (1.0), else 0
-    o1 = (int)(s2 & ~w2 & M);
+    if constexpr (WM) {
+        const uint32_t w2 = w >> 2;
+        h0 = (int)(w & M);
+        h1 = (int)(w2 & M);
+        o0 = (int)(s1 & ~w & M);   // m: code 01 -> 0010 (1.0), else 0
+        o1 = (int)(s2 & ~w2 & M);
+    } else {
+        h0 = (int)(s1 & M4);       // b1 -> bit 2 (2.0)
+        h1 = (int)(s2 & M4);
+        o0 = o1 = 0;
+    }
 }
 
+template <bool WM>
 __device__ __forceinline__ F4Frag decode_f4(uint32_t wa, uint32_t wb) {
     int x0, x1, x2, x3, h0, h1, h2, h3, o0, o1, o2, o3;
-    decode_f4_word(wa, x0, x1, h0, h1, o0, o1);
-    decode_f4_word(wb, x2, x3, h2, h3, o2, o3);
+    decode_f4_word<WM>(wa, x0, x1, h0, h1, o0, o1);
+    decode_f4_word<WM>(wb, x2, x3, h2, h3, o2, o3);
     F4Frag f;
     f.x = i32x4{x0, x1, x2, x3};
     f.h = i32x4{h0, h1, h2, h3};
@@ -1238,9 +1251,15 @@ __device__ __forceinline__ F4Frag decode_f4(uint32_t wa, uint32_t wb) {
     return f;
 }
 
+// E8M0 block scale of an h operand decoded with decode_f4<WM>: h is 1.0 (WM) or 2.0 (!WM) per set slot
+template <bool WM>
+constexpr int H_SCALE = WM ? E8M0_ONE : E8M0_HALF;
+
+// SA / SB: E8M0 block scales of the A / B operand (H_SCALE for an h plane)
+template <int SA = E8M0_ONE, int SB = E8M0_ONE>
 __device__ __forceinline__ f32x16v mfma_f4(const i32x4& a, const i32x4& b, const f32x16v& c) {
     const i32x8 A = {a[0], a[1], a[2], a[3], 0, 0, 0, 0}, B = {b[0], b[1], b[2], b[3], 0, 0, 0, 0};
-    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, c, 4, 4, 0, E8M0_ONE, 0, E8M0_ONE);
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, c, 4, 4, 0, SA, 0, SB);
 }
 
 // NC column blocks J0 .. J0+NC-1 share the row strip's decode; DIAG0: block 0 is the diagonal.
@@ -1300,12 +1319,12 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         for (int c = 0; c < NC; ++c) {
             gxx[c] = mfma_f4(a.x, b[c].x, gxx[c]);
             if (CM) gxo[c] = mfma_f4(a.x, b[c].o, gxo[c]);
-            if (DOM) gxh[c] = mfma_f4(a.x, b[c].h, gxh[c]);
+            if (DOM) gxh[c] = mfma_f4<E8M0_ONE, H_SCALE<CM>>(a.x, b[c].h, gxh[c]);
             if (RM && !(DIAG0 && c == 0)) gox[c] = mfma_f4(a.o, b[c].x, gox[c]);
-            if (DOM && !(DIAG0 && c == 0)) ghx[c] = mfma_f4(a.h, b[c].x, ghx[c]);
+            if (DOM && !(DIAG0 && c == 0)) ghx[c] = mfma_f4<H_SCALE<RM>, E8M0_ONE>(a.h, b[c].x, ghx[c]);
             if (RM && CM) goo[c] = mfma_f4(a.o, b[c].o, goo[c]);
-            if (DOM && RM) goh[c] = mfma_f4(a.o, b[c].h, goh[c]);
-            if (DOM && CM && !(DIAG0 && c == 0)) gho[c] = mfma_f4(a.h, b[c].o, gho[c]);
+            if (DOM && RM) goh[c] = mfma_f4<E8M0_ONE, H_SCALE<CM>>(a.o, b[c].h, goh[c]);
+            if (DOM && CM && !(DIAG0 && c == 0)) gho[c] = mfma_f4<H_SCALE<RM>, E8M0_ONE>(a.h, b[c].o, gho[c]);
         }
         // full 8-product steps: F4_VPM VALU after each MFMA; otherwise (additive-only items, missing-free
         // blocks) the decode is spread evenly over the MFMAs there are (additive-only C2: -6.6 % band time)
@@ -1317,7 +1336,7 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
             }
         } else {
             constexpr int n_mfma = NC * (1 + CM + RM + (RM && CM) + (DOM ? 2 + RM + CM : 0));
-            constexpr int n_valu = NC * (RM ? 9 : 7) * 2 + NC * (CM ? 9 : 7) * 2;
+            constexpr int n_valu = NC * (RM ? 9 : 6) * 2 + NC * (CM ? 9 : 6) * 2;
 #pragma unroll
             for (int m = 0; m < n_mfma; ++m) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -1329,37 +1348,38 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     // even chunks, Q odd ones; each is reloaded right after its last word is decoded and read again two K
     // steps later, with no register copies of loads in flight (those would force vmcnt(0)).
     auto kloop = [&](auto RMc, auto CMc, const int t_lo, const int t_hi) {
+        constexpr bool RM = decltype(RMc)::value, CM = decltype(CMc)::value;
         const int last = t_hi - 1;
         uint4 pr = rowp[2 * t_lo], qr = rowp[2 * t_lo + 2], pc[NC], qc[NC];
 #pragma unroll
         for (int c = 0; c < NC; ++c) { pc[c] = colp[c][2 * t_lo]; qc[c] = colp[c][2 * t_lo + 2]; }
         // two named fragment sets: set 1 is decoded while set 0 feeds the MFMAs and vice versa, so no
         // fragment is copied (a single rotating set costs ~12 v_mov per K step)
-        F4Frag a0 = decode_f4(pr.x, pr.y), a1, b0[NC], b1[NC];
+        F4Frag a0 = decode_f4<RM>(pr.x, pr.y), a1, b0[NC], b1[NC];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) b0[c] = decode_f4(pc[c].x, pc[c].y);
+        for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(pc[c].x, pc[c].y);
         for (int t = t_lo; t < t_hi; t += 2) {
-            a1 = decode_f4(pr.z, pr.w);
+            a1 = decode_f4<RM>(pr.z, pr.w);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b1[c] = decode_f4(pc[c].z, pc[c].w);
+            for (int c = 0; c < NC; ++c) b1[c] = decode_f4<CM>(pc[c].z, pc[c].w);
             mfmas_v(a0, b0, RMc, CMc);  // K step 2t   (chunk t, words 0-1)
             pr = rowp[2 * min(t + 2, last)];
 #pragma unroll
             for (int c = 0; c < NC; ++c) pc[c] = colp[c][2 * min(t + 2, last)];
-            a0 = decode_f4(qr.x, qr.y);
+            a0 = decode_f4<RM>(qr.x, qr.y);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b0[c] = decode_f4(qc[c].x, qc[c].y);
+            for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(qc[c].x, qc[c].y);
             mfmas_v(a1, b1, RMc, CMc);  // K step 2t+1 (chunk t, words 2-3)
-            a1 = decode_f4(qr.z, qr.w);
+            a1 = decode_f4<RM>(qr.z, qr.w);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b1[c] = decode_f4(qc[c].z, qc[c].w);
+            for (int c = 0; c < NC; ++c) b1[c] = decode_f4<CM>(qc[c].z, qc[c].w);
             mfmas_v(a0, b0, RMc, CMc);  // K step 2t+2 (chunk t+1, words 0-1)
             qr = rowp[2 * min(t + 3, last)];
 #pragma unroll
             for (int c = 0; c < NC; ++c) qc[c] = colp[c][2 * min(t + 3, last)];
-            a0 = decode_f4(pr.x, pr.y);
+            a0 = decode_f4<RM>(pr.x, pr.y);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b0[c] = decode_f4(pc[c].x, pc[c].y);
+            for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(pc[c].x, pc[c].y);
             mfmas_v(a1, b1, RMc, CMc);  // K step 2t+3 (chunk t+1, words 2-3)
         }
     };
@@ -1537,14 +1557,14 @@ __device__ __forceinline__ void f4_step(const F4Frag& a, const F4Frag& b, f32x16
                                         f32x16v& goo, f32x16v& gxh, f32x16v& goh, f32x16v& ghx, f32x16v& gho) {
     gxx = mfma_f4(a.x, b.x, gxx);
     if (CM) gxo = mfma_f4(a.x, b.o, gxo);
-    if (DOM) gxh = mfma_f4(a.x, b.h, gxh);
+    if (DOM) gxh = mfma_f4<E8M0_ONE, H_SCALE<CM>>(a.x, b.h, gxh);
     if (RM) gox = mfma_f4(a.o, b.x, gox);
-    if (DOM) ghx = mfma_f4(a.h, b.x, ghx);
+    if (DOM) ghx = mfma_f4<H_SCALE<RM>, E8M0_ONE>(a.h, b.x, ghx);
     if (RM && CM) goo = mfma_f4(a.o, b.o, goo);
-    if (DOM && RM) goh = mfma_f4(a.o, b.h, goh);
-    if (DOM && CM) gho = mfma_f4(a.h, b.o, gho);
+    if (DOM && RM) goh = mfma_f4<E8M0_ONE, H_SCALE<CM>>(a.o, b.h, goh);
+    if (DOM && CM) gho = mfma_f4<H_SCALE<RM>, E8M0_ONE>(a.h, b.o, gho);
     constexpr int n_mfma = 1 + CM + RM + (RM && CM) + (DOM ? 2 + RM + CM : 0);
-    constexpr int n_valu = 2 * 9 + 2 * 9;  // the next step's two decodes
+    constexpr int n_valu = (RM ? 18 : 12) + (CM ? 18 : 12);  // the next step's two decodes
 #pragma unroll
     for (int m = 0; m < n_mfma; ++m) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -1657,9 +1677,9 @@ __global__ void __launch_bounds__(256, 2) band_f4_t2_kernel(
                 __builtin_amdgcn_sched_barrier(0);  // issued here, ahead of the products (the scheduler sinks them)
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
-                    const F4Frag a0 = decode_f4(ra[c].x, ra[c].y), f0 = decode_f4(rb[c].x, rb[c].y);
+                    const F4Frag a0 = decode_f4<RM>(ra[c].x, ra[c].y), f0 = decode_f4<CM>(rb[c].x, rb[c].y);
                     f4_step<DOM, RM, CM>(a0, f0, gxx, gxo, gox, goo, gxh, goh, ghx, gho);
-                    const F4Frag a1 = decode_f4(ra[c].z, ra[c].w), f1 = decode_f4(rb[c].z, rb[c].w);
+                    const F4Frag a1 = decode_f4<RM>(ra[c].z, ra[c].w), f1 = decode_f4<CM>(rb[c].z, rb[c].w);
                     f4_step<DOM, RM, CM>(a1, f1, gxx, gxo, gox, goo, gxh, goh, ghx, gho);
                 }
 #pragma unroll
