@@ -2110,8 +2110,9 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
     if (n_items <= 0) return hipSuccess;
     if (max_nc != 1) return hipErrorInvalidValue;  // single block-pair items
     if (blk_miss != nullptr && n_it > F4_SEG_CHUNKS) return hipErrorInvalidValue;  // routing: unsegmented rows only
-    // round_items > 0: the items go in launches of that many (one round of the wave slots each), see ld_engine.cpp
-    const int chunk = round_items > 0 ? round_items : n_items;
+    // round_items > 0: the items go in launches of that many (one round of the wave slots each), see ld_engine.cpp;
+    // not the KC launch (items holding a replayed rare variant: few, the others return at once)
+    int chunk = round_items > 0 ? round_items : n_items;
 #define NLDSC_BAND(DOM_, WPS_, SEG_, KC_)                                                                           \
     for (int o = 0; o < n_items; o += chunk)                                                                      \
     hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_, KC_>), dim3(std::min(chunk, n_items - o)), dim3(64), 0, st, geno, pitch_words,  \
@@ -2123,6 +2124,7 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
     else NLDSC_BAND(false, 2, 0, KC_)
     // segmented kernel: the add+dom variant needs more than 256 registers (2 waves / SIMD would spill)
     if (which & 1) { NLDSC_PICK(false); }
+    chunk = n_items;
     if (blk_rep && (which & 2)) { NLDSC_PICK(true); }
 #undef NLDSC_PICK
 #undef NLDSC_BAND
