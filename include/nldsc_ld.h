@@ -127,6 +127,8 @@ int nldsc_engine_ksplit(const nldsc_engine* e);
  * its items went in launches of one round of the GPU's wave slots each (so the items of a launch stay at nearby K
  * offsets and share their strips through L2), 0 when they went in one launch. */
 int nldsc_engine_band_round_items(const nldsc_engine* e);
+/* K-split factor of the last run's partial last round when its band went in round launches (1: not split). */
+int nldsc_engine_band_tail_ksplit(const nldsc_engine* e);
 /* Band kernel of the last run: NLDSC_BAND_F32 (fp32 MFMA GEMM), NLDSC_BAND_I8, NLDSC_BAND_F4 (one wave per
  * 32x32 block pair), NLDSC_BAND_F4_SEG (rows above 2^19 samples), NLDSC_BAND_F4_KSPLIT, NLDSC_BAND_F4_2X2
  * (4-wave workgroups over 2x2 block pairs sharing their strips through LDS), NLDSC_BAND_F4_ROUTED (the default

@@ -131,6 +131,7 @@ struct nldsc_engine {
     bool replay_overlap = true;  // $NLDSC_REPLAY_OVERLAP=0 runs the rare-variant replay in line on the main stream
     int last_ksplit = 1;
     int last_round_items = 0;
+    int last_tail_ksplit = 1;
     // fp4 band kernels on the GPU plan ($NLDSC_T2): 1 (default) missing-free super-items in the 2 x 2 block-pair
     // workgroups, the rest in the single-block kernel; 2 everything in the 2 x 2 workgroups; 0 single-block only
     int t2_mode = 1;
@@ -685,6 +686,13 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     const int round_items = use_f4 && ksplit == 1 && e->band_rounds && n_it <= nldsc::F4_SEG_CHUNKS &&
                             n_it >= 1024 && n_items >= 4 * slots ? slots : 0;
     e->last_round_items = round_items;
+    // The last, partial round leaves wave slots idle for a whole item length (C3: 1 458 items in 2 048 slots); those
+    // items are K-split instead when the cost model finds it cheaper (C3: P = 7, 5 rounds of 1/7 of an item).
+    const int tail = round_items > 0 ? n_items % round_items : 0;
+    const int tail_p = tail > 0 ? choose_ksplit(tail) : 1;
+    const int n_full = tail_p > 1 ? n_items - tail : n_items;
+    e->last_tail_ksplit = tail_p;
+    if (tail_p > 1) HIPCHK(e->gram.ensure((size_t)tail * tail_p * 8192));
     // which = 1: the launch for the items without a replayed SNP (beside the replay), 2: the KC launch after it
     const uint8_t* blk_rep = replay ? e->blk_rep.p : nullptr;
     auto launch_band_path = [&](int which) -> hipError_t {
@@ -701,11 +709,17 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
                                                e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N,
                                                p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p,
                                                blk_rep, e->gram.p, which, st);
-        if (use_f4)
-            return nldsc::launch_band_f4(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p,
-                                         e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr,
-                                         own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true, blk_rep,
-                                         which, st, miss, round_items);
+        if (use_f4) {
+            hipError_t r = nldsc::launch_band_f4(dom, max_nc, n_full, geno, pitch_words, n_it, e->cst.p, e->items.p,
+                                                 e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N,
+                                                 p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
+                                                 e->ws_acc.p, true, blk_rep, which, st, miss, round_items);
+            if (r != hipSuccess || n_full == n_items) return r;
+            return nldsc::launch_band_f4_split(dom, tail_p, n_items - n_full, geno, pitch_words, n_it, e->cst.p,
+                                               e->items.p + n_full, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
+                                               p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p,
+                                               e->l2d_acc.p, e->ws_acc.p, blk_rep, e->gram.p, which, st, miss);
+        }
         return nldsc::launch_band_i8(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p, e->pos.p,
                                      e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin,
                                      own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true, blk_rep, which, st);
@@ -793,6 +807,7 @@ int nldsc_engine_path(const nldsc_engine* e, int32_t* exact_i8, double* ops_alg_
 
 int nldsc_engine_ksplit(const nldsc_engine* e) { return e ? e->last_ksplit : NLDSC_E_ARG; }
 int nldsc_engine_band_round_items(const nldsc_engine* e) { return e ? e->last_round_items : NLDSC_E_ARG; }
+int nldsc_engine_band_tail_ksplit(const nldsc_engine* e) { return e ? e->last_tail_ksplit : NLDSC_E_ARG; }
 int nldsc_engine_band_kernel(const nldsc_engine* e) { return e ? e->last_band_kernel : NLDSC_E_ARG; }
 
 int nldsc_ld_calculate(const nldsc_ld_params* p, nldsc_ld_result* r, char* err, size_t errlen) {

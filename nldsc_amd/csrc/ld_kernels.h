@@ -79,7 +79,8 @@ hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* ge
                                 const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                                 const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr,
                                 int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc,
-                                const uint8_t* blk_rep, float* gram, int which, hipStream_t st);
+                                const uint8_t* blk_rep, float* gram, int which, hipStream_t st,
+                                const uint8_t* blk_miss = nullptr);
 // 2 x 2 block-pair workgroups (unsegmented rows, gpu plan): super-items (I2, J2, 1, 0) over row / column
 // super-blocks of two 32-SNP blocks, planned from the single-block rows (launch_plan) by launch_plan_super (meta2
 // as meta; counts2 capacity ceil(nblk2/16)^2) and launch_plan_emit_super; the kernel reads `rows` (nblk) to skip the

@@ -1752,11 +1752,14 @@ __global__ void __launch_bounds__(64, 2) band_f4_part_kernel(const uint32_t* __r
                                                            const double* __restrict__ pos, const int* __restrict__ Lw,
                                                            const int* __restrict__ Rw,
                                                            const uint8_t* __restrict__ sflags, int n_snp, int P,
-                                                           float* __restrict__ gram) {
+                                                           float* __restrict__ gram,
+                                                           const uint8_t* __restrict__ blk_miss) {
     __shared__ BandI8Lds sh;
     __shared__ float tr[32 * 33];
     const int u = xcd_slot(blockIdx.x, gridDim.x), item = u / P, piece = u % P;
     const int4 it = items[item];
+    // blk_miss: the 2 x 2 kernel runs the missing-free super-items (band_f4_epi_kernel skips the same items)
+    if (blk_miss != nullptr && t2_routed(blk_miss, it.x >> 1, it.y >> 1, (n_snp + 31) >> 5)) return;
     const int t_lo = (int)(((long long)piece * n_it / P) & ~1LL);
     const int t_hi = piece == P - 1 ? n_it : (int)(((long long)(piece + 1) * n_it / P) & ~1LL);
     float* part = gram + (size_t)u * 8192;
@@ -1777,11 +1780,13 @@ __global__ void __launch_bounds__(64, 2) band_f4_epi_kernel(const SnpConst* __re
                                                           int own_hi, double* __restrict__ l2_acc,
                                                           double* __restrict__ l2d_acc, int* __restrict__ ws_acc,
                                                           const uint8_t* __restrict__ blk_rep, int P,
-                                                          const float* __restrict__ gram) {
+                                                          const float* __restrict__ gram,
+                                                          const uint8_t* __restrict__ blk_miss) {
     __shared__ BandI8Lds sh;
     __shared__ float tr[32 * 33];
     const int4 it = items[blockIdx.x];
     if (skip_item<KC>(blk_rep, it)) return;
+    if (blk_miss != nullptr && t2_routed(blk_miss, it.x >> 1, it.y >> 1, (n_snp + 31) >> 5)) return;
     const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
     const int I = it.x, J = it.y;
     const bool diag = I == J;
@@ -2083,18 +2088,20 @@ hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* ge
                                 const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                                 const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr,
                                 int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc,
-                                const uint8_t* blk_rep, float* gram, int which, hipStream_t st) {
+                                const uint8_t* blk_rep, float* gram, int which, hipStream_t st,
+                                const uint8_t* blk_miss) {
     if (n_items <= 0) return hipSuccess;
     if (n_it > F4_SEG_CHUNKS || P < 1 || 2 * P > n_it) return hipErrorInvalidValue;
     const dim3 grid_p((unsigned)n_items * (unsigned)P);
     if (!(which & 1)) goto kc;  // the partial tiles of every item come from the main launch
     if (dom) hipLaunchKernelGGL((band_f4_part_kernel<true>), grid_p, dim3(64), 0, st, geno, pitch_words, n_it, cst,
-                                items, pos, Lw, Rw, sflags, n_snp, P, gram);
+                                items, pos, Lw, Rw, sflags, n_snp, P, gram, blk_miss);
     else hipLaunchKernelGGL((band_f4_part_kernel<false>), grid_p, dim3(64), 0, st, geno, pitch_words, n_it, cst,
-                            items, pos, Lw, Rw, sflags, n_snp, P, gram);
+                            items, pos, Lw, Rw, sflags, n_snp, P, gram, blk_miss);
 #define NLDSC_EPI(DOM_, KC_)                                                                                        \
     hipLaunchKernelGGL((band_f4_epi_kernel<DOM_, KC_>), dim3(n_items), dim3(64), 0, st, cst, items, pos, Lw, Rw,    \
-                       sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, blk_rep, P, gram)
+                       sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, blk_rep, P, gram, \
+                       blk_miss)
     if (dom) NLDSC_EPI(true, false); else NLDSC_EPI(false, false);
 kc:
     if (blk_rep && (which & 2)) { if (dom) NLDSC_EPI(true, true); else NLDSC_EPI(false, true); }

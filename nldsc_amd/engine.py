@@ -105,7 +105,9 @@ class Engine:
                  ksplit=self._L.nldsc_engine_ksplit(self._h),
                  band_kernel=BAND_KERNELS.get(self._L.nldsc_engine_band_kernel(self._h), "?"),
                  band_round_items=(self._L.nldsc_engine_band_round_items(self._h)
-                                   if hasattr(self._L, "nldsc_engine_band_round_items") else 0))
+                                   if hasattr(self._L, "nldsc_engine_band_round_items") else 0),
+                 band_tail_ksplit=(self._L.nldsc_engine_band_tail_ksplit(self._h)
+                                   if hasattr(self._L, "nldsc_engine_band_tail_ksplit") else 1))
         return d
 
 

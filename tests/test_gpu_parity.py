@@ -753,16 +753,26 @@ def test_2x2_workgroups_bitwise_single_block(engine, case, t2):
                                        maf=(0.0, 0.0)), label=f"2x2 {case} T2={t2}")
 
 
-@pytest.mark.parametrize("dom", [True, False])
-def test_band_round_launches_bitwise_one_launch(engine, dom):
+ROUND_CASES = {
+    # (N, M, length cM, dom, tail K-split required): ~9 400-9 700 items in 2 048-item rounds; the cost model K-splits
+    # the partial last round at both lengths (N = 131 101: 1 025 K chunks; N = 315 599: C3 rows)
+    "n131k_dom": (131_101, 12_000, 15.0, True, False),
+    "n131k_add": (131_101, 12_000, 15.0, False, False),
+    "n315k_dom_tail": (315_599, 12_000, 15.0, True, True),
+}
+
+
+@pytest.mark.parametrize("case", sorted(ROUND_CASES))
+def test_band_round_launches_bitwise_one_launch(engine, case):
     """The single-block fp4 band in launches of one round of the wave slots each (the default for long rows,
-    N >= 2^17, when the band has at least four rounds of items) gives bitwise the results of one launch of all items
-    ($NLDSC_BAND_ROUNDS=0): the per-SNP sums are order-independent fixed point, and every item runs exactly once.
-    N = 131 101 (1 025 K chunks), 12 000 SNPs at 800 per cM, 1 % missing: ~9 700 single-block items."""
+    N >= 2^17, when the band has at least four rounds of items), with the partial last round K-split when the cost
+    model prefers it, gives bitwise the results of one launch of all items ($NLDSC_BAND_ROUNDS=0): the per-SNP sums
+    are order-independent fixed point, the K-split partial Gram tiles are exact integers, and every item runs once.
+    12 000 SNPs at 800 per cM, 1 % missing; a few SNPs against the exact truth."""
     from nldsc_amd import synth
     from nldsc_amd.engine import Engine
-    N, M = 131_101, 12_000
-    buf, pos = synth.device_bed(M, N, seed=31, length_cm=15.0, missing=0.01)
+    N, M, length, dom, tail = ROUND_CASES[case]
+    buf, pos = synth.device_bed(M, N, seed=31, length_cm=length, missing=0.01)
     flags = MODES["f4"] | _lib_flag("FLAG_EXACT_RARE") | (0 if dom else _lib_flag("FLAG_ADDITIVE_ONLY"))
     args = (1.0, 1e-4, 1e-5, 1.0 / M, pos)
 
@@ -774,13 +784,13 @@ def test_band_round_launches_bitwise_one_launch(engine, dom):
             assert (t["band_round_items"] > 0) == rounds, t
             if rounds:
                 assert t["band_items"] >= 4 * t["band_round_items"], t
+                assert t["band_tail_ksplit"] > 1 or not tail, t
             return r
     got = fresh(True)
     ref = _env_run("NLDSC_BAND_ROUNDS", "0", lambda: fresh(False))
     for k in got:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
     assert (got["l2_ws"] > 100).all() and np.isfinite(got["l2"]).all()
-    # a few SNPs against the exact truth (block edges, the chromosome ends)
     targets = np.array([0, 31, 32, 4095, 4096, 6000, M - 33, M - 1], np.int32)
     bed = buf.cpu().numpy().tobytes()
     rows = np.frombuffer(bed, np.uint8, offset=3).reshape(M, -1)
@@ -790,4 +800,4 @@ def test_band_round_launches_bitwise_one_launch(engine, dom):
         exp = dict(exp, l2d=np.full(len(targets), np.nan), l2d_ws=np.full(len(targets), -1, np.int32),
                    l2d_wse=np.full(len(targets), -1, np.int32))
     assert_ld_close(sub, exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
-                                       maf=(0.0, 0.0)), label=f"rounds dom={dom}")
+                                       maf=(0.0, 0.0)), label=f"rounds {case}")
