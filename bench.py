@@ -366,7 +366,8 @@ def main():
                                                  "Gram entries per pair (vv, vm, mv, mm additive; vh, mh, hv, hm "
                                                  "dominance), skipped products of missing-free blocks included")
         traffic, traffic_src = pmc_traffic(
-            ("band_f4_t2_kernel", "band_f4_kernel") if tims[-1].get("band_kernel") == "f4_routed" else kname.split("<")[0],
+            ("band_f4_t2_kernel", "band_f4_kernel", "band_f4_part_kernel", "band_f4_epi_kernel")  # (+ the K-split tail)
+            if tims[-1].get("band_kernel") == "f4_routed" else kname.split("<")[0],
             N, M, args.missing)
         roof.update(traffic=traffic, traffic_source=traffic_src,
                     algorithmic_bytes_per_launch=eng.n_snp * 4 * ((((N + 3) // 4) + 31) // 32 * 8),
