@@ -222,6 +222,13 @@ def main():
                     help="c4: chromosomes computed at once per GPU (host threads, one engine stream each)")
     args = ap.parse_args()
 
+    # --gpus N without a launcher: start the N ranks here (torch.distributed.run in a child process, before
+    # anything touches the GPU) and exit with their status; under a launcher, WORLD_SIZE must equal --gpus
+    if not args.rehearse:
+        from nldsc_amd.launch import ranks_or_spawn
+        rc = ranks_or_spawn(os.path.abspath(__file__), sys.argv[1:], args.gpus, args.backend)
+        if rc is not None:
+            sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -269,7 +276,7 @@ def main():
     if split:
         # --split: ONE chromosome position-sharded over the ranks (strong scaling): rank g keeps only its
         # owned SNP range plus one window of halo rows resident and computes the owned SNPs
-        from nldsc_amd.distributed import gather_ranges, gather_spans, halo_range, shard_ranges
+        from nldsc_amd.distributed import RESULT_KEYS, gather_spans, gather_table, halo_range, shard_ranges, table_width
         lo, hi = shard_ranges(pos, args.window_cm, s_world)[s_rank]
         a, b = halo_range(pos, args.window_cm, (lo, hi))
         nb = (N + 3) // 4
@@ -277,9 +284,12 @@ def main():
         eng.load_bed_device(sl.data_ptr(), sl.numel(), b - a, N)
         del sl
         own, own_rel, pos = (lo, hi), (lo - a, hi - a), pos[a:b]
-        full_local = {k: np.empty(M, np.float64 if k in ("l2", "l2d", "maf", "residuals_std") else np.int32)
-                      for k in ("l2", "l2d", "maf", "residuals_std", "l2_ws", "l2d_ws", "l2d_wse")}
-        spans = gather_spans(own, device=coll) if world > 1 else None  # the sharding is fixed across steps
+        # the owned slice of the score table stays in HBM ([7, width] fp64 block, nldsc_engine_run_device); the
+        # blocks are gathered device to device (RCCL) and only rank 0 copies the gathered table to the host
+        spans = gather_spans(own, device=coll) if world > 1 else [own]  # the sharding is fixed across steps
+        table = torch.empty((len(RESULT_KEYS), table_width(spans)), dtype=torch.float64, device=f"cuda:{local}")
+        gbuf = torch.empty(world * table.numel(), dtype=torch.float64,
+                           device=table.device if coll == "cuda" else "cpu") if world > 1 else None
     else:
         eng.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
     bed_host = None
@@ -296,13 +306,14 @@ def main():
     def step():
         nonlocal out
         if split:  # owned slice of the one chromosome, then the table assembled on rank 0 (RCCL over xGMI)
-            out = eng.run(w, args.maf, args.std_thr, rsq, pos, own=own_rel, flags=flags, out=out)
+            eng.run_device(w, args.maf, args.std_thr, rsq, pos, table, own=own_rel, flags=flags)
             tim = eng.timings()
-            for k, v in full_local.items():
-                v[own[0]:own[1]] = out[k][own_rel[0]:own_rel[1]]
             tg = time.perf_counter()
             if world > 1:
-                gather_ranges(full_local, own, M, device=coll, spans=spans)
+                full = gather_table(table if coll == "cuda" else table.cpu(), spans, M, out=gbuf)
+                out = full if full is not None else out
+            else:  # rehearsal of one rank: its slice to the host
+                out = {"l2_ws": table[4].cpu().numpy()}
             tim["gather_ms"] = 1e3 * (time.perf_counter() - tg)
             return tim
         out = eng.run(w, args.maf, args.std_thr, rsq, pos, flags=flags, out=out)

@@ -109,6 +109,15 @@ int nldsc_engine_load_bed_device(nldsc_engine* e, const void* bed, size_t len, i
 int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32_t own_end,
                      nldsc_ld_result* r, char* err, size_t errlen);
 
+/* nldsc_engine_run with the owned slice of the result left in device memory (the multi-GPU gather of
+ * SURVEY.md §8 e1 then runs device to device over RCCL, without a host round trip): `table_dev`, device memory
+ * of the engine's device holding 7 * width doubles with width >= own_end - own_begin, receives row k =
+ * l2, l2d, maf, residuals_std, l2_ws, l2d_ws, l2d_wse (LDScoreResult, data.h:21-31; window sizes as doubles),
+ * column c = SNP own_begin + c, columns past the owned range NaN.  Returns once the table is written (the
+ * engine stream is synchronised), so any stream may read it. */
+int nldsc_engine_run_device(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32_t own_end,
+                            double* table_dev, int32_t width, char* err, size_t errlen);
+
 /* Per-stage device timings (milliseconds, HIP events on the engine stream) of the last run:
  * [0] genotype count, [1] per-SNP statistics, [2] window replay + schedule (host time; overlaps [0]),
  * [3] band correlation kernel (all launches), [4] finalize, [5] total.
@@ -154,10 +163,9 @@ int nldsc_engine_load_bed_file_range(nldsc_engine* e, const char* path, int32_t 
  * replays the reference's sliding-window pointers (stream.h:131-155,182-197) from positions and
  * MAF-pass flags (flags[j] bit 0) into L/R (n_snp each; L = -1 for SNPs the reference does not
  * compute) and lists the work items (I, J0, nc, 0) covering every needed 32x32 block pair for the
- * owned range (max_nc 1 or 2).  max_nc = 4 lists the skewed 2x2 tiles of the exact path instead:
- * (I, J, mask, 0), bit w of mask scheduling block pair (I, J), (I, J+1), (I+1, J+1), (I+1, J+2)
- * for w = 0..3.  Returns the item count; when it exceeds `cap` (or items == NULL) nothing is written
- * to `items` and the count is returned; < 0 on bad arguments. */
+ * owned range (max_nc 1 or 2; any other value is an argument error).  Returns the item count; when it
+ * exceeds `cap` (or items == NULL) nothing is written to `items` and the count is returned; < 0 on bad
+ * arguments. */
 int nldsc_plan_band(const double* positions, const uint8_t* flags, int32_t n_snp, double ld_wind, int32_t own_begin,
                     int32_t own_end, int32_t max_nc, int32_t* L, int32_t* R, int32_t* items, int32_t cap);
 

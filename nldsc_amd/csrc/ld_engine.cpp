@@ -149,6 +149,9 @@ struct nldsc_engine {
     HostPinned h_meta;   // GPU plan counters (items, diagonal items)
     HostPinned h_pos;    // pinned copy of the positions (the upload does not stall this thread)
     HostPinned h_res;    // pinned landing buffer of the result copies (DMA, then host copies out)
+    // [0..1] device-table runs: sums of the positive WSA / WSD over the owned slice; [2] MFMA products issued
+    DevBuf<unsigned long long> sums;
+    HostPinned h_sums;
     DevBuf<int> Ew, plan_counts, plan_meta, plan_counts2;
     DevBuf<int2> plan_rows, plan_rows2;
     DevBuf<int4> items2;  // super-items of the 2 x 2 kernel
@@ -170,7 +173,7 @@ struct nldsc_engine {
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         if (ev_plan) (void)hipEventDestroy(ev_plan);
         Ew.release(); plan_counts.release(); plan_meta.release(); plan_rows.release();
-        plan_counts2.release(); plan_rows2.release(); items2.release(); blk_miss.release();
+        plan_counts2.release(); plan_rows2.release(); items2.release(); blk_miss.release(); sums.release();
         if (stream) (void)hipStreamDestroy(stream);
         if (plan_stream) (void)hipStreamDestroy(plan_stream);
         if (ev_pos) (void)hipEventDestroy(ev_pos);
@@ -416,24 +419,45 @@ int nldsc_engine_load_bed_file(nldsc_engine* e, const char* path, int32_t n_snp,
     return nldsc_engine_load_bed_file_range(e, path, n_snp, n_org, 0, n_snp, err, errlen);
 }
 
-int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32_t own_end,
-                     nldsc_ld_result* r, char* err, size_t errlen) {
-    if (!e || !p || !r) return set_err(err, errlen, NLDSC_E_ARG, "NULL argument");
+}  // extern "C"
+
+namespace {
+
+// The hot path of one run.  Results go to the host arrays of `r`, or (table_dev != nullptr) stay in device memory
+// as the owned slice of the score table (nldsc_engine_run_device).
+int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32_t own_end, nldsc_ld_result* r,
+             double* table_dev, int32_t width, char* err, size_t errlen) {
+    if (!e || !p || (!r && !table_dev)) return set_err(err, errlen, NLDSC_E_ARG, "NULL argument");
     if (!e->bed.p) return set_err(err, errlen, NLDSC_E_ARG, "no BED image loaded");
     if (p->n_snp != e->n_snp || p->n_org != e->n_org)
         return set_err(err, errlen, NLDSC_E_ARG, "params (%d SNPs x %d) do not match the loaded BED (%d x %d)",
                        p->n_snp, p->n_org, e->n_snp, e->n_org);
     if (!p->positions) return set_err(err, errlen, NLDSC_E_ARG, "positions is NULL");
-    if (!r->l2 || !r->l2d || !r->maf || !r->residuals_std || !r->l2_ws || !r->l2d_ws || !r->l2d_wse)
+    if (!table_dev && (!r->l2 || !r->l2d || !r->maf || !r->residuals_std || !r->l2_ws || !r->l2d_ws || !r->l2d_wse))
         return set_err(err, errlen, NLDSC_E_ARG, "a result array is NULL");
     const int M = p->n_snp, N = p->n_org;
     if (own_begin < 0 || own_end > M || own_begin > own_end)
         return set_err(err, errlen, NLDSC_E_ARG, "owned range [%d, %d) outside [0, %d)", own_begin, own_end, M);
+    if (table_dev && (width <= 0 || width < own_end - own_begin))
+        return set_err(err, errlen, NLDSC_E_ARG, "table width %d below the owned range's %d SNPs", width,
+                       own_end - own_begin);
     if (own_begin == own_end) {  // nothing owned: no kernel runs and no output is written (an empty GPU plan
-        // would leave the left pointers unfilled)
+        // would leave the left pointers unfilled); a device table is all NaN
         for (int k = 0; k < 6; ++k) e->ms[k] = 0.0;
         e->pairs = e->flop_alg = e->ops_alg_i8 = e->flop_issued = 0.0;
         e->n_band_items = 0;
+        e->last_ksplit = 1;
+        e->last_tail_ksplit = 1;
+        e->last_round_items = 0;
+        e->last_band_kernel = NLDSC_BAND_F4;
+        if (table_dev) {
+            HIPCHK(hipSetDevice(e->device));
+            HIPCHK(e->sums.ensure(3));
+            HIPCHK(hipMemsetAsync(e->sums.p, 0, 3 * sizeof(unsigned long long), e->stream));
+            HIPCHK(nldsc::launch_pack_table(e->l2.p, e->l2d.p, e->maf.p, e->rstd.p, e->ws3.p, M, own_begin, own_end,
+                                            width, table_dev, e->sums.p, e->stream));
+            HIPCHK(hipStreamSynchronize(e->stream));
+        }
         return NLDSC_OK;
     }
     const bool dom = !(p->flags & NLDSC_FLAG_ADDITIVE_ONLY);
@@ -556,6 +580,12 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     // the main stream; the replay itself (a few long sequential sums) runs on the plan stream beside the band
     // launch for the items without a replayed SNP, and only the KC launch and finalize wait for it.
     const bool replay = N < (1 << 23) && !(p->flags & NLDSC_FLAG_EXACT_RARE);
+    // Invariant of the overlap: the replay rewrites, for replayed SNPs only, sflags bit 1 (residual pass; a byte
+    // read-modify-write), cst and lut.  What runs beside it on the main stream reads sflags bits 0 (MAF pass:
+    // left_pointer_kernel, the host flag copy) and 2 (missing calls: block_missing_kernel, the band kernels' rm /
+    // cm), which the replay never changes, and never reads a replayed SNP's cst / lut before ev_replay: the items
+    // of blocks holding one are skipped (skip_item) until the KC launch, and the K-split part kernel, which runs
+    // them, stores Gram tiles without reading constants.  No other kernel writes sflags after snp_stats_kernel.
     if (replay) {
         HIPCHK(nldsc::launch_replay_flags(e->counts.p, e->oriented ? e->flip.p : nullptr, e->sflags.p, M,
                                           e->blk_rep.p, st));
@@ -571,13 +601,12 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
 
     // ---- window replay + schedule ----
     auto t_host0 = std::chrono::steady_clock::now();
-    int n_items = 0, n_diag = 0;
+    int n_items = 0;
     if (gpu_plan) {
         HIPCHK(hipEventSynchronize(e->ev_plan));  // the count kernel is running meanwhile
         HIPCHK(hipStreamWaitEvent(st, e->ev_plan, 0));  // emit / left pointers / band read the schedule
         const int* meta = reinterpret_cast<const int*>(e->h_meta.p);
         n_items = meta[1];
-        n_diag = meta[2];
         ksplit = choose_ksplit(n_items);
         use_t2 = t2_cand && ksplit == 1 && n_items > 0;
         if (use_t2) {
@@ -585,10 +614,6 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
             HIPCHK(e->items2.ensure(std::max<size_t>((size_t)n_items2, 1)));
             HIPCHK(nldsc::launch_plan_emit_super(M, e->plan_rows2.p, e->plan_meta.p + 4, e->plan_counts2.p,
                                                  e->items2.p, st));
-        }
-        if (use_t2 && routed) {
-            HIPCHK(e->blk_miss.ensure((size_t)nblk));
-            HIPCHK(nldsc::launch_block_missing(e->sflags.p, M, e->blk_miss.p, st));
         }
         if (!use_t2 || routed) {
             HIPCHK(e->items.ensure(std::max<size_t>((size_t)n_items, 1)));
@@ -645,8 +670,11 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     HIPCHK(hipMemcpyAsync(e->Rw.p, e->h_stage.p + bL, bL, hipMemcpyHostToDevice, st));
     if (bI) HIPCHK(hipMemcpyAsync(e->items.p, e->h_stage.p + 2 * bL, bI, hipMemcpyHostToDevice, st));
     n_items = (int)e->h_items.size();
-    for (const nldsc::PlanItem& it : e->h_items) n_diag += it.x == it.y;
     ksplit = choose_ksplit(n_items);
+    }
+    if (use_f4) {  // per 32-SNP block: holds a missing call (the kernels' m-product predicate; routing, issued count)
+        HIPCHK(e->blk_miss.ensure((size_t)nblk));
+        HIPCHK(nldsc::launch_block_missing(e->sflags.p, M, e->blk_miss.p, st));
     }
     HIPCHK(hipMemsetAsync(e->l2_acc.p, 0, sizeof(double) * M, st));
     HIPCHK(hipMemsetAsync(e->l2d_acc.p, 0, sizeof(double) * M, st));
@@ -655,20 +683,6 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
 
     HIPCHK(hipEventRecord(e->ev[3], st));
     e->n_band_items = n_items;
-    {
-        // 32x32 block products issued per sample slot: exact paths xx, xo, ox, oo (+ xh, oh, and hx, ho
-        // off the diagonal) per block pair; fp32 AA (+ AR, and RA off the diagonal)
-        double blocks = 0;
-        if (gpu_plan) blocks = n_items;
-        else for (const nldsc::PlanItem& it : e->h_items) blocks += it.z;
-        // (the single-block fp4 kernel also skips m.x on diagonal blocks: the transpose of x.m; the 2 x 2
-        // workgroups issue every product)
-        const double products = use_t2 && !routed ? blocks * (dom ? 8.0 : 4.0)
-                              : use_i8 ? blocks * (dom ? 8.0 : 4.0) - (dom ? 2.0 * n_diag : 0.0)
-                                         - (use_f4 ? 1.0 * n_diag : 0.0)
-                                       : blocks * (dom ? 3.0 : 1.0) - (dom ? 1.0 * n_diag : 0.0);
-        e->flop_issued = products * 2.0 * BLK * BLK * (double)row_bytes * 4.0;
-    }
     e->last_ksplit = ksplit;
     e->last_band_kernel = use_t2 ? (routed ? NLDSC_BAND_F4_ROUTED : NLDSC_BAND_F4_2X2) : !use_f4 ? (use_i8 ? NLDSC_BAND_I8 : NLDSC_BAND_F32)
                         : ksplit > 1 ? NLDSC_BAND_F4_KSPLIT : n_it > nldsc::F4_SEG_CHUNKS ? NLDSC_BAND_F4_SEG
@@ -744,25 +758,54 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     HIPCHK(nldsc::launch_finalize(e->Lw.p, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, own_begin, own_end, dom,
                                   e->l2.p, e->l2d.p, e->ws3.p, st));
     HIPCHK(hipEventRecord(e->ev[5], st));
-    // the owned slices land in pinned memory by DMA (pageable copies are staged by the runtime, slower),
-    // then go to the caller's arrays
+    // matrix-core products the band kernels issued, counted on the GPU per work item as each kernel decides them
+    // (missing-free blocks skip the m products, diagonal blocks the transposed ones, routed items run in the 2 x 2
+    // kernel): sums[2]; sums[0..1] are the device-table run's pair counts
+    HIPCHK(e->sums.ensure(3));
+    HIPCHK(e->h_sums.ensure(3 * sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(e->sums.p, 0, 3 * sizeof(unsigned long long), st));
+    HIPCHK(nldsc::launch_issued_products(e->items.p, use_t2 && !routed ? 0 : n_items, use_t2 ? e->items2.p : nullptr,
+                                         n_items2, gpu_plan ? e->plan_rows.p : nullptr,
+                                         use_f4 ? e->blk_miss.p : nullptr, nblk, path, dom, use_t2 && routed,
+                                         e->sums.p + 2, st));
     const int n_own = own_end - own_begin;
-    const size_t o = own_begin, b8 = sizeof(double) * (size_t)std::max(n_own, 0), b4 = sizeof(int) * (size_t)std::max(n_own, 0);
-    double* const dsrc[4] = {e->l2.p + o, e->l2d.p + o, e->maf.p + o, e->rstd.p + o};
-    double* const ddst[4] = {r->l2 + o, r->l2d + o, r->maf + o, r->residuals_std + o};
-    int* const isrc[3] = {e->ws3.p + o, e->ws3.p + M + o, e->ws3.p + 2 * (size_t)M + o};
-    int32_t* const idst[3] = {r->l2_ws + o, r->l2d_ws + o, r->l2d_wse + o};
-    if (n_own > 0) {
-        HIPCHK(e->h_res.ensure(4 * b8 + 3 * b4));
-        for (int k = 0; k < 4; ++k)
-            HIPCHK(hipMemcpyAsync(e->h_res.p + k * b8, dsrc[k], b8, hipMemcpyDeviceToHost, st));
-        for (int k = 0; k < 3; ++k)
-            HIPCHK(hipMemcpyAsync(e->h_res.p + 4 * b8 + k * b4, isrc[k], b4, hipMemcpyDeviceToHost, st));
-    }
-    HIPCHK(hipStreamSynchronize(st));
-    if (n_own > 0) {
-        for (int k = 0; k < 4; ++k) std::memcpy(ddst[k], e->h_res.p + k * b8, b8);
-        for (int k = 0; k < 3; ++k) std::memcpy(idst[k], e->h_res.p + 4 * b8 + k * b4, b4);
+    double sw = 0, sd = 0;
+    if (table_dev) {
+        // the owned slice stays on the device (the caller gathers it device to device); only the pair counts of
+        // the metric come back
+        HIPCHK(nldsc::launch_pack_table(e->l2.p, e->l2d.p, e->maf.p, e->rstd.p, e->ws3.p, M, own_begin, own_end, width,
+                                        table_dev, e->sums.p, st));
+        HIPCHK(hipMemcpyAsync(e->h_sums.p, e->sums.p, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        const unsigned long long* s = reinterpret_cast<const unsigned long long*>(e->h_sums.p);
+        sw = (double)s[0];
+        sd = dom ? (double)s[1] : 0.0;
+    } else {
+        // the owned slices land in pinned memory by DMA (pageable copies are staged by the runtime, slower),
+        // then go to the caller's arrays
+        const size_t o = own_begin, b8 = sizeof(double) * (size_t)std::max(n_own, 0),
+                     b4 = sizeof(int) * (size_t)std::max(n_own, 0);
+        double* const dsrc[4] = {e->l2.p + o, e->l2d.p + o, e->maf.p + o, e->rstd.p + o};
+        double* const ddst[4] = {r->l2 + o, r->l2d + o, r->maf + o, r->residuals_std + o};
+        int* const isrc[3] = {e->ws3.p + o, e->ws3.p + M + o, e->ws3.p + 2 * (size_t)M + o};
+        int32_t* const idst[3] = {r->l2_ws + o, r->l2d_ws + o, r->l2d_wse + o};
+        HIPCHK(hipMemcpyAsync(e->h_sums.p, e->sums.p, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        if (n_own > 0) {
+            HIPCHK(e->h_res.ensure(4 * b8 + 3 * b4));
+            for (int k = 0; k < 4; ++k)
+                HIPCHK(hipMemcpyAsync(e->h_res.p + k * b8, dsrc[k], b8, hipMemcpyDeviceToHost, st));
+            for (int k = 0; k < 3; ++k)
+                HIPCHK(hipMemcpyAsync(e->h_res.p + 4 * b8 + k * b4, isrc[k], b4, hipMemcpyDeviceToHost, st));
+        }
+        HIPCHK(hipStreamSynchronize(st));
+        if (n_own > 0) {
+            for (int k = 0; k < 4; ++k) std::memcpy(ddst[k], e->h_res.p + k * b8, b8);
+            for (int k = 0; k < 3; ++k) std::memcpy(idst[k], e->h_res.p + 4 * b8 + k * b4, b4);
+        }
+        for (int j = own_begin; j < own_end; ++j) {
+            if (r->l2_ws[j] > 0) sw += r->l2_ws[j];
+            if (dom && r->l2d_ws[j] > 0) sd += r->l2d_ws[j];
+        }
     }
     auto t_end = std::chrono::steady_clock::now();
 
@@ -773,11 +816,8 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     HIPCHK(hipEventElapsedTime(&f, e->ev[3], e->ev[4])); e->ms[3] = f;
     HIPCHK(hipEventElapsedTime(&f, e->ev[4], e->ev[5])); e->ms[4] = f;
     e->ms[5] = std::chrono::duration<double, std::milli>(t_end - t_start).count();
-    double sw = 0, sd = 0;
-    for (int j = own_begin; j < own_end; ++j) {
-        if (r->l2_ws[j] > 0) sw += r->l2_ws[j];
-        if (dom && r->l2d_ws[j] > 0) sd += r->l2d_ws[j];
-    }
+    e->flop_issued = (double)reinterpret_cast<const unsigned long long*>(e->h_sums.p)[2] * 2.0 * BLK * BLK *
+                     (double)row_bytes * 4.0;
     e->pairs = sw;
     // BASELINE.md metric: FLOP_alg = 2N(1/2 sum WSA + sum WSD); additive-only 2N * 1/2 sum WSA
     e->flop_alg = 2.0 * (double)N * (0.5 * sw + sd);
@@ -785,6 +825,22 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
     // 2 per ordered dominance pair (xh, oh): 2N (4 * 1/2 sum WSA + 2 sum WSD) int8 ops
     e->ops_alg_i8 = 2.0 * (double)N * (2.0 * sw + 2.0 * sd);
     return NLDSC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32_t own_end,
+                     nldsc_ld_result* r, char* err, size_t errlen) {
+    if (!r) return set_err(err, errlen, NLDSC_E_ARG, "NULL argument");
+    return run_impl(e, p, own_begin, own_end, r, nullptr, 0, err, errlen);
+}
+
+int nldsc_engine_run_device(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32_t own_end,
+                            double* table_dev, int32_t width, char* err, size_t errlen) {
+    if (!table_dev) return set_err(err, errlen, NLDSC_E_ARG, "NULL table");
+    return run_impl(e, p, own_begin, own_end, nullptr, table_dev, width, err, errlen);
 }
 
 int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, double* flop_issued,

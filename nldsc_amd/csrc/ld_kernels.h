@@ -14,10 +14,12 @@ namespace nldsc {
 // X, H, Ob: sums of x, h, o over the SNP's sample slots (the fp4 path's Gram uses the missing
 // indicator m = 1 - o over all slots, so o-products are recovered as X - x.m, Ob_i + Ob_j - K + m.m, ...);
 // SA, SR: sums of (x - mu o) / sa and (2h - beta x - c o) / s over the individuals (for the ka / kr terms).
+// isa, is: 1 / sa and 1 / s (0 where sa / s are 0), so the pair epilogue multiplies instead of dividing.
 struct SnpConst {
     double mu, sa, c, beta, s;
     double X, H, Ob;
     double ka, kr, SA, SR;
+    double isa, is;
 };
 
 // resident rows: after a load, save each row's last byte and fill the pitch padding (rows >= n_snp all 0x55)
@@ -101,6 +103,18 @@ hipError_t launch_band_f4_t2(bool dom, int n_items2, const uint32_t* geno, int p
 hipError_t launch_block_missing(const uint8_t* sflags, int n_snp, uint8_t* blk_miss, hipStream_t st);
 hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2d_acc, const int* ws_acc, int n_snp,
                            int own_lo, int own_hi, bool dom, double* l2, double* l2d, int* ws3, hipStream_t st);
+// the matrix-core products the band kernels issued (one per 32x32 block product over all K), counted per work item
+// as each kernel decides them: kind 2 fp4 single-block items (+ 2 x 2 super-items when items2 != nullptr; `routed`:
+// each item counted in the kernel the routing sends it to), 1 int8, 0 fp32 (items of it.z column blocks);
+// blk_miss may be nullptr for kinds 0 and 1.  out[0] += the count (zeroed before)
+hipError_t launch_issued_products(const int4* items, int n_items, const int4* items2, int n_items2, const int2* rows,
+                                 const uint8_t* blk_miss, int nblk, int kind, bool dom, bool routed,
+                                 unsigned long long* out, hipStream_t st);
+// the owned slice [own_lo, own_hi) of the finalized results as a [7][width] fp64 table in device memory (columns
+// past the slice NaN) + sums[0] += sum of positive WSA, sums[1] += sum of positive WSD over the slice (zeroed before)
+hipError_t launch_pack_table(const double* l2, const double* l2d, const double* maf, const double* rstd, const int* ws3,
+                             int n_snp, int own_lo, int own_hi, int width, double* table, unsigned long long* sums,
+                             hipStream_t st);
 hipError_t launch_synth_bed(uint8_t* rows, int n_snp, int n_org, int nb, const float* thr, float rho, float missing,
                             uint64_t seed, hipStream_t st);
 

@@ -263,6 +263,8 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const uint8_t* 
     K.X = sX; K.H = sH; K.Ob = sOb;
     K.SA = K.sa != 0.0 ? (sX - K.mu * sOb) / K.sa : 0.0;  // ~0: exactly centred
     K.SR = K.s != 0.0 ? (2.0 * sH - K.beta * sX - K.c * sOb) / K.s : 0.0;
+    K.isa = K.sa != 0.0 ? 1.0 / K.sa : 0.0;  // (NaN for an all-missing SNP: its windows stay poisoned)
+    K.is = K.s != 0.0 ? 1.0 / K.s : 0.0;
     cst[j] = K;
     sflags[j] = fl;
 }
@@ -522,13 +524,14 @@ __global__ void __launch_bounds__(64) reference_residual_kernel(const uint8_t* _
     const double u = drop == 0 ? a[2] - a[1] : drop == 1 ? 0.5 * (a[2] - a[0]) : a[1] - a[0];  // 1 / sa
     const double w = drop == 0 ? u - a[1] : -a[0];                                               // mu / sa
     K.sa = 1.0 / u;
+    K.isa = u;
     K.mu = w / u;
     K.ka = ka;
     K.SA = (K.X - K.mu * K.Ob) / K.sa;
     for (int c = 0; c < 4; ++c) L[c].x = CA(c) / sd_a;
     if (!((double)sd > std_thr)) {  // SNPFilter::residuals_std: excluded (also NaN: a constant additive coding)
         sflags[j] &= (uint8_t)~2u;
-        K.c = K.beta = K.s = K.kr = K.SR = 0.0;
+        K.c = K.beta = K.s = K.kr = K.SR = K.is = 0.0;
         for (int c = 0; c < 4; ++c) L[c].y = 0.f;
         cst[j] = K;
         return;
@@ -540,6 +543,7 @@ __global__ void __launch_bounds__(64) reference_residual_kernel(const uint8_t* _
     const double kr = (double)(C(1) / sd);
     for (int q = 0; q < 3; ++q) r[q] = (double)(C(sc[q]) / sd) - kr;
     K.s = 2.0 / (2.0 * r[1] - r[0] - r[2]);
+    K.is = 0.5 * (2.0 * r[1] - r[0] - r[2]);
     K.beta = -(r[2] - r[1]) * K.s;
     K.c = -r[0] * K.s;
     K.kr = kr;
@@ -729,14 +733,91 @@ __device__ __forceinline__ double r2_adjusted(double dot, double n) {
     return 1. - (1. - r2) * (n - 1) / (n - 2);
 }
 
+// The same with the per-run constants 1 / n and (n - 1) / (n - 2) hoisted (no fp64 division per pair).
+struct R2Adj {
+    double inv_n, q;
+    __device__ __forceinline__ explicit R2Adj(double n) : inv_n(1. / n), q((n - 1) / (n - 2)) {}
+    __device__ __forceinline__ double operator()(double dot) const {
+        const double corr = dot * inv_n;
+        return 1. - (1. - corr * corr) * q;
+    }
+};
+
+// ---- per-SNP sums of a block pair by wavefront reductions (ldscalc.h:34-47's reduction over neighbours) ----
+// A 32x32 Gram tile is spread over the wave as MFMA accumulators: lane (i, h) holds column SNP i against the 16
+// row SNPs rb + (r & 3) + 8 (r >> 2) + 4 h, r = 0..15.  Column sums are the lane's own 16 values plus its partner
+// lane's (i, 1 - h); row sums are reduced across the 32 lanes of a half in registers (cross-lane DPP / swizzle
+// moves, fixed order: bit-reproducible), with no LDS atomics and no barrier.
+struct SlotSum {
+    double l2, l2d;
+    int cnt;  // WSA | WSD << 8 | WSDE << 16 (each <= 64 per block pair)
+};
+__device__ __forceinline__ SlotSum operator+(const SlotSum& a, const SlotSum& b) {
+    return SlotSum{a.l2 + b.l2, a.l2d + b.l2d, a.cnt + b.cnt};
+}
+
+// v from lane (lane ^ M): M = 1, 2 quad permutes and 8 a row rotation (DPP, no LDS), 4 and 16 ds_swizzle
+// (bit mode, within 32 lanes), 32 the other half of the wave (ds_bpermute)
+template <int M>
+__device__ __forceinline__ int xlane(int v) {
+    if constexpr (M == 1) return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    else if constexpr (M == 2) return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    else if constexpr (M == 8) return __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    else if constexpr (M == 4 || M == 16) return __builtin_amdgcn_ds_swizzle(v, 0x1F | (M << 10));
+    else return __shfl_xor(v, M, 64);
+}
+template <int M>
+__device__ __forceinline__ double xlane(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = xlane<M>((int)(b & 0xFFFFFFFFll)), hi = xlane<M>((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int M>
+__device__ __forceinline__ SlotSum xlane(const SlotSum& v) {
+    return SlotSum{xlane<M>(v.l2), xlane<M>(v.l2d), xlane<M>(v.cnt)};
+}
+
+// Transposed reduction of 4 row values per lane (rows k = 0..3 of a row group) over the 32 lanes of a half: two
+// halving exchanges (each lane sends the rows it gives up and keeps the others), then a butterfly over lane octets.
+// Afterwards the 8 lanes i with i >> 3 == k hold row k's total.  5 cross-lane moves per quantity for 4 rows.
+__device__ __forceinline__ SlotSum reduce_rows4(const SlotSum (&v)[4], int i) {
+    const bool b16 = (i & 16) != 0, b8 = (i & 8) != 0;
+    SlotSum k0 = b16 ? v[2] : v[0], k1 = b16 ? v[3] : v[1];
+    const SlotSum s0 = b16 ? v[0] : v[2], s1 = b16 ? v[1] : v[3];
+    k0 = k0 + xlane<16>(s0);
+    k1 = k1 + xlane<16>(s1);
+    SlotSum k = b8 ? k1 : k0;
+    k = k + xlane<8>(b8 ? k0 : k1);
+    k = k + xlane<4>(k);
+    k = k + xlane<2>(k);
+    k = k + xlane<1>(k);
+    return k;
+}
+
+// One slot's sums of one work item -> the per-SNP totals (2^-44 fixed point, order-independent across items).
+__device__ __forceinline__ void flush_slot(const SnpSlot& si, const SlotSum& v, int own_lo, int own_hi, int n_snp,
+                                           double* l2_acc, double* l2d_acc, int* ws_acc) {
+    const int g = si.g;
+    if (v.cnt == 0 || g < own_lo || g >= own_hi || g >= n_snp) return;
+    const int wsa = v.cnt & 0xFF, wsd = (v.cnt >> 8) & 0xFF, wse = v.cnt >> 16;
+    int* nanf = &ws_acc[3 * (size_t)n_snp + g];
+    if (wsa) {
+        acc_fixed(&l2_acc[g], nanf, 1, v.l2);
+        atomicAdd(&ws_acc[g], wsa);
+    }
+    if (wsd) {
+        acc_fixed(&l2d_acc[g], nanf, 2, v.l2d);
+        atomicAdd(&ws_acc[(size_t)n_snp + g], wsd);
+        if (wse) atomicAdd(&ws_acc[2 * (size_t)n_snp + g], wse);
+    }
+}
+
 constexpr int NC_MAX = 2;
 constexpr int NS_MAX = 32 * (1 + NC_MAX);
 
 struct BandLds {
     float2 tab[4 * NS_MAX];  // [code][slot], slot stride NS = 32 * (1 + NC) of the body
     SnpSlot info[NS_MAX];
-    double l2[NS_MAX], l2d[NS_MAX];
-    int wsa[NS_MAX], wsd[NS_MAX], wse[NS_MAX];
 };
 
 // DIAG0: column block 0 is the row block itself (J0 == I).  Its R_I^T X_I product is the
@@ -752,11 +833,6 @@ __device__ __forceinline__ void band_body(BandLds& sh, const int4 it, const uint
     constexpr int NS = 32 * (1 + NC);  // SNP slots: 32 rows, then NC x 32 columns
     float2 (*tab)[NS] = reinterpret_cast<float2 (*)[NS]>(sh.tab);
     SnpSlot* info = sh.info;
-    double* s_l2 = sh.l2;
-    double* s_l2d = sh.l2d;
-    int* s_wsa = sh.wsa;
-    int* s_wsd = sh.wsd;
-    int* s_wse = sh.wse;
 
     const int lane = threadIdx.x;
     const int i = lane & 31, h = lane >> 5;
@@ -778,8 +854,6 @@ __device__ __forceinline__ void band_body(BandLds& sh, const int4 it, const uint
             si.pos = 0.0; si.L = -1; si.R = -2; si.fl = 0;
         }
         info[s] = si;
-        s_l2[s] = 0.0; s_l2d[s] = 0.0;
-        s_wsa[s] = 0; s_wsd[s] = 0; s_wse[s] = 0;
     }
     __syncthreads();
 
@@ -854,59 +928,69 @@ __device__ __forceinline__ void band_body(BandLds& sh, const int4 it, const uint
     }
 
     // ---- fused epilogue: r2adj, window / MAF / residual masks, per-SNP sums ------------------
+    // (the row SNPs' sums over both column blocks, then reduced across the wave as in pair_epilogue)
     const double n_pad = 16.0 * (double)pitch_words - n_org;
+    const R2Adj r2adj(n_org);
+    SlotSum col[NC], mine = {0.0, 0.0, 0};
+    int my_row = -1;
 #pragma unroll
-    for (int b = 0; b < NC; ++b) {
-        const int sj = 32 + 32 * b + i;
-        const SnpSlot cj = info[sj];
-        const bool diag = (J0 + b) == I;
-        const bool pj = cj.fl & 1, rpj = (cj.fl & 2) != 0;
-        const bool compj = cj.L >= 0;
+    for (int b = 0; b < NC; ++b) col[b] = SlotSum{0.0, 0.0, 0};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int si = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const SnpSlot ci = info[si];
-            const bool pi = ci.fl & 1, rpi = (ci.fl & 2) != 0;
-            const bool inwin = fabs(cj.pos - ci.pos) <= ld_wind && ci.g != cj.g;
-            // j in N(i): SNP i's window scan (stream.h:142-155) covers j
-            const bool nij = inwin && ci.L >= 0 && cj.g >= ci.L && cj.g <= ci.R && pj;
-            // i in N(j): only for off-diagonal blocks (a diagonal block holds both orders)
-            const bool nji = !diag && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
-            if (nij || nji) {
-                // the n_pad non-individual slots hold code 01 (missing): remove their products (non-zero only
-                // for the replayed rare variants, whose missing calls are not centred at 0)
-                const float2 mi = tab[1][si], mj = tab[1][sj];
-                const double r2 = r2_adjusted((double)haa[b][r] - n_pad * mi.x * mj.x, n_org);
-                if (nij) { atomicAdd(&s_l2[si], r2); atomicAdd(&s_wsa[si], 1); }
-                if (nji) { atomicAdd(&s_l2[sj], r2); atomicAdd(&s_wsa[sj], 1); }
-                if (DOM) {
-                    if (nij && rpj) {  // a_i . r_j -> L2D_i (ldscalc.h:40-46)
-                        const double rd = r2_adjusted((double)har[b][r] - n_pad * mi.x * mj.y, n_org);
-                        atomicAdd(&s_l2d[si], rd); atomicAdd(&s_wsd[si], 1);
-                        if (rd > rsq_thr) atomicAdd(&s_wse[si], 1);
-                    }
-                    if (nji && rpi) {  // r_i . a_j -> L2D_j
-                        const double rd = r2_adjusted((double)hra[b][r] - n_pad * mi.y * mj.x, n_org);
-                        atomicAdd(&s_l2d[sj], rd); atomicAdd(&s_wsd[sj], 1);
-                        if (rd > rsq_thr) atomicAdd(&s_wse[sj], 1);
+    for (int q = 0; q < 4; ++q) {
+        SlotSum rowv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rowv[k] = SlotSum{0.0, 0.0, 0};
+#pragma unroll
+        for (int b = 0; b < NC; ++b) {
+            const int sj = 32 + 32 * b + i;
+            const SnpSlot cj = info[sj];
+            const bool diag = (J0 + b) == I;
+            const bool pj = cj.fl & 1, rpj = (cj.fl & 2) != 0;
+            const bool compj = cj.L >= 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int r = 4 * q + k;
+                const int si = k + 8 * q + 4 * h;
+                const SnpSlot ci = info[si];
+                const bool pi = ci.fl & 1, rpi = (ci.fl & 2) != 0;
+                const bool inwin = fabs(cj.pos - ci.pos) <= ld_wind && ci.g != cj.g;
+                // j in N(i): SNP i's window scan (stream.h:142-155) covers j
+                const bool nij = inwin && ci.L >= 0 && cj.g >= ci.L && cj.g <= ci.R && pj;
+                // i in N(j): only for off-diagonal blocks (a diagonal block holds both orders)
+                const bool nji = !diag && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
+                if (nij || nji) {
+                    // the n_pad non-individual slots hold code 01 (missing): remove their products (non-zero only
+                    // for the replayed rare variants, whose missing calls are not centred at 0)
+                    const float2 mi = tab[1][si], mj = tab[1][sj];
+                    const double r2 = r2adj((double)haa[b][r] - n_pad * mi.x * mj.x);
+                    if (nij) { rowv[k].l2 += r2; rowv[k].cnt += 1; }
+                    if (nji) { col[b].l2 += r2; col[b].cnt += 1; }
+                    if (DOM) {
+                        if (nij && rpj) {  // a_i . r_j -> L2D_i (ldscalc.h:40-46)
+                            const double rd = r2adj((double)har[b][r] - n_pad * mi.x * mj.y);
+                            rowv[k].l2d += rd;
+                            rowv[k].cnt += (1 << 8) + (rd > rsq_thr ? 1 << 16 : 0);
+                        }
+                        if (nji && rpi) {  // r_i . a_j -> L2D_j
+                            const double rd = r2adj((double)hra[b][r] - n_pad * mi.y * mj.x);
+                            col[b].l2d += rd;
+                            col[b].cnt += (1 << 8) + (rd > rsq_thr ? 1 << 16 : 0);
+                        }
                     }
                 }
             }
         }
+        const SlotSum t = reduce_rows4(rowv, i);
+        if ((i & 7) == q) {
+            mine = t;
+            my_row = (i >> 3) + 8 * q + 4 * h;
+        }
     }
-    __syncthreads();
-    for (int s = lane; s < NS; s += 64) {
-        const int g = info[s].g;
-        if (g < own_lo || g >= own_hi || g >= n_snp) continue;
-        if (s_wsa[s]) {
-            acc_fixed(&l2_acc[g], &ws_acc[3 * (size_t)n_snp + g], 1, s_l2[s]);
-            atomicAdd(&ws_acc[g], s_wsa[s]);
-        }
-        if (DOM && s_wsd[s]) {
-            acc_fixed(&l2d_acc[g], &ws_acc[3 * (size_t)n_snp + g], 2, s_l2d[s]);
-            atomicAdd(&ws_acc[(size_t)n_snp + g], s_wsd[s]);
-            if (s_wse[s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + g], s_wse[s]);
-        }
+    if (my_row >= 0) flush_slot(info[my_row], mine, own_lo, own_hi, n_snp, l2_acc, l2d_acc, ws_acc);
+#pragma unroll
+    for (int b = 0; b < NC; ++b) {
+        const SlotSum c = col[b] + xlane<32>(col[b]);
+        if (h == 0) flush_slot(info[32 + 32 * b + i], c, own_lo, own_hi, n_snp, l2_acc, l2d_acc, ws_acc);
     }
 }
 
@@ -967,75 +1051,97 @@ __device__ __forceinline__ int xcd_slot(int b, int n) {
     return x * per + min(x, rem) + (b >> 3);
 }
 
-// Epilogue of one 32x32 block pair (row slots rb.., column slots cb.. of the LDS slot tables):
-// standardised dots from the 8 integer Gram entries in fp64, r2adj, window/pointer masks, and
-// per-SNP sums (ldscalc.h:33-55).  diag: the pair is a diagonal block (row block == column block).
+// Epilogue of one 32x32 block pair (row slots rb.., column slots cb.. of the slot tables `info` / `cst`):
+// standardised dots from the 8 integer Gram entries in fp64, r2adj, window/pointer masks, and the pair's
+// per-SNP sums (ldscalc.h:33-55), reduced across the wave in registers (reduce_rows4) and added to the per-SNP
+// totals (flush_slot).  diag: the pair is a diagonal block (row block == column block).  Called by every lane.
 // MB: the Gram is in the missing basis {x, h, m} (fp4 path): gxo holds x.m, gox m.x, goo m.m, goh m.h,
 // gho h.m, and `kslots` is the number of individual slots (n_org; the other slots are all-zero in every
 // plane); o = 1 - m over the individual slots.
 template <bool DOM, class Acc, bool MB = false, bool KC = false>
-__device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpConst* cst, double* s_l2, double* s_l2d,
-                                              int* s_wsa, int* s_wsd, int* s_wse, int rb, int cb, bool diag, int i,
-                                              int h, const Acc& gxx, const Acc& gxo, const Acc& gox, const Acc& goo,
-                                              const Acc& gxh, const Acc& goh, const Acc& ghx, const Acc& gho,
-                                              double ld_wind, double n_org, double rsq_thr, double kslots = 0.0) {
+__device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpConst* cst, int rb, int cb, bool diag,
+                                              int i, int h, const Acc& gxx, const Acc& gxo, const Acc& gox,
+                                              const Acc& goo, const Acc& gxh, const Acc& goh, const Acc& ghx,
+                                              const Acc& gho, double ld_wind, double n_org, double rsq_thr,
+                                              double kslots, int own_lo, int own_hi, int n_snp,
+                                              double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
+                                              int* __restrict__ ws_acc) {
+    const R2Adj r2adj(n_org);
     const int sj = cb + i;
     const SnpSlot cj = info[sj];
     const SnpConst kj = cst[sj];
     const bool pj = cj.fl & 1, rpj = (cj.fl & 2) != 0;
     const bool compj = cj.L >= 0;
+    SlotSum col = {0.0, 0.0, 0}, mine = {0.0, 0.0, 0};
+    int my_row = -1;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int si = rb + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const SnpSlot ci = info[si];
-        const bool pi = ci.fl & 1, rpi = (ci.fl & 2) != 0;
-        const bool inwin = fabs(cj.pos - ci.pos) <= ld_wind && ci.g != cj.g;
-        const bool nij = inwin && ci.L >= 0 && cj.g >= ci.L && cj.g <= ci.R && pj;
-        const bool nji = !diag && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
-        if (nij || nji) {
-            const SnpConst ki = cst[si];
-            // MB: the fp4 Gram is over v = m + 2x (the raw 2-bit code placed as an e2m1 value), h and m:
-            // x.x = (v.v - v.m - m.v + m.m) / 4, x.m = (v.m - m.m) / 2, m.x = (m.v - m.m) / 2 (exact)
-            const double mm = (double)goo[r];
-            const double xx = MB ? 0.25 * ((double)gxx[r] - (double)gxo[r] - (double)gox[r] + mm) : (double)gxx[r];
-            const double xo = MB ? ki.X - 0.5 * ((double)gxo[r] - mm) : (double)gxo[r];
-            const double ox = MB ? kj.X - 0.5 * ((double)gox[r] - mm) : (double)gox[r];
-            const double oo = MB ? ki.Ob + kj.Ob - kslots + mm : mm;
-            // KC: the item holds a replayed rare variant (ka / kr terms; kept out of the common path, whose
-            // registers are all taken)
-            const double aa = (xx - kj.mu * xo - ki.mu * (ox - kj.mu * oo)) / (ki.sa * kj.sa) +
-                              (KC ? kj.ka * ki.SA + ki.ka * (kj.SA + kj.ka * n_org) : 0.0);
-            const double r2 = r2_adjusted(aa, n_org);
-            if (nij) { atomicAdd(&s_l2[si], r2); atomicAdd(&s_wsa[si], 1); }
-            if (nji) { atomicAdd(&s_l2[sj], r2); atomicAdd(&s_wsa[sj], 1); }
-            if (DOM) {
-                if (nij && rpj) {  // A_i . R_j -> L2D_i (ldscalc.h:40-46)
-                    const double xh = MB ? 0.5 * ((double)gxh[r] - (double)goh[r]) : (double)gxh[r];
-                    const double oh = MB ? kj.H - (double)goh[r] : (double)goh[r];
-                    const double ar = (2.0 * xh - kj.beta * xx - kj.c * xo -
-                                       ki.mu * (2.0 * oh - kj.beta * ox - kj.c * oo)) / (ki.sa * kj.s) +
-                                      (KC ? kj.kr * ki.SA + ki.ka * (kj.SR + kj.kr * n_org) : 0.0);
-                    const double rd = r2_adjusted(ar, n_org);
-                    atomicAdd(&s_l2d[si], rd); atomicAdd(&s_wsd[si], 1);
-                    if (rd > rsq_thr) atomicAdd(&s_wse[si], 1);
-                }
-                if (!diag && nji && rpi) {  // R_i . A_j -> L2D_j
-                    const double hx = MB ? 0.5 * ((double)ghx[r] - (double)gho[r]) : (double)ghx[r];
-                    const double ho = MB ? ki.H - (double)gho[r] : (double)gho[r];
-                    const double ra = (2.0 * hx - ki.beta * xx - ki.c * ox -
-                                       kj.mu * (2.0 * ho - ki.beta * xo - ki.c * oo)) / (ki.s * kj.sa) +
-                                      (KC ? ki.kr * kj.SA + kj.ka * (ki.SR + ki.kr * n_org) : 0.0);
-                    const double rd = r2_adjusted(ra, n_org);
-                    atomicAdd(&s_l2d[sj], rd); atomicAdd(&s_wsd[sj], 1);
-                    if (rd > rsq_thr) atomicAdd(&s_wse[sj], 1);
+    for (int q = 0; q < 4; ++q) {  // row group q: registers r = 4q + k, rows rb + k + 8q + 4h
+        SlotSum rowv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int r = 4 * q + k;
+            const int si = rb + k + 8 * q + 4 * h;
+            const SnpSlot ci = info[si];
+            const bool pi = ci.fl & 1, rpi = (ci.fl & 2) != 0;
+            const bool inwin = fabs(cj.pos - ci.pos) <= ld_wind && ci.g != cj.g;
+            // j in N(i): SNP i's window scan (stream.h:142-155) covers j; i in N(j) only off the diagonal
+            const bool nij = inwin && ci.L >= 0 && cj.g >= ci.L && cj.g <= ci.R && pj;
+            const bool nji = !diag && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
+            SlotSum rv = {0.0, 0.0, 0};
+            if (nij || nji) {
+                const SnpConst ki = cst[si];
+                // MB: the fp4 Gram is over v = m + 2x (the raw 2-bit code placed as an e2m1 value), h and m:
+                // x.x = (v.v - v.m - m.v + m.m) / 4, x.m = (v.m - m.m) / 2, m.x = (m.v - m.m) / 2 (exact)
+                const double mm = (double)goo[r];
+                const double xx = MB ? 0.25 * ((double)gxx[r] - (double)gxo[r] - (double)gox[r] + mm) : (double)gxx[r];
+                const double xo = MB ? ki.X - 0.5 * ((double)gxo[r] - mm) : (double)gxo[r];
+                const double ox = MB ? kj.X - 0.5 * ((double)gox[r] - mm) : (double)gox[r];
+                const double oo = MB ? ki.Ob + kj.Ob - kslots + mm : mm;
+                // KC: the item holds a replayed rare variant (ka / kr terms; kept out of the common path, whose
+                // registers are all taken)
+                const double aa = (xx - kj.mu * xo - ki.mu * (ox - kj.mu * oo)) * (ki.isa * kj.isa) +
+                                  (KC ? kj.ka * ki.SA + ki.ka * (kj.SA + kj.ka * n_org) : 0.0);
+                const double r2 = r2adj(aa);
+                if (nij) { rv.l2 = r2; rv.cnt = 1; }
+                if (nji) { col.l2 += r2; col.cnt += 1; }
+                if (DOM) {
+                    if (nij && rpj) {  // A_i . R_j -> L2D_i (ldscalc.h:40-46)
+                        const double xh = MB ? 0.5 * ((double)gxh[r] - (double)goh[r]) : (double)gxh[r];
+                        const double oh = MB ? kj.H - (double)goh[r] : (double)goh[r];
+                        const double ar = (2.0 * xh - kj.beta * xx - kj.c * xo -
+                                           ki.mu * (2.0 * oh - kj.beta * ox - kj.c * oo)) * (ki.isa * kj.is) +
+                                          (KC ? kj.kr * ki.SA + ki.ka * (kj.SR + kj.kr * n_org) : 0.0);
+                        const double rd = r2adj(ar);
+                        rv.l2d = rd;
+                        rv.cnt += (1 << 8) + (rd > rsq_thr ? 1 << 16 : 0);
+                    }
+                    if (!diag && nji && rpi) {  // R_i . A_j -> L2D_j
+                        const double hx = MB ? 0.5 * ((double)ghx[r] - (double)gho[r]) : (double)ghx[r];
+                        const double ho = MB ? ki.H - (double)gho[r] : (double)gho[r];
+                        const double ra = (2.0 * hx - ki.beta * xx - ki.c * ox -
+                                           kj.mu * (2.0 * ho - ki.beta * xo - ki.c * oo)) * (ki.is * kj.isa) +
+                                          (KC ? ki.kr * kj.SA + kj.ka * (ki.SR + ki.kr * n_org) : 0.0);
+                        const double rd = r2adj(ra);
+                        col.l2d += rd;
+                        col.cnt += (1 << 8) + (rd > rsq_thr ? 1 << 16 : 0);
+                    }
                 }
             }
+            rowv[k] = rv;
+        }
+        const SlotSum t = reduce_rows4(rowv, i);  // lanes i >> 3 == k: row rb + k + 8q + 4h
+        if ((i & 7) == q) {
+            mine = t;
+            my_row = rb + (i >> 3) + 8 * q + 4 * h;
         }
     }
+    col = col + xlane<32>(col);  // the partner lane (i, 1 - h) holds the other 16 rows of column i
+    if (my_row >= 0) flush_slot(info[my_row], mine, own_lo, own_hi, n_snp, l2_acc, l2d_acc, ws_acc);
+    if (h == 0) flush_slot(cj, col, own_lo, own_hi, n_snp, l2_acc, l2d_acc, ws_acc);
 }
 
 // Items holding a rare variant whose vectors are the reference's fp32 ones (ka / kr != 0: blk_rep[block] = 1,
-// set by reference_residual_kernel) need the epilogue's ka / kr terms, which the common epilogue has no
+// set by replay_flags_kernel) need the epilogue's ka / kr terms, which the common epilogue has no
 // registers left for: they run in a second launch of the kernel instantiated with KC = true, and the KC = false
 // launch skips them.  blk_rep == nullptr: no replayed SNP (KC = false only).
 template <bool KC>
@@ -1048,8 +1154,6 @@ __device__ __forceinline__ bool skip_item(const uint8_t* blk_rep, int4 it) {
 struct BandI8Lds {
     SnpSlot info[NS_MAX];
     SnpConst cst[NS_MAX];
-    double l2[NS_MAX], l2d[NS_MAX];
-    int wsa[NS_MAX], wsd[NS_MAX], wse[NS_MAX];
 };
 
 // NC column blocks J0 .. J0+NC-1 share the row decode; DIAG0: block 0 is the diagonal (J0 == I).
@@ -1076,8 +1180,6 @@ __device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const
         }
         sh.info[s] = si;
         sh.cst[s] = cst[g];
-        sh.l2[s] = 0.0; sh.l2d[s] = 0.0;
-        sh.wsa[s] = 0; sh.wsd[s] = 0; sh.wse[s] = 0;
     }
     __syncthreads();
 
@@ -1149,23 +1251,9 @@ __device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const
     // ---- fused epilogue (fp64): standardised dots from the integer Gram, r2adj, masks, sums ----
 #pragma unroll
     for (int b = 0; b < NC; ++b)
-        pair_epilogue<DOM, i32x16, false, KC>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * b,
-                                              DIAG0 && b == 0, i, h, gxx[b], gxo[b], gox[b], goo[b], gxh[b], goh[b],
-                                              ghx[b], gho[b], ld_wind, n_org, rsq_thr);
-    __syncthreads();
-    for (int s = lane; s < NS; s += 64) {
-        const int g = sh.info[s].g;
-        if (g < own_lo || g >= own_hi || g >= n_snp) continue;
-        if (sh.wsa[s]) {
-            acc_fixed(&l2_acc[g], &ws_acc[3 * (size_t)n_snp + g], 1, sh.l2[s]);
-            atomicAdd(&ws_acc[g], sh.wsa[s]);
-        }
-        if (DOM && sh.wsd[s]) {
-            acc_fixed(&l2d_acc[g], &ws_acc[3 * (size_t)n_snp + g], 2, sh.l2d[s]);
-            atomicAdd(&ws_acc[(size_t)n_snp + g], sh.wsd[s]);
-            if (sh.wse[s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + g], sh.wse[s]);
-        }
-    }
+        pair_epilogue<DOM, i32x16, false, KC>(sh.info, sh.cst, 0, 32 + 32 * b, DIAG0 && b == 0, i, h, gxx[b], gxo[b],
+                                              gox[b], goo[b], gxh[b], goh[b], ghx[b], gho[b], ld_wind, n_org, rsq_thr,
+                                              0.0, own_lo, own_hi, n_snp, l2_acc, l2d_acc, ws_acc);
 }
 
 // One block pair per item (the engine plans single column blocks for the exact paths), 2 waves / SIMD.
@@ -1295,8 +1383,6 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         }
         sh.info[s] = si;
         sh.cst[s] = cst[g];
-        sh.l2[s] = 0.0; sh.l2d[s] = 0.0;
-        sh.wsa[s] = 0; sh.wsd[s] = 0; sh.wse[s] = 0;
     }
     __syncthreads();
 
@@ -1415,9 +1501,9 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         }
 #pragma unroll
         for (int c = 0; c < NC; ++c)
-            pair_epilogue<DOM, f32x16v, true, KC>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32 + 32 * c,
-                                                  DIAG0 && c == 0, i, h, gxx[c], gxo[c], gox[c], goo[c], gxh[c],
-                                                  goh[c], ghx[c], gho[c], ld_wind, n_org, rsq_thr, n_org);
+            pair_epilogue<DOM, f32x16v, true, KC>(sh.info, sh.cst, 0, 32 + 32 * c, DIAG0 && c == 0, i, h, gxx[c], gxo[c],
+                                                  gox[c], goo[c], gxh[c], goh[c], ghx[c], gho[c], ld_wind, n_org,
+                                                  rsq_thr, n_org, own_lo, own_hi, n_snp, l2_acc, l2d_acc, ws_acc);
     } else {
         static_assert(NC == 1, "segmented K loop: one column block");
         i32x16 ixx = {}, ixo = {}, iox = {}, ioo = {}, ixh = {}, ioh = {}, ihx = {}, iho = {};
@@ -1471,22 +1557,9 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
 #pragma unroll
             for (int r = 0; r < 16; ++r) iox[r] = tri[i * 33 + (r & 3) + 8 * (r >> 2) + 4 * h];
         }
-        pair_epilogue<DOM, i32x16, true, KC>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32, DIAG0, i,
-                                             h, ixx, ixo, iox, ioo, ixh, ioh, ihx, iho, ld_wind, n_org, rsq_thr, n_org);
-    }
-    __syncthreads();
-    for (int s = lane; s < NS; s += 64) {
-        const int g = sh.info[s].g;
-        if (g < own_lo || g >= own_hi || g >= n_snp) continue;
-        if (sh.wsa[s]) {
-            acc_fixed(&l2_acc[g], &ws_acc[3 * (size_t)n_snp + g], 1, sh.l2[s]);
-            atomicAdd(&ws_acc[g], sh.wsa[s]);
-        }
-        if (DOM && sh.wsd[s]) {
-            acc_fixed(&l2d_acc[g], &ws_acc[3 * (size_t)n_snp + g], 2, sh.l2d[s]);
-            atomicAdd(&ws_acc[(size_t)n_snp + g], sh.wsd[s]);
-            if (sh.wse[s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + g], sh.wse[s]);
-        }
+        pair_epilogue<DOM, i32x16, true, KC>(sh.info, sh.cst, 0, 32, DIAG0, i, h, ixx, ixo, iox, ioo, ixh, ioh, ihx,
+                                             iho, ld_wind, n_org, rsq_thr, n_org, own_lo, own_hi, n_snp, l2_acc,
+                                             l2d_acc, ws_acc);
     }
 }
 
@@ -1538,10 +1611,8 @@ struct T2Lds {
     uint4 stage[S][4][2][64];  // [buffer][strip][chunk of the stage][lane (i + 32 h)]
     SnpSlot info[T2_SLOTS];
     SnpConst cst[T2_SLOTS];
-    // per-SNP sums per wave: each block pair's partial sums are formed exactly as the single-block kernel forms
-    // them (one wave, the same epilogue), so the fixed-point totals are bitwise that kernel's
-    double l2[4][T2_SLOTS], l2d[4][T2_SLOTS];
-    int wsa[4][T2_SLOTS], wsd[4][T2_SLOTS], wse[4][T2_SLOTS];
+    // (each block pair's per-SNP sums are formed by its wave exactly as the single-block kernel forms them — the
+    // same epilogue — so the fixed-point totals are bitwise that kernel's)
 };
 
 template <int N>
@@ -1604,10 +1675,6 @@ __global__ void __launch_bounds__(256, 2) band_f4_t2_kernel(
         }
         sh.info[tid] = si;
         sh.cst[tid] = blk < nblk ? cst[g] : SnpConst{};
-    }
-    for (int s = lane; s < T2_SLOTS; s += 64) {
-        sh.l2[w][s] = 0.0; sh.l2d[w][s] = 0.0;
-        sh.wsa[w][s] = 0; sh.wsd[w][s] = 0; sh.wse[w][s] = 0;
     }
     const int rb = 2 * I2 + (w >> 1), cb = 2 * J2 + (w & 1);
     bool need = rb < nblk && cb < nblk;
@@ -1694,24 +1761,48 @@ __global__ void __launch_bounds__(256, 2) band_f4_t2_kernel(
     else kloop(std::false_type{}, std::false_type{}, std::true_type{});
     wait_vmcnt<0>();  // the tail's surplus loads
     if (!need) return;  // no barrier follows
-    pair_epilogue<DOM, f32x16v, true, KC>(sh.info, sh.cst, sh.l2[w], sh.l2d[w], sh.wsa[w], sh.wsd[w], sh.wse[w],
-                                          32 * sA, 64 + 32 * (w & 1), rb == cb, i, h, gxx, gxo, gox, goo, gxh, goh,
-                                          ghx, gho, ld_wind, n_org, rsq_thr, n_org);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    // this wave's 64 slots: its row block (lanes 0-31) and column block (lanes 32-63)
-    const int s = h ? 64 + 32 * (w & 1) + i : 32 * sA + i, g = sh.info[s].g;
-    if (g >= own_lo && g < own_hi && g < n_snp) {
-        if (sh.wsa[w][s]) {
-            acc_fixed(&l2_acc[g], &ws_acc[3 * (size_t)n_snp + g], 1, sh.l2[w][s]);
-            atomicAdd(&ws_acc[g], sh.wsa[w][s]);
+    pair_epilogue<DOM, f32x16v, true, KC>(sh.info, sh.cst, 32 * sA, 64 + 32 * (w & 1), rb == cb, i, h, gxx, gxo, gox,
+                                          goo, gxh, goh, ghx, gho, ld_wind, n_org, rsq_thr, n_org, own_lo, own_hi,
+                                          n_snp, l2_acc, l2d_acc, ws_acc);
+}
+
+// Matrix-core work the band kernels issued (32x32 block products over the whole K range), counted per work item
+// exactly as each kernel decides it: kind 2 fp4 single-block items (mfmas_v: 1 + cm + rm + rm cm + dom (2 + rm +
+// cm), the transposed products skipped on diagonal blocks; items the 2 x 2 kernel takes skipped when `routed`),
+// kind 1 int8 items (4 + dom (2 + 2 !diag)), kind 0 fp32 items of it.z column blocks (1 + dom (2 - diag) each);
+// and, when items2 != nullptr, every needed block pair of the 2 x 2 super-items (f4_step: no diagonal skip).
+// rm / cm = blk_miss of the row / column block.  out[0] += products.
+__global__ void issued_products_kernel(const int4* __restrict__ items, int n_items, const int4* __restrict__ items2,
+                                       int n_items2, const int2* __restrict__ rows, const uint8_t* __restrict__ blk_miss,
+                                       int nblk, int kind, int dom, int routed, unsigned long long* __restrict__ out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long n = 0;
+    if (t < n_items) {
+        const int4 it = items[t];
+        const bool diag = it.x == it.y;
+        if (kind == 2) {
+            if (!(routed && t2_routed(blk_miss, it.x >> 1, it.y >> 1, nblk))) {
+                const int rm = blk_miss[it.x] != 0, cm = blk_miss[it.y] != 0, nd = !diag;
+                n = 1 + cm + rm * nd + rm * cm + (dom ? 1 + nd + rm + cm * nd : 0);
+            }
+        } else if (kind == 1) {
+            n = 4 + (dom ? (diag ? 2 : 4) : 0);
+        } else {
+            for (int b = 0; b < it.z; ++b) n += 1 + (dom ? (it.y + b == it.x ? 1 : 2) : 0);
         }
-        if (DOM && sh.wsd[w][s]) {
-            acc_fixed(&l2d_acc[g], &ws_acc[3 * (size_t)n_snp + g], 2, sh.l2d[w][s]);
-            atomicAdd(&ws_acc[(size_t)n_snp + g], sh.wsd[w][s]);
-            if (sh.wse[w][s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + g], sh.wse[w][s]);
+    } else if (items2 != nullptr && t < n_items + n_items2) {
+        const int4 it = items2[t - n_items];
+        if (!(routed && !t2_routed(blk_miss, it.x, it.y, nblk))) {
+            for (int w = 0; w < 4; ++w) {
+                const int rb = 2 * it.x + (w >> 1), cb = 2 * it.y + (w & 1);
+                if (rb >= nblk || cb >= nblk || cb - rb < rows[rb].x || cb - rb > rows[rb].y) continue;
+                const int rm = blk_miss[rb] != 0, cm = blk_miss[cb] != 0;
+                n += 1 + cm + rm + rm * cm + (dom ? 2 + rm + cm : 0);
+            }
         }
     }
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o, 64);
+    if ((threadIdx.x & 63) == 0 && n) atomicAdd(out, n);
 }
 
 // blk_miss[b] = 1 if block b holds a SNP with a missing call (flag bit 2) — zeroed before
@@ -1801,8 +1892,6 @@ __global__ void __launch_bounds__(64, 2) band_f4_epi_kernel(const SnpConst* __re
         }
         sh.info[s] = si;
         sh.cst[s] = cst[g];
-        sh.l2[s] = 0.0; sh.l2d[s] = 0.0;
-        sh.wsa[s] = 0; sh.wsd[s] = 0; sh.wse[s] = 0;
     }
     f32x16v g8[8];
 #pragma unroll
@@ -1826,23 +1915,9 @@ __global__ void __launch_bounds__(64, 2) band_f4_epi_kernel(const SnpConst* __re
 #pragma unroll
         for (int r = 0; r < 16; ++r) g8[2][r] = tr[i * 33 + (r & 3) + 8 * (r >> 2) + 4 * h];
     }
-    pair_epilogue<DOM, f32x16v, true, KC>(sh.info, sh.cst, sh.l2, sh.l2d, sh.wsa, sh.wsd, sh.wse, 0, 32, diag, i, h,
-                                          g8[0], g8[1], g8[2], g8[3], g8[4], g8[5], g8[6], g8[7], ld_wind, n_org,
-                                          rsq_thr, n_org);
-    __syncthreads();
-    for (int s = lane; s < 64; s += 64) {
-        const int g = sh.info[s].g;
-        if (g < own_lo || g >= own_hi || g >= n_snp) continue;
-        if (sh.wsa[s]) {
-            acc_fixed(&l2_acc[g], &ws_acc[3 * (size_t)n_snp + g], 1, sh.l2[s]);
-            atomicAdd(&ws_acc[g], sh.wsa[s]);
-        }
-        if (DOM && sh.wsd[s]) {
-            acc_fixed(&l2d_acc[g], &ws_acc[3 * (size_t)n_snp + g], 2, sh.l2d[s]);
-            atomicAdd(&ws_acc[(size_t)n_snp + g], sh.wsd[s]);
-            if (sh.wse[s]) atomicAdd(&ws_acc[2 * (size_t)n_snp + g], sh.wse[s]);
-        }
-    }
+    pair_epilogue<DOM, f32x16v, true, KC>(sh.info, sh.cst, 0, 32, diag, i, h, g8[0], g8[1], g8[2], g8[3], g8[4], g8[5],
+                                          g8[6], g8[7], ld_wind, n_org, rsq_thr, n_org, own_lo, own_hi, n_snp, l2_acc,
+                                          l2d_acc, ws_acc);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1867,6 +1942,42 @@ __global__ void finalize_kernel(const int* __restrict__ Lw, const double* __rest
     } else {  // not computed: initial values of ldscalc.h:16-21
         l2[g] = qnan; l2d[g] = qnan;
         ws3[g] = -1; ws3[(size_t)n_snp + g] = -1; ws3[2 * (size_t)n_snp + g] = -1;
+    }
+}
+
+// Owned slice of the score table for the multi-GPU gather (nldsc_engine_run_device): row k of `table` = l2, l2d,
+// maf, rstd, WSA, WSD, WSDE (doubles), column c = SNP own_lo + c, NaN past the slice; and the metric's pair counts
+// (positive window sizes) summed per wave, one 64-bit atomic per wave.
+__global__ void __launch_bounds__(256) pack_table_kernel(const double* __restrict__ l2, const double* __restrict__ l2d,
+                                                         const double* __restrict__ maf,
+                                                         const double* __restrict__ rstd,
+                                                         const int* __restrict__ ws3, int n_snp, int own_lo,
+                                                         int own_hi, int width, double* __restrict__ table,
+                                                         unsigned long long* __restrict__ sums) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int g = own_lo + c;
+    unsigned long long sa = 0, sd = 0;
+    if (c < width) {
+        const double qnan = __builtin_nan("");
+        const bool in = g < own_hi;
+        const int a = in ? ws3[g] : -1, d = in ? ws3[(size_t)n_snp + g] : -1, x = in ? ws3[2 * (size_t)n_snp + g] : -1;
+        table[c] = in ? l2[g] : qnan;
+        table[(size_t)width + c] = in ? l2d[g] : qnan;
+        table[2 * (size_t)width + c] = in ? maf[g] : qnan;
+        table[3 * (size_t)width + c] = in ? rstd[g] : qnan;
+        table[4 * (size_t)width + c] = in ? (double)a : qnan;
+        table[5 * (size_t)width + c] = in ? (double)d : qnan;
+        table[6 * (size_t)width + c] = in ? (double)x : qnan;
+        sa = a > 0 ? (unsigned long long)a : 0ull;
+        sd = d > 0 ? (unsigned long long)d : 0ull;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        sa += __shfl_down(sa, o, 64);
+        sd += __shfl_down(sd, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && (sa | sd)) {
+        atomicAdd(&sums[0], sa);
+        atomicAdd(&sums[1], sd);
     }
 }
 
@@ -2144,6 +2255,25 @@ hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, st, Lw, l2_acc, l2d_acc, ws_acc, n_snp,
                        own_lo, own_hi, dom ? 1 : 0, l2, l2d, ws3);
+    return hipGetLastError();
+}
+
+hipError_t launch_issued_products(const int4* items, int n_items, const int4* items2, int n_items2, const int2* rows,
+                                 const uint8_t* blk_miss, int nblk, int kind, bool dom, bool routed,
+                                 unsigned long long* out, hipStream_t st) {
+    const int n = n_items + (items2 != nullptr ? n_items2 : 0);
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(issued_products_kernel, dim3((n + 255) / 256), dim3(256), 0, st, items, n_items, items2,
+                       n_items2, rows, blk_miss, nblk, kind, dom ? 1 : 0, routed ? 1 : 0, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_table(const double* l2, const double* l2d, const double* maf, const double* rstd, const int* ws3,
+                             int n_snp, int own_lo, int own_hi, int width, double* table, unsigned long long* sums,
+                             hipStream_t st) {
+    if (width <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pack_table_kernel, dim3((width + 255) / 256), dim3(256), 0, st, l2, l2d, maf, rstd, ws3, n_snp,
+                       own_lo, own_hi, width, table, sums);
     return hipGetLastError();
 }
 

@@ -91,34 +91,50 @@ def gather_spans(own: tuple[int, int], *, device=None) -> list[tuple[int, int]]:
     return [(int(a), int(b)) for a, b in spans.view(world, 2).cpu().tolist()]
 
 
-def gather_ranges(local: dict, own: tuple[int, int], n_snp: int, *, device=None,
-                  spans: list[tuple[int, int]] | None = None) -> dict | None:
-    """Gather every rank's owned slice of the result table; the full table on rank 0, None elsewhere.
-    One all_gather of a [world, 7, width] fp64 block (RCCL over xGMI with device tensors, gloo on CPU)."""
-    import torch
-    import torch.distributed as dist
-    world, rank = dist.get_world_size(), dist.get_rank()
-    spans = gather_spans(own, device=device) if spans is None else spans
-    lo, hi = own
-    n_own = hi - lo
-    width = max(max(b - a for a, b in spans), 1)
-    tab = np.full((len(RESULT_KEYS), width), np.nan)
-    for k, key in enumerate(RESULT_KEYS):
-        tab[k, :n_own] = np.asarray(local[key][lo:hi], dtype=np.float64)
-    t = torch.from_numpy(tab)
-    if device is not None:
-        t = t.to(device, non_blocking=False)
-    out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)  # flat: gloo's shape rule
-    dist.all_gather_into_tensor(out, t.reshape(-1))
-    if rank != 0:
-        return None
-    arr = out.view((world,) + tuple(t.shape)).cpu().numpy()
+def table_width(spans: list[tuple[int, int]]) -> int:
+    """Columns of the per-rank score table block: the widest owned range."""
+    return max(max((b - a for a, b in spans), default=1), 1)
+
+
+def assemble(arr: np.ndarray, spans: list[tuple[int, int]], n_snp: int) -> dict:
+    """The full result table from the gathered [world, 7, width] block (rank g's columns = its owned SNPs)."""
     full = empty_result(n_snp)
     for g, (a, b) in enumerate(spans):
         for k, key in enumerate(RESULT_KEYS):
             v = arr[g, k, : b - a]
             full[key][a:b] = v if full[key].dtype.kind == "f" else v.astype(np.int32)
     return full
+
+
+def gather_table(table, spans: list[tuple[int, int]], n_snp: int, *, out=None) -> dict | None:
+    """One all_gather of every rank's [7, width] fp64 table block (torch tensor; with RCCL it stays in device
+    memory until rank 0 copies the gathered [world, 7, width] block to the host); the full result dict on rank 0,
+    None elsewhere.  `out`: a reusable flat buffer of world * 7 * width elements on the table's device."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if out is None:
+        out = torch.empty(world * table.numel(), dtype=table.dtype, device=table.device)  # flat: gloo's shape rule
+    dist.all_gather_into_tensor(out, table.reshape(-1))
+    if rank != 0:
+        return None
+    return assemble(out.view((world,) + tuple(table.shape)).cpu().numpy(), spans, n_snp)
+
+
+def gather_ranges(local: dict, own: tuple[int, int], n_snp: int, *, device=None,
+                  spans: list[tuple[int, int]] | None = None) -> dict | None:
+    """Gather every rank's owned slice of host result arrays; the full table on rank 0, None elsewhere.
+    One all_gather of a [world, 7, width] fp64 block (RCCL over xGMI with device tensors, gloo on CPU)."""
+    import torch
+    spans = gather_spans(own, device=device) if spans is None else spans
+    lo, hi = own
+    tab = np.full((len(RESULT_KEYS), table_width(spans)), np.nan)
+    for k, key in enumerate(RESULT_KEYS):
+        tab[k, :hi - lo] = np.asarray(local[key][lo:hi], dtype=np.float64)
+    t = torch.from_numpy(tab)
+    if device is not None:
+        t = t.to(device, non_blocking=False)
+    return gather_table(t, spans, n_snp)
 
 
 def calculate_sharded(load_and_run: Callable[[tuple[int, int]], dict], positions: np.ndarray, ld_wind: float,
@@ -129,6 +145,29 @@ def calculate_sharded(load_and_run: Callable[[tuple[int, int]], dict], positions
     own = shard_ranges(positions, ld_wind, world)[rank]
     local = load_and_run(own)
     return gather_ranges(local, own, n_snp, device=device)
+
+
+def calculate_sharded_device(bed_path: str, n_snp: int, n_org: int, ld_wind: float, maf: float, std_thr: float,
+                             rsq_thr: float, positions: np.ndarray, *, flags: int = 0, device: int = 0) -> dict | None:
+    """The RCCL path of `calculate_sharded` + `engine_runner`: this rank's engine reads its halo_range of the .bed,
+    writes its owned slice of the score table straight into a device block (nldsc_engine_run_device), and the
+    blocks are gathered device to device; only rank 0's gathered table crosses to the host."""
+    import torch
+    import torch.distributed as dist
+    from .engine import Engine
+    world, rank = dist.get_world_size(), dist.get_rank()
+    pos = np.asarray(positions, dtype=np.float64)
+    own = shard_ranges(pos, ld_wind, world)[rank]
+    dev = torch.device(f"cuda:{device}")
+    spans = gather_spans(own, device=dev)
+    tab = torch.full((len(RESULT_KEYS), table_width(spans)), float("nan"), dtype=torch.float64, device=dev)
+    lo, hi = own
+    if hi > lo:
+        a, b = halo_range(pos, ld_wind, own)
+        with Engine(device) as e:
+            e.load_bed_file_range(bed_path, n_snp, n_org, a, b)
+            e.run_device(ld_wind, maf, std_thr, rsq_thr, pos[a:b], tab, own=(lo - a, hi - a), flags=flags)
+    return gather_table(tab, spans, n_snp)
 
 
 def engine_runner(bed_path: str, n_snp: int, n_org: int, ld_wind: float, maf: float, std_thr: float,

@@ -90,6 +90,22 @@ class Engine:
                                                ctypes.byref(res), err, len(err)), err)
         return arrs
 
+    def run_device(self, ld_wind, maf, std_thr, rsq_thr, positions, table, *, own=None, flags=0):
+        """As `run`, but the owned slice of the score table stays on the device: `table` is a float64 device
+        tensor of shape (7, width) on this engine's GPU (rows l2, l2d, maf, residuals_std, l2_ws, l2d_ws, l2d_wse;
+        column c = SNP own[0] + c; NaN past the slice), written when this returns (C ABI nldsc_engine_run_device)."""
+        n = self.n_snp
+        own = (0, n) if own is None else own
+        if table.dim() != 2 or table.shape[0] != 7 or not table.is_cuda or str(table.dtype) != "torch.float64" \
+                or not table.is_contiguous():
+            raise ValueError("table must be a contiguous float64 CUDA tensor of shape (7, width)")
+        p, _keep = _lib.make_params(n, self.n_org, ld_wind, maf, std_thr, rsq_thr, positions, flags=flags)
+        err = _lib.errbuf()
+        _lib.check(self._L.nldsc_engine_run_device(self._h, ctypes.byref(p), int(own[0]), int(own[1]),
+                                                      ctypes.c_void_p(table.data_ptr()), int(table.shape[1]), err,
+                                                      len(err)), err)
+        return table
+
     def timings(self) -> dict:
         ms = (ctypes.c_double * 6)()
         flop, issued, pairs = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
@@ -101,9 +117,11 @@ class Engine:
         d.update(flop_alg=flop.value, flop_issued=issued.value, pairs=pairs.value, band_items=nl.value)
         ex, ops = ctypes.c_int32(), ctypes.c_double()
         self._L.nldsc_engine_path(self._h, ctypes.byref(ex), ctypes.byref(ops))
+        L = self._L  # (an older build loaded for A/B timing may lack the newer entry points)
         d.update(exact_i8=ex.value > 0, path={0: "f32", 1: "i8", 2: "f4"}[ex.value], ops_alg_i8=ops.value,
-                 ksplit=self._L.nldsc_engine_ksplit(self._h),
-                 band_kernel=BAND_KERNELS.get(self._L.nldsc_engine_band_kernel(self._h), "?"),
+                 ksplit=L.nldsc_engine_ksplit(self._h) if hasattr(L, "nldsc_engine_ksplit") else 1,
+                 band_kernel=(BAND_KERNELS.get(L.nldsc_engine_band_kernel(self._h), "?")
+                              if hasattr(L, "nldsc_engine_band_kernel") else "?"),
                  band_round_items=(self._L.nldsc_engine_band_round_items(self._h)
                                    if hasattr(self._L, "nldsc_engine_band_round_items") else 0),
                  band_tail_ksplit=(self._L.nldsc_engine_band_tail_ksplit(self._h)

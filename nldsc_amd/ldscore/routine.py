@@ -142,15 +142,16 @@ def _process_group():
 
 
 def _calculate_sharded(dist, params):
-    import torch
-
     from .. import distributed as D
     dev = _local_device()
     pos = np.asarray(params.positions, dtype=np.float64)
-    run = D.engine_runner(params.bedfile, params.n_snp, params.n_org, params.ld_wind, params.maf, params.std_thr,
-                          params.rsq_thr, pos, flags=params.flags, device=dev)
-    full = D.calculate_sharded(run, pos, params.ld_wind, params.n_snp,
-                               device=torch.device(f"cuda:{dev}") if _backend() == "nccl" else None)
+    if _backend() == "nccl":  # the owned slices stay in device memory and are gathered over RCCL
+        full = D.calculate_sharded_device(params.bedfile, params.n_snp, params.n_org, params.ld_wind, params.maf,
+                                          params.std_thr, params.rsq_thr, pos, flags=params.flags, device=dev)
+    else:  # gloo: host result arrays, CPU collectives
+        run = D.engine_runner(params.bedfile, params.n_snp, params.n_org, params.ld_wind, params.maf,
+                              params.std_thr, params.rsq_thr, pos, flags=params.flags, device=dev)
+        full = D.calculate_sharded(run, pos, params.ld_wind, params.n_snp)
     return None if full is None else _Result(full)
 
 

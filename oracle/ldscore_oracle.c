@@ -21,9 +21,11 @@
  *
  * Third-party arithmetic restated (not vendored): Armadillo `arma::mean`
  * (fp32, two accumulators) and `arma::dot` -> BLAS `sdot` for n > 32
- * (modelled as 32 fp32 partial sums with fused multiply-add, the structure of
- * the x86-64 OpenBLAS sdot kernels); neither has a pinned version in the
- * reference (CMakeLists.txt:22-27).
+ * (modelled as OpenBLAS 0.3.28's SkylakeX kernel, dot_f below: 4 x 16 FMA
+ * accumulators folded, a 32-step, horizontal adds, the tail added in double —
+ * bit-identical to the sdot of the OpenBLAS scipy ships in this image,
+ * tests/test_oracle.py); neither has a pinned version in the reference
+ * (CMakeLists.txt:22-27).
  */
 #include <immintrin.h>
 #include <math.h>

@@ -591,6 +591,77 @@ def test_missing_free_blocks_skip_m_products(engine, N):
                                       maf=(0.0, 0.0)), label=f"missing-free blocks N={N}")
 
 
+@pytest.mark.parametrize("t2", ["0", "1"])
+@pytest.mark.parametrize("dom", [True, False])
+def test_issued_products_counted_per_item(engine, t2, dom):
+    """flop_issued (the bench's mfma_pipe_frac) counts what each kernel issues per work item: fp4 single-block items
+    1 + cm + rm + rm cm + dom (2 + rm + cm) 32x32 block products over all K, less the transposed ones of diagonal
+    blocks; items the routing sends to the 2 x 2 kernel (missing-free super-items) 1 + 2 dom; int8 4 + dom (2 + 2
+    !diag); fp32 1 + dom (2 - diag).  Blocks alternate between missing-free, one missing call and 2 % missing."""
+    from nldsc_amd import _lib, synth
+    from nldsc_amd.engine import Engine
+    N, M = 1003, 800
+    spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=8.0, seed=77, missing=0.02)
+    g = synth.genotypes(spec)
+    clean = synth.genotypes(synth.SynthSpec(n_org=N, n_snp=M, length_cm=8.0, seed=77, missing=0.0))
+    blk = np.arange(M) // 32
+    g[blk % 3 != 2] = clean[blk % 3 != 2]
+    g[(blk % 3 == 1) & (np.arange(M) % 32 == 5), N // 2] = -1
+    rows = synth.pack_bed_rows(g)
+    pos = synth.positions_cm(spec)
+    nblk = (M + 31) // 32
+    miss = np.array([(g[32 * b:32 * b + 32] < 0).any() for b in range(nblk)], int)
+    _, _, items = _lib.plan_band(pos, np.ones(M, np.uint8), 1.0, max_nc=1)
+    I, J = items[:, 0], items[:, 1]
+    rm, cm, nd = miss[I], miss[J], (I != J).astype(int)
+    f4 = 1 + cm + rm * nd + rm * cm + (1 + nd + rm + cm * nd if dom else 0)
+    if t2 == "1":  # super-items whose four (clamped) blocks are missing-free run in the 2 x 2 kernel
+        mb = lambda b: miss[np.minimum(b, nblk - 1)]  # noqa: E731
+        routed = ~(mb(I & ~1) | mb((I & ~1) + 1) | mb(J & ~1) | mb((J & ~1) + 1)).astype(bool)
+        assert routed.any() and not routed.all()
+        f4 = np.where(routed, 1 + (2 if dom else 0), f4)
+    expect = {"f4": int(f4.sum()), "i8": int((4 + (2 + 2 * nd if dom else 0)).sum()),
+              "f32": int((1 + (2 - (1 - nd) if dom else 0)).sum())}
+    row_bytes = -(-((N + 3) // 4) // 64) * 64
+    flags = _lib_flag("FLAG_EXACT_RARE") | (0 if dom else _lib_flag("FLAG_ADDITIVE_ONLY"))
+
+    def run():
+        out = {}
+        with Engine(0) as e:
+            e.load_bed_bytes(synth.bed_bytes(rows), M, N)
+            for mode in MODES:
+                e.run(1.0, 0.01, 1e-5, 1.0 / M, pos, flags=flags | MODES[mode])
+                out[mode] = e.timings()["flop_issued"] / (2.0 * 32 * 32 * 4 * row_bytes)
+        return out
+    got = _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", t2, run))
+    assert got == {k: float(v) for k, v in expect.items()}, (got, expect)
+
+
+def test_device_table_equals_host_run(engine):
+    """nldsc_engine_run_device (the multi-GPU gather's source) writes the owned slice of the score table into a
+    device [7, width] block — columns past the slice NaN — equal to the host run's arrays, with the same pair
+    count; an empty owned range gives an all-NaN block."""
+    import torch
+    from nldsc_amd.distributed import RESULT_KEYS
+    bed, pos, meta, _, _ = load_set("n1003")
+    M = meta["n_snp"]
+    engine.load_bed_bytes(bed, M, meta["n_org"])
+    args = (meta["ld_wind"], meta["maf"], meta["std_thr"], meta["rsq_thr"], pos)
+    for own in [(0, M), (17, 400), (M - 1, M), (400, 400)]:
+        host = engine.run(*args, own=own)
+        th = engine.timings()
+        n = own[1] - own[0]
+        tab = torch.full((7, n + 9), 123.0, dtype=torch.float64, device="cuda:0")
+        engine.run_device(*args, tab, own=own)
+        td = engine.timings()
+        arr = tab.cpu().numpy()
+        for k, key in enumerate(RESULT_KEYS):
+            np.testing.assert_array_equal(arr[k, :n], host[key][own[0]:own[1]].astype(np.float64),
+                                          err_msg=f"{own} {key}")
+        assert np.isnan(arr[:, n:]).all()
+        assert td["pairs"] == th["pairs"] and td["flop_issued"] == th["flop_issued"], (td, th)
+
+
 @pytest.mark.parametrize("mode", sorted(MODES))
 @pytest.mark.parametrize("n_org,strict", [(50_000, False), (50_001, True), (50_001, False), (315_599, False)])
 def test_rare_variants_reference_residual(engine, mode, n_org, strict):
@@ -801,3 +872,56 @@ def test_band_round_launches_bitwise_one_launch(engine, case):
                    l2d_wse=np.full(len(targets), -1, np.int32))
     assert_ld_close(sub, exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
                                        maf=(0.0, 0.0)), label=f"rounds {case}")
+
+
+def test_round_launches_with_replayed_rare_variants_in_the_tail(engine):
+    """The default CLI path in full: rare variants replayed in the reference's fp32 arithmetic (no
+    FLAG_EXACT_RARE), the band in round launches, and the partial last round K-split — where the KC epilogue of
+    the tail reads the partial Gram tiles the main launch wrote.  Rare SNPs (<= 16 calls in a genotype class) sit in
+    the last row blocks (whose items end the tile-ordered plan: the K-split tail) and mid-chromosome.  Bitwise equal
+    to one launch ($NLDSC_BAND_ROUNDS=0) and to the replay run in line on the main stream
+    ($NLDSC_REPLAY_OVERLAP=0); the replayed SNPs' residual std equals the oracle's bit for bit and their scores
+    pass the bar against it."""
+    import torch
+    from nldsc_amd import synth
+    from nldsc_amd.engine import Engine
+    N, M = 315_599, 12_000
+    buf, pos = synth.device_bed(M, N, seed=33, length_cm=15.0, missing=0.01)
+    nb = (N + 3) // 4
+    img = buf.cpu().numpy().copy()
+    del buf
+    rows = img[3:].reshape(M, nb)
+    rng = np.random.default_rng(7)
+    rare = np.array(sorted({M - 1, M - 5, M - 40, M - 70, M - 130, 6001, 6002, 300}), np.int64)
+    for j in rare:  # 100 het, 8 hom-A2 calls, 1 % missing: MAF 1.8e-4 passes 1e-4; 8 calls in a class: replayed
+        g = np.zeros(N, np.int8)
+        pick = rng.choice(N, 108, replace=False)
+        g[pick[:100]], g[pick[100:]] = 1, 2
+        g[rng.random(N) < 0.01] = -1
+        rows[j] = synth.pack_bed_rows(g[None])[0]
+    dev = torch.from_numpy(img).to("cuda:0")
+    flags = MODES["f4"]
+    args = (1.0, 1e-4, 1e-5, 1.0 / M, pos)
+
+    def fresh(rounds):
+        with Engine(0) as e:
+            e.load_bed_device(dev.data_ptr(), dev.numel(), M, N)
+            r = e.run(*args, flags=flags)
+            t = e.timings()
+            assert (t["band_round_items"] > 0) == rounds, t
+            if rounds:
+                assert t["band_tail_ksplit"] > 1, t
+            return r
+    got = fresh(True)
+    for var, value, rounds in (("NLDSC_BAND_ROUNDS", "0", False), ("NLDSC_REPLAY_OVERLAP", "0", True)):
+        ref = _env_run(var, value, lambda: fresh(rounds))
+        for k in got:
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{var}={value} {k}")
+    bed = img.tobytes()
+    t = np.array(sorted(set(rare.tolist()) | {M - 2, M - 33, 6000, 5990}), np.int32)
+    exp = O.run_c(bed, M, N, *args, targets=t, flags=O.NO_COPIES)
+    sub = {k: v[t] for k, v in got.items()}
+    is_rare = np.isin(t, rare)
+    assert np.isfinite(exp["residuals_std"][is_rare]).all()
+    np.testing.assert_array_equal(sub["residuals_std"][is_rare], exp["residuals_std"][is_rare])
+    assert_ld_close(sub, exp, label="rounds + replayed rare tail vs oracle")

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Same-box, same-process A/B of engine builds: every build runs the same resident synthetic chromosome, the builds
+interleaved run by run (so clock drift and box-to-box spread fall on all of them alike); band / total ms medians
+per build and workload as one JSON line.
+    python tools/ab_libs.py --libs new=nldsc_amd/libnldsc_amd.so old=ab_libs/r2base.so --workload c2 c3 --runs 8
+Workloads: c2 (N 50 000, additive only), c3 (N 315 599, add+dom, 1 % missing), c3m0 (c3 without missing calls),
+c5 (1000 kb windows, 288 bp per SNP, missing-free; --c5-snp SNPs)."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+WORKLOADS = {  # name: (N, M, length_cm, window, missing, additive_only)
+    "c2": (50_000, 80_000, 280.0, 1.0, 0.01, True),
+    "c3": (315_599, 80_000, 280.0, 1.0, 0.01, False),
+    "c3m0": (315_599, 80_000, 280.0, 1.0, 0.0, False),
+    "c5": (315_599, None, None, 1.0e6, 0.0, False),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", nargs="+", required=True, help="name=path.so")
+    ap.add_argument("--workload", nargs="+", default=["c3"], choices=sorted(WORKLOADS))
+    ap.add_argument("--runs", type=int, default=8)
+    ap.add_argument("--c5-snp", type=int, default=300_000)
+    a = ap.parse_args()
+    import torch
+    torch.cuda.init()
+    from nldsc_amd import _lib, synth
+    from nldsc_amd.engine import Engine
+    libs = dict(x.split("=", 1) for x in a.libs)
+    out = {}
+    for wl in a.workload:
+        N, M, L, w, miss, add = WORKLOADS[wl]
+        if wl == "c5":
+            M, L = a.c5_snp, 288.0 * a.c5_snp
+        buf, pos = synth.device_bed(M, N, seed=7, length_cm=L, missing=miss)
+        if wl == "c5":
+            pos = np.round(pos)
+        flags = _lib.FLAG_ADDITIVE_ONLY if add else 0
+        engines = {}
+        for name, path in libs.items():
+            e = Engine(0, lib_path=path)
+            e.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
+            engines[name] = e
+        del buf
+        torch.cuda.empty_cache()
+        res = {name: {"band": [], "total": []} for name in libs}
+        ref = None
+        for r in range(a.runs + 1):
+            for name, e in engines.items():
+                got = e.run(w, 1e-4, 1e-5, 1.0 / M, pos, flags=flags)
+                t = e.timings()
+                if r > 0:  # run 0 is the warmup
+                    res[name]["band"].append(t["band_ms"])
+                    res[name]["total"].append(t["total_ms"])
+                if ref is None:
+                    ref = got
+                else:  # every build must agree on the integer outputs
+                    for k in ("l2_ws", "l2d_ws"):
+                        assert np.array_equal(got[k], ref[k]), (wl, name, k)
+        out[wl] = {name: {"band_ms_median": float(np.median(v["band"])), "band_ms_min": float(np.min(v["band"])),
+                          "total_ms_median": float(np.median(v["total"])), "runs": len(v["band"])}
+                   for name, v in res.items()}
+        print(json.dumps({wl: out[wl]}), file=sys.stderr, flush=True)
+        for e in engines.values():
+            e.close()
+    print(json.dumps({"ab": out, "libs": libs, "runs": a.runs}))
+
+
+if __name__ == "__main__":
+    main()
