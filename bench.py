@@ -52,6 +52,10 @@ def band_kernel_name(variant: str, dom: bool, default: str) -> str:
         "f4_routed": f"band_f4_t2_kernel<{d}, 4, false> for missing-free 2x2 super-items (4-wave workgroups sharing "
                      f"their strips through LDS) + band_f4_kernel<{d}, 2, 0, false> for the rest (one wave per 32x32 "
                      "block pair); v_mfma_scale_f32_32x32x64_f8f6f4, e2m1 operands, exact integer Gram in fp32",
+        "f4_quad": f"band_f4_q_kernel<{d}, 4, false> for missing-free 4x4 super-items (4-wave workgroups, one 64x64 "
+                   f"SNP tile of 2x2 block pairs per wave, strips shared through an LDS ring) + band_f4_kernel<{d}, 2, 0, "
+                   "false> for the rest (one wave per 32x32 block pair); v_mfma_scale_f32_32x32x64_f8f6f4, e2m1 "
+                   "operands, exact integer Gram in fp32",
         "f4": f"band_f4_kernel<{d}, 2, 0, false> (one wave per 32x32 block pair; v_mfma_scale_f32_32x32x64_f8f6f4, "
               "e2m1 operands, exact integer Gram in fp32)",
         "f4_ksplit": f"band_f4_part_kernel<{d}> + band_f4_epi_kernel (K-split; v_mfma_scale_f32_32x32x64_f8f6f4)",
@@ -377,8 +381,9 @@ def main():
                                                  "Gram entries per pair (vv, vm, mv, mm additive; vh, mh, hv, hm "
                                                  "dominance), skipped products of missing-free blocks included")
         traffic, traffic_src = pmc_traffic(
-            ("band_f4_t2_kernel", "band_f4_kernel", "band_f4_part_kernel", "band_f4_epi_kernel")  # (+ the K-split tail)
-            if tims[-1].get("band_kernel") == "f4_routed" else kname.split("<")[0],
+            ("band_f4_t2_kernel", "band_f4_q_kernel", "band_f4_kernel", "band_f4_part_kernel",
+             "band_f4_epi_kernel")  # (the super-item kernel + the single-block rest + the K-split tail)
+            if tims[-1].get("band_kernel") in ("f4_routed", "f4_quad") else kname.split("<")[0],
             N, M, args.missing)
         roof.update(traffic=traffic, traffic_source=traffic_src,
                     algorithmic_bytes_per_launch=eng.n_snp * 4 * ((((N + 3) // 4) + 31) // 32 * 8),

@@ -150,6 +150,8 @@ int nldsc_engine_band_tail_ksplit(const nldsc_engine* e);
 #define NLDSC_BAND_F4_KSPLIT 4
 #define NLDSC_BAND_F4_2X2 5
 #define NLDSC_BAND_F4_ROUTED 6
+#define NLDSC_BAND_F4_QUAD 7 /* $NLDSC_T2=3: missing-free 4x4 super-items in the quad workgroups (64x64 tiles per
+                                wave), the rest in the single-block kernel */
 int nldsc_engine_band_kernel(const nldsc_engine* e);
 
 /* Load SNP rows [snp_begin, snp_end) of a .bed file of n_snp_file SNPs as the engine's image

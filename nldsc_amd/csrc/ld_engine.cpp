@@ -107,8 +107,12 @@ struct nldsc_engine {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t plan_stream = nullptr;  // the GPU schedule runs here, beside the count kernel
+    hipStream_t band_stream2 = nullptr;  // odd round launches when $NLDSC_BAND_STREAMS=2
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t ev_pos = nullptr;        // positions uploaded (the schedule's only input)
     hipEvent_t ev[6] = {};
+    hipEvent_t ev_dbg[2] = {};  // $NLDSC_DEBUG_TIMING: after the super-item launch, before the single-block launches
+    bool debug_timing = false;
     hipEvent_t ev_plan = nullptr;  // GPU plan counters landed in h_meta
     hipEvent_t ev_stats = nullptr;   // SNP constants and replay flags written (the replay's inputs)
     hipEvent_t ev_replay = nullptr;  // replayed constants written (the KC launch and finalize wait on it)
@@ -116,6 +120,7 @@ struct nldsc_engine {
     DevBuf<uint8_t> bed;
     DevBuf<uint8_t> lastb;  // each row's original last byte (the per-run count kernel masks a copy of it)
     DevBuf<uint8_t> flip;   // per SNP: resident row stores the swapped (00 <-> 11) coding
+    DevBuf<uint8_t> row_miss;  // per SNP: bit 0 / 1 = a missing call among the reference's / PLINK's individual slots
     bool orient = true;     // store rows minor-homozygote-as-00 at load (NLDSC_ORIENT=0: file coding)
     bool oriented = false;  // the resident image was oriented
     int32_t n_snp = 0, n_org = 0;
@@ -132,11 +137,16 @@ struct nldsc_engine {
     int last_ksplit = 1;
     int last_round_items = 0;
     int last_tail_ksplit = 1;
-    // fp4 band kernels on the GPU plan ($NLDSC_T2): 1 (default) missing-free super-items in the 2 x 2 block-pair
-    // workgroups, the rest in the single-block kernel; 2 everything in the 2 x 2 workgroups; 0 single-block only
+    // fp4 band kernels on the GPU plan ($NLDSC_T2): 1 (default) missing-free 2 x 2 super-items in the 2 x 2
+    // block-pair workgroups, the rest in the single-block kernel; 3 the same with missing-free 4 x 4 super-items in
+    // the quad workgroups (64 x 64 tiles per wave); 2 everything in the 2 x 2 workgroups; 0 single-block only
     int t2_mode = 1;
     // single-block fp4 band in launches of one round of wave slots ($NLDSC_BAND_ROUNDS=0: one launch)
     bool band_rounds = true;
+    // round launches alternated over two streams ($NLDSC_BAND_STREAMS=2): round k + 1's workgroups take the wave
+    // slots round k's finished items free (two rounds in flight at most)
+    int band_streams = 1;
+    bool compact = true;  // $NLDSC_COMPACT=0: routed runs list every single-block item (routed ones return at once)
     DevBuf<uint8_t> blk_miss;
     int last_band_kernel = NLDSC_BAND_F4;
     DevBuf<double> pos, maf, rstd, l2_acc, l2d_acc, l2, l2d;
@@ -154,7 +164,11 @@ struct nldsc_engine {
     HostPinned h_sums;
     DevBuf<int> Ew, plan_counts, plan_meta, plan_counts2;
     DevBuf<int2> plan_rows, plan_rows2;
-    DevBuf<int4> items2;  // super-items of the 2 x 2 kernel
+    DevBuf<int4> items2;  // super-items of the 2 x 2 / quad kernel
+    DevBuf<int4> items_u;  // routed runs: the single-block items no super-item kernel takes (compacted)
+    DevBuf<int> compact_tmp;
+    HostPinned h_route;    // their count
+    hipEvent_t ev_route = nullptr;
     bool gpu_plan = true;  // band schedule on the GPU for non-negative sorted positions (NLDSC_GPU_PLAN=0: host)
     // timings of the last run
     double ms[6] = {0, 0, 0, 0, 0, 0};
@@ -167,7 +181,7 @@ struct nldsc_engine {
 
     ~nldsc_engine() {
         (void)hipSetDevice(device);
-        bed.release(); lastb.release(); flip.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
+        bed.release(); lastb.release(); flip.release(); row_miss.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
         ws3.release(); lut.release(); cst.release(); sflags.release(); pos.release(); maf.release(); rstd.release();
         l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release(); gram.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
@@ -179,6 +193,11 @@ struct nldsc_engine {
         if (ev_pos) (void)hipEventDestroy(ev_pos);
         if (ev_stats) (void)hipEventDestroy(ev_stats);
         if (ev_replay) (void)hipEventDestroy(ev_replay);
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_route) (void)hipEventDestroy(ev_route);
+        items_u.release(); compact_tmp.release();
+        if (ev_join) (void)hipEventDestroy(ev_join);
+        if (band_stream2) (void)hipStreamDestroy(band_stream2);
     }
 };
 
@@ -223,6 +242,7 @@ hipError_t alloc_image(nldsc_engine* e, int32_t n_snp, int32_t n_org) {
     hipError_t he = e->bed.ensure((size_t)padded_rows(n_snp) * (size_t)row_pitch(n_org));
     if (he == hipSuccess) he = e->lastb.ensure((size_t)n_snp);
     if (he == hipSuccess) he = e->flip.ensure((size_t)n_snp);
+    if (he == hipSuccess) he = e->row_miss.ensure((size_t)n_snp);
     return he;
 }
 
@@ -234,6 +254,13 @@ hipError_t finish_image(nldsc_engine* e, int32_t n_snp, int32_t n_org) {
     e->oriented = e->orient;
     if (he == hipSuccess && e->oriented)
         he = nldsc::launch_orient_rows(e->bed.p, e->lastb.p, n_snp, row_pitch(n_org), e->flip.p, e->stream);
+    // rows holding a missing call in either sample order (the last byte keeps its high / low N % 4 pairs)
+    const int rem = n_org % 4;
+    const uint32_t keep_compat = rem ? (0xFFu << (8 - 2 * rem)) & 0xFFu : 0xFFu;
+    const uint32_t keep_strict = rem ? (1u << (2 * rem)) - 1u : 0xFFu;
+    if (he == hipSuccess)
+        he = nldsc::launch_row_missing(e->bed.p, e->lastb.p, n_snp, nb, row_pitch(n_org), keep_compat, keep_strict,
+                                       e->row_miss.p, e->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
     if (he == hipSuccess) {
         e->n_snp = n_snp;
@@ -269,8 +296,11 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_ORIENT")) e->orient = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_KSPLIT")) e->ksplit_ok = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_REPLAY_OVERLAP")) e->replay_overlap = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_T2")) e->t2_mode = std::max(0, std::min(2, std::atoi(v)));
+    if (const char* v = std::getenv("NLDSC_T2")) e->t2_mode = std::max(0, std::min(3, std::atoi(v)));
     if (const char* v = std::getenv("NLDSC_BAND_ROUNDS")) e->band_rounds = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_BAND_STREAMS")) e->band_streams = std::atoi(v) == 2 ? 2 : 1;
+    if (const char* v = std::getenv("NLDSC_COMPACT")) e->compact = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_DEBUG_TIMING")) e->debug_timing = std::atoi(v) != 0;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
@@ -278,12 +308,20 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     }
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->plan_stream, hipStreamNonBlocking);
+    if (he == hipSuccess && e->band_streams == 2) {
+        he = hipStreamCreateWithFlags(&e->band_stream2, hipStreamNonBlocking);
+        if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
+        if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
+    }
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_pos, hipEventDisableTiming);
     for (auto& ev : e->ev)
         if (he == hipSuccess) he = hipEventCreate(&ev);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_plan, hipEventDisableTiming);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_stats, hipEventDisableTiming);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_replay, hipEventDisableTiming);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_route, hipEventDisableTiming);
+    for (auto& ev : e->ev_dbg)
+        if (he == hipSuccess) he = hipEventCreate(&ev);
     if (he != hipSuccess) {
         delete e;
         return set_err(err, errlen, NLDSC_E_HIP, "HIP error %s creating stream/events", hipGetErrorString(he));
@@ -511,7 +549,9 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                           std::all_of(p->positions, p->positions + M, [](double x) { return x >= 0.0; });
     // the 2 x 2 block-pair workgroups: fp4, unsegmented rows, GPU plan, and no K-split (choose_ksplit below)
     const bool t2_cand = e->t2_mode > 0 && gpu_plan && use_f4 && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 2;
-    const bool routed = e->t2_mode == 1;
+    const bool routed = e->t2_mode == 1 || e->t2_mode == 3;
+    const bool quad = e->t2_mode == 3;
+    const int route_shift = quad ? 2 : 1;  // super-items of 2^route_shift blocks a side
     // K-split (f4, unsegmented rows) when the items fill the wave slots (2 per SIMD) in few, partly empty
     // rounds — a rank's shard of one chromosome — and splitting the K loop in P pieces fills them better
     // Model: a round of items takes ~0.67 us per K chunk (C3: 2 466 chunks, 1.65 ms per round, 12.7 rounds in
@@ -565,6 +605,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                                   e->plan_rows.p, e->plan_counts.p, e->plan_meta.p, e->plan_stream));
         if (t2_cand)
             HIPCHK(nldsc::launch_plan_super(M, e->plan_rows.p, e->plan_rows2.p, e->plan_counts2.p, e->plan_meta.p + 4,
+                                            route_shift,
                                             e->plan_stream));
         HIPCHK(hipMemcpyAsync(e->h_meta.p, e->plan_meta.p, 8 * sizeof(int), hipMemcpyDeviceToHost, e->plan_stream));
         HIPCHK(hipEventRecord(e->ev_plan, e->plan_stream));
@@ -576,50 +617,66 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     HIPCHK(hipEventRecord(e->ev[1], st));
     HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->oriented ? e->flip.p : nullptr, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->cst.p,
                                    e->sflags.p, e->maf.p, e->rstd.p, st));
-    // rare variants: the reference's fp32 residual replayed (its sums assume N < 2^23).  The flags go first on
-    // the main stream; the replay itself (a few long sequential sums) runs on the plan stream beside the band
-    // launch for the items without a replayed SNP, and only the KC launch and finalize wait for it.
+    // rare variants: the reference's fp32 residual replayed (its sums assume N < 2^23); the flags per block here,
+    // the replay itself after the schedule (below)
     const bool replay = N < (1 << 23) && !(p->flags & NLDSC_FLAG_EXACT_RARE);
     // Invariant of the overlap: the replay rewrites, for replayed SNPs only, sflags bit 1 (residual pass; a byte
     // read-modify-write), cst and lut.  What runs beside it on the main stream reads sflags bits 0 (MAF pass:
-    // left_pointer_kernel, the host flag copy) and 2 (missing calls: block_missing_kernel, the band kernels' rm /
-    // cm), which the replay never changes, and never reads a replayed SNP's cst / lut before ev_replay: the items
+    // left_pointer_kernel, the host flag copy) and 2 (missing calls: the band kernels' rm / cm), which the
+    // replay never changes, and never reads a replayed SNP's cst / lut before ev_replay: the items
     // of blocks holding one are skipped (skip_item) until the KC launch, and the K-split part kernel, which runs
     // them, stores Gram tiles without reading constants.  No other kernel writes sflags after snp_stats_kernel.
     if (replay) {
         HIPCHK(nldsc::launch_replay_flags(e->counts.p, e->oriented ? e->flip.p : nullptr, e->sflags.p, M,
                                           e->blk_rep.p, st));
-        hipStream_t rs = e->replay_overlap ? e->plan_stream : st;
         HIPCHK(hipEventRecord(e->ev_stats, st));
-        HIPCHK(hipStreamWaitEvent(rs, e->ev_stats, 0));
-        HIPCHK(nldsc::launch_reference_residuals(e->bed.p, row_bytes, N, strict, e->counts.p,
-                                                 e->oriented ? e->flip.p : nullptr, M, p->std_thr, e->cst.p, e->lut.p,
-                                                 e->sflags.p, e->rstd.p, rs));
-        HIPCHK(hipEventRecord(e->ev_replay, rs));
     }
     HIPCHK(hipEventRecord(e->ev[2], st));
 
     // ---- window replay + schedule ----
     auto t_host0 = std::chrono::steady_clock::now();
     int n_items = 0;
+    const int order = strict ? 1 : 0;  // bit of row_miss: the individual slots of this run's sample order
+    bool compact = false;
     if (gpu_plan) {
         HIPCHK(hipEventSynchronize(e->ev_plan));  // the count kernel is running meanwhile
-        HIPCHK(hipStreamWaitEvent(st, e->ev_plan, 0));  // emit / left pointers / band read the schedule
         const int* meta = reinterpret_cast<const int*>(e->h_meta.p);
         n_items = meta[1];
         ksplit = choose_ksplit(n_items);
         use_t2 = t2_cand && ksplit == 1 && n_items > 0;
+        // The work lists go out on the plan stream, beside the count kernel: the items, the super-items, the routing
+        // (blk_miss, from the load-time row_miss: it needs no count) and, with super-item routing, the list of the
+        // items the single-block kernel keeps, compacted in order, so its launches (round launches, the K-split tail)
+        // are sized by its own work — its length reaches the host before the band.  The main stream waits for them.
+        hipStream_t ps = e->plan_stream;
         if (use_t2) {
             n_items2 = meta[5];
             HIPCHK(e->items2.ensure(std::max<size_t>((size_t)n_items2, 1)));
             HIPCHK(nldsc::launch_plan_emit_super(M, e->plan_rows2.p, e->plan_meta.p + 4, e->plan_counts2.p,
-                                                 e->items2.p, st));
+                                                 e->items2.p, route_shift, ps));
         }
         if (!use_t2 || routed) {
             HIPCHK(e->items.ensure(std::max<size_t>((size_t)n_items, 1)));
             if (n_items > 0)
-                HIPCHK(nldsc::launch_plan_emit(M, e->plan_rows.p, e->plan_meta.p, e->plan_counts.p, e->items.p, st));
+                HIPCHK(nldsc::launch_plan_emit(M, e->plan_rows.p, e->plan_meta.p, e->plan_counts.p, e->items.p, ps));
         }
+        if (use_f4) {  // per 32-SNP block: holds a missing call (the kernels' m-product predicate: routing, issued count)
+            HIPCHK(e->blk_miss.ensure((size_t)nblk));
+            HIPCHK(nldsc::launch_block_missing_rows(e->row_miss.p, M, order, e->blk_miss.p, ps));
+        }
+        compact = use_t2 && routed && n_items > 0 && e->compact;
+        if (compact) {
+            const size_t n_chunks = ((size_t)n_items + 1023) / 1024;
+            HIPCHK(e->items_u.ensure((size_t)n_items));
+            HIPCHK(e->compact_tmp.ensure(n_chunks + 1));
+            HIPCHK(e->h_route.ensure(sizeof(int)));
+            *reinterpret_cast<volatile int*>(e->h_route.p) = -1;  // (the copy below lands the count, >= 0)
+            HIPCHK(nldsc::launch_compact_items(e->items.p, n_items, e->blk_miss.p, route_shift, nblk, e->compact_tmp.p,
+                                               e->compact_tmp.p + n_chunks, e->items_u.p, ps));
+            HIPCHK(hipMemcpyAsync(e->h_route.p, e->compact_tmp.p + n_chunks, sizeof(int), hipMemcpyDeviceToHost, ps));
+        }
+        HIPCHK(hipEventRecord(e->ev_route, ps));
+        HIPCHK(hipStreamWaitEvent(st, e->ev_route, 0));  // left pointers / band read the schedule and the lists
         HIPCHK(nldsc::launch_left_pointers(e->Aw.p, e->sflags.p, e->pos.p, M, e->Lw.p, st));
     } else {
     e->h_L.resize(M);
@@ -672,9 +729,20 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     n_items = (int)e->h_items.size();
     ksplit = choose_ksplit(n_items);
     }
-    if (use_f4) {  // per 32-SNP block: holds a missing call (the kernels' m-product predicate; routing, issued count)
+    if (use_f4 && !gpu_plan) {  // (the GPU plan computes it on the plan stream)
         HIPCHK(e->blk_miss.ensure((size_t)nblk));
-        HIPCHK(nldsc::launch_block_missing(e->sflags.p, M, e->blk_miss.p, st));
+        HIPCHK(nldsc::launch_block_missing_rows(e->row_miss.p, M, order, e->blk_miss.p, st));
+    }
+    // rare variants: the reference's fp32 residual replayed (its sums assume N < 2^23).  The flags went first on the
+    // main stream; the replay itself (a few long sequential sums) runs on the plan stream beside the band launch for
+    // the items without a replayed SNP, and only the KC launch and finalize wait for it.
+    if (replay) {
+        hipStream_t rs = e->replay_overlap ? e->plan_stream : st;
+        HIPCHK(hipStreamWaitEvent(rs, e->ev_stats, 0));
+        HIPCHK(nldsc::launch_reference_residuals(e->bed.p, row_bytes, N, strict, e->counts.p,
+                                                 e->oriented ? e->flip.p : nullptr, M, p->std_thr, e->cst.p, e->lut.p,
+                                                 e->sflags.p, e->rstd.p, rs));
+        HIPCHK(hipEventRecord(e->ev_replay, rs));
     }
     HIPCHK(hipMemsetAsync(e->l2_acc.p, 0, sizeof(double) * M, st));
     HIPCHK(hipMemsetAsync(e->l2d_acc.p, 0, sizeof(double) * M, st));
@@ -684,10 +752,16 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     HIPCHK(hipEventRecord(e->ev[3], st));
     e->n_band_items = n_items;
     e->last_ksplit = ksplit;
-    e->last_band_kernel = use_t2 ? (routed ? NLDSC_BAND_F4_ROUTED : NLDSC_BAND_F4_2X2) : !use_f4 ? (use_i8 ? NLDSC_BAND_I8 : NLDSC_BAND_F32)
+    e->last_band_kernel = use_t2 ? (quad ? NLDSC_BAND_F4_QUAD : routed ? NLDSC_BAND_F4_ROUTED : NLDSC_BAND_F4_2X2) : !use_f4 ? (use_i8 ? NLDSC_BAND_I8 : NLDSC_BAND_F32)
                         : ksplit > 1 ? NLDSC_BAND_F4_KSPLIT : n_it > nldsc::F4_SEG_CHUNKS ? NLDSC_BAND_F4_SEG
                         : NLDSC_BAND_F4;
     if (ksplit > 1) HIPCHK(e->gram.ensure((size_t)n_items * ksplit * 8192));
+    const int slots = 8 * e->n_cu;
+    // which = 1: the launch for the items without a replayed SNP (beside the replay), 2: the KC launch after it
+    const uint8_t* blk_rep = replay ? e->blk_rep.p : nullptr;
+    int n_single = n_items;            // single-block items (compacted when routed)
+    const int4* single = e->items.p;
+    int round_items = 0, tail_p = 1, n_full = 0;
     // Unsegmented single-block fp4 items go in launches of one round of the wave slots each (2 per SIMD): the items
     // of a launch start together and, all of equal length, stay at nearby K offsets, so the waves on one XCD that
     // share a strip (the plan's 16 x 16 tiles) read it from that XCD's L2.  In one launch of all items the waves
@@ -695,57 +769,100 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // GHz; band -2 to -4 % after the launch tails).  Only for bands of several rounds, and only for long rows: the
     // waves of a round also reach their epilogues together, which then no longer overlap another wave's products —
     // at N = 50 000 (strips of 0.4 MB, L2-resident anyway; epilogue ~1/3 of an item) round launches made the band
-    // 2.8 -> 5.1 ms.
-    const int slots = 8 * e->n_cu;
-    const int round_items = use_f4 && ksplit == 1 && e->band_rounds && n_it <= nldsc::F4_SEG_CHUNKS &&
-                            n_it >= 1024 && n_items >= 4 * slots ? slots : 0;
-    e->last_round_items = round_items;
-    // The last, partial round leaves wave slots idle for a whole item length (C3: 1 458 items in 2 048 slots); those
-    // items are K-split instead when the cost model finds it cheaper (C3: P = 7, 5 rounds of 1/7 of an item).
-    const int tail = round_items > 0 ? n_items % round_items : 0;
-    const int tail_p = tail > 0 ? choose_ksplit(tail) : 1;
-    const int n_full = tail_p > 1 ? n_items - tail : n_items;
-    e->last_tail_ksplit = tail_p;
-    if (tail_p > 1) HIPCHK(e->gram.ensure((size_t)tail * tail_p * 8192));
-    // which = 1: the launch for the items without a replayed SNP (beside the replay), 2: the KC launch after it
-    const uint8_t* blk_rep = replay ? e->blk_rep.p : nullptr;
-    auto launch_band_path = [&](int which) -> hipError_t {
-        const uint8_t* miss = use_t2 && routed ? e->blk_miss.p : nullptr;
-        if (use_t2) {
-            hipError_t r = nldsc::launch_band_f4_t2(dom, n_items2, geno, pitch_words, n_it, e->cst.p, e->items2.p,
-                                                    e->plan_rows.p, nblk, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
-                                                    p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p,
-                                                    e->l2d_acc.p, e->ws_acc.p, true, blk_rep, miss, which, st);
-            if (r != hipSuccess || !routed) return r;
-        }
+    // 2.8 -> 5.1 ms.  The last, partial round leaves wave slots idle for a whole item length (C3: 1 458 items in
+    // 2 048 slots); those items are K-split instead when the cost model finds it cheaper (C3: P = 7, 5 rounds of 1/7
+    // of an item).
+    auto size_single = [&]() -> hipError_t {
+        round_items = use_f4 && ksplit == 1 && e->band_rounds && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 1024 &&
+                      n_single >= 4 * slots ? slots : 0;
+        const int tail = round_items > 0 ? n_single % round_items : 0;
+        tail_p = tail > 0 ? choose_ksplit(tail) : 1;
+        n_full = tail_p > 1 ? n_single - tail : n_single;
+        e->last_round_items = round_items;
+        e->last_tail_ksplit = tail_p;
+        return tail_p > 1 ? e->gram.ensure((size_t)tail * tail_p * 8192) : hipSuccess;
+    };
+    auto launch_super = [&](int which) -> hipError_t {
+        return (quad ? nldsc::launch_band_f4_q : nldsc::launch_band_f4_t2)(
+            dom, n_items2, geno, pitch_words, n_it, e->cst.p, e->items2.p, e->plan_rows.p, nblk, e->pos.p, e->Lw.p,
+            e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
+            e->ws_acc.p, true, blk_rep, routed ? e->blk_miss.p : nullptr, which, st);
+    };
+    // (uncompacted routed list, $NLDSC_COMPACT=0: the kernels skip the items a super-item kernel takes)
+    const uint8_t* single_miss = use_t2 && routed && !compact ? e->blk_miss.p : nullptr;
+    auto launch_single = [&](int which) -> hipError_t {
         if (use_f4 && ksplit > 1)
-            return nldsc::launch_band_f4_split(dom, ksplit, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p,
+            return nldsc::launch_band_f4_split(dom, ksplit, n_single, geno, pitch_words, n_it, e->cst.p, single,
                                                e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N,
                                                p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p,
                                                blk_rep, e->gram.p, which, st);
         if (use_f4) {
-            hipError_t r = nldsc::launch_band_f4(dom, max_nc, n_full, geno, pitch_words, n_it, e->cst.p, e->items.p,
+            // (two band streams: the odd rounds go to band_stream2, forked from and joined back into `st`)
+            const bool two = round_items > 0 && e->band_stream2 != nullptr && (which & 1);
+            if (two) {
+                hipError_t r = hipEventRecord(e->ev_fork, st);
+                if (r == hipSuccess) r = hipStreamWaitEvent(e->band_stream2, e->ev_fork, 0);
+                if (r != hipSuccess) return r;
+            }
+            hipError_t r = nldsc::launch_band_f4(dom, max_nc, n_full, geno, pitch_words, n_it, e->cst.p, single,
                                                  e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N,
                                                  p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
-                                                 e->ws_acc.p, true, blk_rep, which, st, miss, round_items);
-            if (r != hipSuccess || n_full == n_items) return r;
-            return nldsc::launch_band_f4_split(dom, tail_p, n_items - n_full, geno, pitch_words, n_it, e->cst.p,
-                                               e->items.p + n_full, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
+                                                 e->ws_acc.p, true, blk_rep, which, st, single_miss, round_items,
+                                                 route_shift, two ? e->band_stream2 : nullptr);
+            if (two) {
+                hipError_t rj = hipEventRecord(e->ev_join, e->band_stream2);
+                if (rj == hipSuccess) rj = hipStreamWaitEvent(st, e->ev_join, 0);
+                if (r == hipSuccess) r = rj;
+            }
+            if (r != hipSuccess || n_full == n_single) return r;
+            return nldsc::launch_band_f4_split(dom, tail_p, n_single - n_full, geno, pitch_words, n_it, e->cst.p,
+                                               single + n_full, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
                                                p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p,
-                                               e->l2d_acc.p, e->ws_acc.p, blk_rep, e->gram.p, which, st, miss);
+                                               e->l2d_acc.p, e->ws_acc.p, blk_rep, e->gram.p, which, st, single_miss,
+                                               route_shift);
         }
-        return nldsc::launch_band_i8(dom, max_nc, n_items, geno, pitch_words, n_it, e->cst.p, e->items.p, e->pos.p,
+        return nldsc::launch_band_i8(dom, max_nc, n_single, geno, pitch_words, n_it, e->cst.p, single, e->pos.p,
                                      e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin,
                                      own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true, blk_rep, which, st);
     };
+    const bool run_single = !use_t2 || routed;  // ($NLDSC_T2=2: every block pair in the 2 x 2 workgroups)
     if (n_items > 0 && (use_f4 || use_i8)) {
-        HIPCHK(launch_band_path(1));
+        if (use_t2) HIPCHK(launch_super(1));
+        if (e->debug_timing) HIPCHK(hipEventRecord(e->ev_dbg[0], st));
+        const auto t_wait0 = std::chrono::steady_clock::now();
+        if (compact) {  // the super-item kernel is queued: the host waits for the compacted count meanwhile
+            // (polling the pinned word the copy lands in: a blocking event wait wakes the thread tens of
+            // microseconds late, time the GPU would idle when the super-item kernel has nothing to do)
+            volatile int* cnt = reinterpret_cast<volatile int*>(e->h_route.p);
+            const auto t0 = std::chrono::steady_clock::now();
+            while (*cnt < 0 && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2)) {
+            }
+            HIPCHK(hipEventSynchronize(e->ev_route));  // (returns at once when the count has landed)
+            n_single = *cnt;
+            single = e->items_u.p;
+        } else if (use_t2 && routed) {
+            single = e->items.p;  // $NLDSC_COMPACT=0: every item listed, the routed ones return at once
+        }
+        HIPCHK(size_single());
+        const auto t_wait1 = std::chrono::steady_clock::now();
+        if (e->debug_timing) HIPCHK(hipEventRecord(e->ev_dbg[1], st));
+        if (run_single) HIPCHK(launch_single(1));
+        if (e->debug_timing) {
+            HIPCHK(hipStreamSynchronize(st));
+            float a = 0, b = 0;
+            HIPCHK(hipEventElapsedTime(&a, e->ev[3], e->ev_dbg[0]));
+            HIPCHK(hipEventElapsedTime(&b, e->ev_dbg[0], e->ev_dbg[1]));
+            std::fprintf(stderr, "[nldsc debug] super %.3f ms, gap to single %.3f ms, host wait %.3f ms, n_single %d/%d\n",
+                         a, b, std::chrono::duration<double, std::milli>(t_wait1 - t_wait0).count(), n_single, n_items);
+        }
         if (replay) {
             HIPCHK(hipStreamWaitEvent(st, e->ev_replay, 0));
-            HIPCHK(launch_band_path(2));
+            if (use_t2) HIPCHK(launch_super(2));
+            if (run_single) HIPCHK(launch_single(2));
         }
-    } else if (replay) {
-        HIPCHK(hipStreamWaitEvent(st, e->ev_replay, 0));  // the fp32 path reads the replayed tables everywhere
+    } else {
+        HIPCHK(size_single());
+        if (replay) HIPCHK(hipStreamWaitEvent(st, e->ev_replay, 0));  // the fp32 path reads the replayed tables
     }
     if (n_items > 0 && !use_f4 && !use_i8) {
         HIPCHK(nldsc::launch_band(dom, 2, n_items, geno, pitch_words, n_it,
@@ -764,9 +881,11 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     HIPCHK(e->sums.ensure(3));
     HIPCHK(e->h_sums.ensure(3 * sizeof(unsigned long long)));
     HIPCHK(hipMemsetAsync(e->sums.p, 0, 3 * sizeof(unsigned long long), st));
-    HIPCHK(nldsc::launch_issued_products(e->items.p, use_t2 && !routed ? 0 : n_items, use_t2 ? e->items2.p : nullptr,
+    HIPCHK(nldsc::launch_issued_products(single, run_single ? n_single : 0, use_t2 ? e->items2.p : nullptr,
                                          n_items2, gpu_plan ? e->plan_rows.p : nullptr,
-                                         use_f4 ? e->blk_miss.p : nullptr, nblk, path, dom, use_t2 && routed,
+                                         use_f4 ? e->blk_miss.p : nullptr, nblk, path, dom,
+                                         (use_t2 && routed ? 2 : 0) | (single_miss != nullptr ? 1 : 0),
+                                         route_shift,
                                          e->sums.p + 2, st));
     const int n_own = own_end - own_begin;
     double sw = 0, sd = 0;

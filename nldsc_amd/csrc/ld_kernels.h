@@ -44,6 +44,14 @@ hipError_t launch_replay_flags(const int* counts, const uint8_t* flip, const uin
 hipError_t launch_reference_residuals(const uint8_t* img, int row_bytes, int n_org, bool strict, const int* counts,
                                      const uint8_t* flip, int n_snp, double std_thr, SnpConst* cst, float2* lut,
                                      uint8_t* sflags, double* rstd_out, hipStream_t st);
+// after a load: row_miss[j] bit 0 / bit 1 = row j holds a missing call (01) among the individual slots of the
+// reference's / PLINK's sample order (keep masks of the last byte as the count kernel's tail_keep)
+hipError_t launch_row_missing(const uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes,
+                              uint32_t keep_compat, uint32_t keep_strict, uint8_t* row_miss, hipStream_t st);
+// per run (fp4): blk_miss[b] from row_miss (order 0 reference, 1 PLINK) — equal to the sflags-bit-2 predicate of the
+// band kernels, known without the count kernel
+hipError_t launch_block_missing_rows(const uint8_t* row_miss, int n_snp, int order, uint8_t* blk_miss,
+                                     hipStream_t st);
 // after a load: swap 00 <-> 11 in rows (and saved last bytes) with more hom-A2 than hom-A1 calls; flip[j] = 1
 hipError_t launch_orient_rows(uint8_t* img, uint8_t* last, int n_snp, int row_bytes, uint8_t* flip, hipStream_t st);
 // exact left pointers L from the all-pass replay's A and the device MAF flags (sorted positions)
@@ -74,7 +82,8 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
-                          int which, hipStream_t st, const uint8_t* blk_miss = nullptr, int round_items = 0);
+                          int which, hipStream_t st, const uint8_t* blk_miss = nullptr, int round_items = 0,
+                          int route_shift = 1, hipStream_t st2 = nullptr);  // st2: odd round launches
 // the same with the K loop split in P pieces (small launches: better filled wave slots): partial Gram tiles to
 // `gram` (n_items * P * 8192 floats), then an epilogue kernel (unsegmented rows, n_it <= F4_SEG_CHUNKS)
 hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* geno, int pitch_words, int n_it,
@@ -82,34 +91,48 @@ hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* ge
                                 const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr,
                                 int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc,
                                 const uint8_t* blk_rep, float* gram, int which, hipStream_t st,
-                                const uint8_t* blk_miss = nullptr);
+                                const uint8_t* blk_miss = nullptr, int route_shift = 1);
 // 2 x 2 block-pair workgroups (unsegmented rows, gpu plan): super-items (I2, J2, 1, 0) over row / column
 // super-blocks of two 32-SNP blocks, planned from the single-block rows (launch_plan) by launch_plan_super (meta2
 // as meta; counts2 capacity ceil(nblk2/16)^2) and launch_plan_emit_super; the kernel reads `rows` (nblk) to skip the
 // block pairs the single-block plan does not hold
 constexpr int T2_STAGES = 4;  // LDS ring stages (2 chunks each) of band_f4_t2_kernel
-hipError_t launch_plan_super(int n, const int2* rows, int2* rows2, int* counts2, int* meta2, hipStream_t st);
+// shift 1: 2 x 2 super-items; shift 2: the quad kernel's 4 x 4 super-items
+hipError_t launch_plan_super(int n, const int2* rows, int2* rows2, int* counts2, int* meta2, int shift, hipStream_t st);
 hipError_t launch_plan_emit_super(int n, const int2* rows2, const int* meta2, const int* offsets2, int4* items2,
-                                  hipStream_t st);
+                                  int shift, hipStream_t st);
 hipError_t launch_band_f4_t2(bool dom, int n_items2, const uint32_t* geno, int pitch_words, int n_it,
                              const SnpConst* cst, const int4* items2, const int2* rows, int nblk, const double* pos,
                              const int* Lw, const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind,
                              double n_org, double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
                              int* ws_acc, bool xcd, const uint8_t* blk_rep, const uint8_t* blk_miss, int which,
                              hipStream_t st);
-// blk_miss[b] = block b holds a missing call.  Passed to both fp4 kernels (unsegmented rows) it routes the
-// super-items: missing-free ones to the 2 x 2 kernel (operand-feed bound at 3 products per K step, where sharing
-// the strips pays), the block pairs of the others to the single-block kernel (MFMA bound at 8 products)
-hipError_t launch_block_missing(const uint8_t* sflags, int n_snp, uint8_t* blk_miss, hipStream_t st);
+// 4 x 4 block-pair workgroups (the quad kernel: one wave per SIMD, 64 x 64 SNP tiles) for the missing-free 4 x 4
+// super-items (I4, J4, 1, 0) of launch_plan_super(shift 2); blk_miss required (route_shift 2 for the other kernels)
+constexpr int Q_STAGES = 4;
+hipError_t launch_band_f4_q(bool dom, int n_items4, const uint32_t* geno, int pitch_words, int n_it,
+                            const SnpConst* cst, const int4* items4, const int2* rows, int nblk, const double* pos,
+                            const int* Lw, const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind,
+                            double n_org, double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
+                            int* ws_acc, bool xcd, const uint8_t* blk_rep, const uint8_t* blk_miss, int which,
+                            hipStream_t st);
+// blk_miss[b] = block b holds a missing call (launch_block_missing_rows).  Passed to the fp4 kernels (unsegmented rows)
+// it routes the super-items: missing-free ones to a super-item kernel (operand-feed bound at 3 products per K step,
+// where sharing the strips pays), the block pairs of the others to the single-block kernel (MFMA bound at 8 products)
 hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2d_acc, const int* ws_acc, int n_snp,
                            int own_lo, int own_hi, bool dom, double* l2, double* l2d, int* ws3, hipStream_t st);
 // the matrix-core products the band kernels issued (one per 32x32 block product over all K), counted per work item
-// as each kernel decides them: kind 2 fp4 single-block items (+ 2 x 2 super-items when items2 != nullptr; `routed`:
-// each item counted in the kernel the routing sends it to), 1 int8, 0 fp32 (items of it.z column blocks);
+// as each kernel decides them: kind 2 fp4 single-block items (+ the super-items when items2 != nullptr; `routed`
+// bit 0: skip single items routed to a super-item kernel, bit 1: count only routed super-items), 1 int8, 0 fp32
+// (items of it.z column blocks);
 // blk_miss may be nullptr for kinds 0 and 1.  out[0] += the count (zeroed before)
 hipError_t launch_issued_products(const int4* items, int n_items, const int4* items2, int n_items2, const int2* rows,
-                                 const uint8_t* blk_miss, int nblk, int kind, bool dom, bool routed,
+                                 const uint8_t* blk_miss, int nblk, int kind, bool dom, int routed, int route_shift,
                                  unsigned long long* out, hipStream_t st);
+// the single-block items no super-item kernel takes (routing of 2^route_shift-block super-items), in their order, to
+// `out`; *total = their count (device); chunk_counts: ceil(n_items / 1024) ints of scratch
+hipError_t launch_compact_items(const int4* items, int n_items, const uint8_t* blk_miss, int route_shift, int nblk,
+                                int* chunk_counts, int* total, int4* out, hipStream_t st);
 // the owned slice [own_lo, own_hi) of the finalized results as a [7][width] fp64 table in device memory (columns
 // past the slice NaN) + sums[0] += sum of positive WSA, sums[1] += sum of positive WSD over the slice (zeroed before)
 hipError_t launch_pack_table(const double* l2, const double* l2d, const double* maf, const double* rstd, const int* ws3,

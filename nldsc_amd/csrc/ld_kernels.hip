@@ -100,6 +100,43 @@ __global__ void __launch_bounds__(256) orient_rows_kernel(uint8_t* __restrict__ 
     }
 }
 
+// After a load: which rows hold a missing call (code 01) among the individual slots of each sample order —
+// row_miss[j] bit 0 for the reference's order (the last byte keeps its high N % 4 pairs), bit 1 for PLINK's (the low
+// pairs); the other slots of the last byte and the pitch padding are not individuals.  It does not depend on the run's
+// parameters, so the fp4 band's routing (blk_miss) is known before the per-run count kernel finishes.
+__device__ __forceinline__ int count_missing(uint32_t word) {
+    return __popc(~(word >> 1) & word & 0x55555555u);  // pairs 01
+}
+__global__ void __launch_bounds__(256) row_missing_kernel(const uint8_t* __restrict__ img,
+                                                          const uint8_t* __restrict__ last, int n_snp, int nb,
+                                                          int row_bytes, uint32_t keep_compat, uint32_t keep_strict,
+                                                          uint8_t* __restrict__ row_miss) {
+    const int j = blockIdx.x;
+    if (j >= n_snp) return;
+    const uint8_t* row = img + (size_t)j * (size_t)row_bytes;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(row);
+    const int full_words = (nb - 1) / 4;  // whole words before the last byte
+    int m = 0;
+    for (int q = threadIdx.x; q < full_words; q += blockDim.x) m += count_missing(w[q]);
+    for (int p = 4 * full_words + threadIdx.x; p < nb - 1; p += blockDim.x) m += count_missing(row[p]);
+    m = __syncthreads_or(m);
+    if (threadIdx.x == 0) {
+        const uint32_t lb = last[j];
+        const int mc = m | count_missing(lb & keep_compat), ms = m | count_missing(lb & keep_strict);
+        row_miss[j] = (uint8_t)((mc ? 1 : 0) | (ms ? 2 : 0));
+    }
+}
+
+// per run: blk_miss[b] = block b holds a row with a missing call in this run's sample order (bit `order` of row_miss)
+__global__ void block_missing_rows_kernel(const uint8_t* __restrict__ row_miss, int n_snp, int order,
+                                          uint8_t* __restrict__ blk_miss) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (32 * b >= n_snp) return;
+    uint8_t m = 0;
+    for (int j = 32 * b; j < min(n_snp, 32 * b + 32); ++j) m |= (row_miss[j] >> order) & 1;
+    blk_miss[b] = m;
+}
+
 // Per run: genotype-code counts of every row (one workgroup per SNP, 16-byte non-temporal loads, 8 in
 // flight per thread) after setting the row's non-individual slots — the last byte's bit pairs that are
 // not individuals for this run's sample order, (saved byte & keep) | (pad & ~keep), and the pitch padding
@@ -682,6 +719,30 @@ __global__ void __launch_bounds__(1024) plan_scan_kernel(int* __restrict__ count
         run += c;
     }
     if (t == 1023) meta[1] = part[1023];
+}
+
+// one workgroup of 1024: exclusive scan of n counts in place; *total = their sum
+__global__ void __launch_bounds__(1024) scan_counts_kernel(int* __restrict__ counts, int n, int* __restrict__ total) {
+    __shared__ int part[1024];
+    const int t = threadIdx.x, per = (n + 1023) / 1024;
+    const int b = min(n, t * per), e = min(n, b + per);
+    int sum = 0;
+    for (int k = b; k < e; ++k) sum += counts[k];
+    part[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int run = t > 0 ? part[t - 1] : 0;
+    for (int k = b; k < e; ++k) {
+        const int c = counts[k];
+        counts[k] = run;
+        run += c;
+    }
+    if (t == 1023) *total = part[1023];
 }
 
 __global__ void plan_emit_kernel(const int2* __restrict__ rows, int nblk, const int* __restrict__ meta,
@@ -1343,6 +1404,42 @@ __device__ __forceinline__ F4Frag decode_f4(uint32_t wa, uint32_t wb) {
 template <bool WM>
 constexpr int H_SCALE = WM ? E8M0_ONE : E8M0_HALF;
 
+// Parity-grouped decode (study variant, NLDSC_PARITY_DECODE=1): one K step takes the even codes of a chunk's four
+// words, the next the odd codes, so every dword of an operand has the same bit placement and each plane sits where
+// one shift (shared by v and the planes of that parity) puts it: even v = (w << 1) & 0x66.., h = w & 0x22.. (1.0;
+// missing-free blocks (w << 1) & 0x44.. = 2.0), m = (w << 1) & ~w & 0x22.. (1.0); odd v = (w >> 1) & 0x66..,
+// h = (w >> 1) & 0x44.. (2.0), m = w & ~(w >> 1) & 0x44.. (2.0) — 8 VALU per word with missing calls instead of 9.
+// Scales per step: h and m planes at 2.0 take the E8M0 scale 2^-1.
+#ifndef NLDSC_PARITY_DECODE
+#define NLDSC_PARITY_DECODE 0
+#endif
+template <bool WM, int PAR>  // PAR 1: even codes, 2: odd codes
+__device__ __forceinline__ F4Frag decode_f4_par(const uint4& c) {
+    constexpr uint32_t M = 0x22222222u, K6 = 0x66666666u, M4 = 0x44444444u;
+    F4Frag f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t w = k == 0 ? c.x : k == 1 ? c.y : k == 2 ? c.z : c.w;
+        if constexpr (PAR == 1) {
+            const uint32_t s1 = w << 1;
+            f.x[k] = (int)(s1 & K6);
+            f.h[k] = (int)(WM ? (w & M) : (s1 & M4));
+            f.o[k] = WM ? (int)(s1 & ~w & M) : 0;
+        } else {
+            const uint32_t s2 = w >> 1;
+            f.x[k] = (int)(s2 & K6);
+            f.h[k] = (int)(s2 & M4);
+            f.o[k] = WM ? (int)(w & ~s2 & M4) : 0;
+        }
+    }
+    return f;
+}
+// E8M0 scales of the h / m planes of decode_f4_par<WM, PAR> (PAR 0: decode_f4<WM>)
+template <bool WM, int PAR>
+constexpr int PAR_H_SCALE = PAR == 2 ? E8M0_HALF : H_SCALE<WM>;
+template <int PAR>
+constexpr int PAR_M_SCALE = PAR == 2 ? E8M0_HALF : E8M0_ONE;
+
 // SA / SB: E8M0 block scales of the A / B operand (H_SCALE for an h plane)
 template <int SA = E8M0_ONE, int SB = E8M0_ONE>
 __device__ __forceinline__ f32x16v mfma_f4(const i32x4& a, const i32x4& b, const f32x16v& c) {
@@ -1396,21 +1493,23 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         colp[c] = reinterpret_cast<const uint4*>(geno + (size_t)((J0 + c) * 32 + i) * (size_t)pitch_words) + h;
     // RM / CM: the row / column block holds missing calls.  A block without any has an all-zero m plane,
     // so the products with it are skipped (imputed hard calls: 3 of the 8 MFMAs remain).
-    auto mfmas_v = [&](const F4Frag& a, const F4Frag (&b)[NC], auto RMc, auto CMc) {
+    auto mfmas_v = [&](const F4Frag& a, const F4Frag (&b)[NC], auto RMc, auto CMc, auto PARc) {
         constexpr bool RM = decltype(RMc)::value, CM = decltype(CMc)::value;
+        constexpr int PAR = decltype(PARc)::value;  // 0: decode_f4; 1 / 2: decode_f4_par even / odd codes
+        constexpr int hA = PAR_H_SCALE<RM, PAR>, hB = PAR_H_SCALE<CM, PAR>, mS = PAR_M_SCALE<PAR>;
         // Issue order xx, xo, xh, ox, hx, oo, oh, ho: the order alone moves the band kernel by up to 12 %
         // (decode interleave, register assignment); this one measured best of 18 orders in round 1.  On a
         // diagonal block m.x and h.x are the transposes of x.m and x.h (skipped).
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             gxx[c] = mfma_f4(a.x, b[c].x, gxx[c]);
-            if (CM) gxo[c] = mfma_f4(a.x, b[c].o, gxo[c]);
-            if (DOM) gxh[c] = mfma_f4<E8M0_ONE, H_SCALE<CM>>(a.x, b[c].h, gxh[c]);
-            if (RM && !(DIAG0 && c == 0)) gox[c] = mfma_f4(a.o, b[c].x, gox[c]);
-            if (DOM && !(DIAG0 && c == 0)) ghx[c] = mfma_f4<H_SCALE<RM>, E8M0_ONE>(a.h, b[c].x, ghx[c]);
-            if (RM && CM) goo[c] = mfma_f4(a.o, b[c].o, goo[c]);
-            if (DOM && RM) goh[c] = mfma_f4<E8M0_ONE, H_SCALE<CM>>(a.o, b[c].h, goh[c]);
-            if (DOM && CM && !(DIAG0 && c == 0)) gho[c] = mfma_f4<H_SCALE<RM>, E8M0_ONE>(a.h, b[c].o, gho[c]);
+            if (CM) gxo[c] = mfma_f4<E8M0_ONE, mS>(a.x, b[c].o, gxo[c]);
+            if (DOM) gxh[c] = mfma_f4<E8M0_ONE, hB>(a.x, b[c].h, gxh[c]);
+            if (RM && !(DIAG0 && c == 0)) gox[c] = mfma_f4<mS, E8M0_ONE>(a.o, b[c].x, gox[c]);
+            if (DOM && !(DIAG0 && c == 0)) ghx[c] = mfma_f4<hA, E8M0_ONE>(a.h, b[c].x, ghx[c]);
+            if (RM && CM) goo[c] = mfma_f4<mS, mS>(a.o, b[c].o, goo[c]);
+            if (DOM && RM) goh[c] = mfma_f4<mS, hB>(a.o, b[c].h, goh[c]);
+            if (DOM && CM && !(DIAG0 && c == 0)) gho[c] = mfma_f4<hA, mS>(a.h, b[c].o, gho[c]);
         }
         // full 8-product steps: F4_VPM VALU after each MFMA; otherwise (additive-only items, missing-free
         // blocks) the decode is spread evenly over the MFMAs there are (additive-only C2: -6.6 % band time)
@@ -1434,39 +1533,52 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     // even chunks, Q odd ones; each is reloaded right after its last word is decoded and read again two K
     // steps later, with no register copies of loads in flight (those would force vmcnt(0)).
     auto kloop = [&](auto RMc, auto CMc, const int t_lo, const int t_hi) {
-        constexpr bool RM = decltype(RMc)::value, CM = decltype(CMc)::value;
+        constexpr bool PD = NLDSC_PARITY_DECODE != 0;
+        // set 0 holds a chunk's words 0-1 (PD: its even codes), set 1 words 2-3 (PD: its odd codes)
+        auto dec0 = [](const uint4& w, auto WMc) {
+            constexpr bool WM = decltype(WMc)::value;
+            if constexpr (PD) return decode_f4_par<WM, 1>(w);
+            else return decode_f4<WM>(w.x, w.y);
+        };
+        auto dec1 = [](const uint4& w, auto WMc) {
+            constexpr bool WM = decltype(WMc)::value;
+            if constexpr (PD) return decode_f4_par<WM, 2>(w);
+            else return decode_f4<WM>(w.z, w.w);
+        };
+        const auto P0 = std::integral_constant<int, PD ? 1 : 0>{};
+        const auto P1 = std::integral_constant<int, PD ? 2 : 0>{};
         const int last = t_hi - 1;
         uint4 pr = rowp[2 * t_lo], qr = rowp[2 * t_lo + 2], pc[NC], qc[NC];
 #pragma unroll
         for (int c = 0; c < NC; ++c) { pc[c] = colp[c][2 * t_lo]; qc[c] = colp[c][2 * t_lo + 2]; }
         // two named fragment sets: set 1 is decoded while set 0 feeds the MFMAs and vice versa, so no
         // fragment is copied (a single rotating set costs ~12 v_mov per K step)
-        F4Frag a0 = decode_f4<RM>(pr.x, pr.y), a1, b0[NC], b1[NC];
+        F4Frag a0 = dec0(pr, RMc), a1, b0[NC], b1[NC];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(pc[c].x, pc[c].y);
+        for (int c = 0; c < NC; ++c) b0[c] = dec0(pc[c], CMc);
         for (int t = t_lo; t < t_hi; t += 2) {
-            a1 = decode_f4<RM>(pr.z, pr.w);
+            a1 = dec1(pr, RMc);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b1[c] = decode_f4<CM>(pc[c].z, pc[c].w);
-            mfmas_v(a0, b0, RMc, CMc);  // K step 2t   (chunk t, words 0-1)
+            for (int c = 0; c < NC; ++c) b1[c] = dec1(pc[c], CMc);
+            mfmas_v(a0, b0, RMc, CMc, P0);  // K step 2t   (chunk t, words 0-1)
             pr = rowp[2 * min(t + 2, last)];
 #pragma unroll
             for (int c = 0; c < NC; ++c) pc[c] = colp[c][2 * min(t + 2, last)];
-            a0 = decode_f4<RM>(qr.x, qr.y);
+            a0 = dec0(qr, RMc);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(qc[c].x, qc[c].y);
-            mfmas_v(a1, b1, RMc, CMc);  // K step 2t+1 (chunk t, words 2-3)
-            a1 = decode_f4<RM>(qr.z, qr.w);
+            for (int c = 0; c < NC; ++c) b0[c] = dec0(qc[c], CMc);
+            mfmas_v(a1, b1, RMc, CMc, P1);  // K step 2t+1 (chunk t, words 2-3)
+            a1 = dec1(qr, RMc);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b1[c] = decode_f4<CM>(qc[c].z, qc[c].w);
-            mfmas_v(a0, b0, RMc, CMc);  // K step 2t+2 (chunk t+1, words 0-1)
+            for (int c = 0; c < NC; ++c) b1[c] = dec1(qc[c], CMc);
+            mfmas_v(a0, b0, RMc, CMc, P0);  // K step 2t+2 (chunk t+1, words 0-1)
             qr = rowp[2 * min(t + 3, last)];
 #pragma unroll
             for (int c = 0; c < NC; ++c) qc[c] = colp[c][2 * min(t + 3, last)];
-            a0 = decode_f4<RM>(pr.x, pr.y);
+            a0 = dec0(pr, RMc);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(pc[c].x, pc[c].y);
-            mfmas_v(a1, b1, RMc, CMc);  // K step 2t+3 (chunk t+1, words 2-3)
+            for (int c = 0; c < NC; ++c) b0[c] = dec0(pc[c], CMc);
+            mfmas_v(a1, b1, RMc, CMc, P1);  // K step 2t+3 (chunk t+1, words 2-3)
         }
     };
     // wave-uniform: does the row block / do the column blocks hold a missing call (flag bit 2)?
@@ -1572,6 +1684,20 @@ __device__ __forceinline__ bool t2_routed(const uint8_t* blk_miss, int I2, int J
              blk_miss[min(2 * J2 + 1, nblk - 1)]);
 }
 
+// the 4 x 4 super-item (I4, J4) holds no missing call in its (clamped) row and column blocks
+__device__ __forceinline__ bool q_routed(const uint8_t* blk_miss, int I4, int J4, int nblk) {
+    uint8_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m |= blk_miss[min(4 * I4 + k, nblk - 1)] | blk_miss[min(4 * J4 + k, nblk - 1)];
+    return m == 0;
+}
+
+// Routing of the single-block items (route_shift 1: 2 x 2 super-items, t2_routed; 2: 4 x 4, q_routed): the item's
+// block pair runs in the super-item kernel.
+__device__ __forceinline__ bool routed_item(const uint8_t* blk_miss, int route_shift, int I, int J, int nblk) {
+    return route_shift == 2 ? q_routed(blk_miss, I >> 2, J >> 2, nblk) : t2_routed(blk_miss, I >> 1, J >> 1, nblk);
+}
+
 // One block pair per item.  WPS 2, except the segmented add+dom kernel (its int32 fold registers need 1).
 template <bool DOM, int WPS, int SEG, bool KC>
 __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
@@ -1582,13 +1708,13 @@ __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __rest
                                                         int own_lo, int own_hi, double* __restrict__ l2_acc,
                                                         double* __restrict__ l2d_acc, int* __restrict__ ws_acc, int xcd,
                                                         const uint8_t* __restrict__ blk_rep,
-                                                        const uint8_t* __restrict__ blk_miss) {
+                                                        const uint8_t* __restrict__ blk_miss, int route_shift) {
     __shared__ BandI8Lds sh;
     __shared__ float tr[32 * 33];
     const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
     if (skip_item<KC>(blk_rep, it)) return;
-    // blk_miss: the 2 x 2 kernel runs the missing-free super-items
-    if (blk_miss != nullptr && t2_routed(blk_miss, it.x >> 1, it.y >> 1, (n_snp + 31) >> 5)) return;
+    // blk_miss: a super-item kernel runs the missing-free super-items
+    if (blk_miss != nullptr && routed_item(blk_miss, route_shift, it.x, it.y, (n_snp + 31) >> 5)) return;
 #define NLDSC_BODY(DIAG_)                                                                                             \
     band_f4_body<DOM, 1, DIAG_, SEG, KC>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind,  \
                                          n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, tr)
@@ -1766,6 +1892,238 @@ __global__ void __launch_bounds__(256, 2) band_f4_t2_kernel(
                                           n_snp, l2_acc, l2d_acc, ws_acc);
 }
 
+// ---- 4 x 4 block-pair workgroups for missing-free super-items (64 x 64 SNP tiles per wave) ----
+// Measured on the 2 x 2 kernel (profiles/r03_pmc_t2_c5.json): each wave decodes two strips for the 3 products of one
+// block pair per K step, ~9 VALU per MFMA, so two waves per SIMD are bound by the VALU issue port (MFMA 42 % busy).
+// Here one wave per SIMD owns a 64 x 64 tile — row blocks 4 I4 + 2 (w >> 1) + {0, 1} x column blocks
+// 4 J4 + 2 (w & 1) + {0, 1}, four block pairs — and decodes four strips for 12 products per K step (4 VALU per
+// MFMA).  The eight strips of a super-item (four row, four column blocks; four on a diagonal super-item) go
+// global -> LDS once per workgroup through the same ring of S two-chunk stages as the 2 x 2 kernel; each feeds
+// four block pairs.  Only for super-items whose eight blocks hold no missing call (q_routed): the m products do
+// not exist, the decode is the missing-free one.  A wave with no needed block pair issues no products; a wave
+// with some computes all four and runs the epilogue of the needed ones (band edges: a few idle products).
+constexpr int Q_SLOTS = 256;  // slot tables: strip s (0-3 row blocks, 4-7 column blocks) x 32 SNPs
+template <int S>
+struct QLds {
+    uint4 stage[S][8][2][64];  // [buffer][strip][chunk of the stage][lane (i + 32 h)]
+    SnpSlot info[Q_SLOTS];
+    SnpConst cst[Q_SLOTS];
+};
+
+// one K step of a wave's four block pairs (a, b): x.x, x.h, h.x (missing-free: 2^-1-scaled h planes)
+template <bool DOM>
+__device__ __forceinline__ void q_step(const F4Frag (&A)[2], const F4Frag (&B)[2], f32x16v (&gxx)[4], f32x16v (&gxh)[4],
+                                       f32x16v (&ghx)[4]) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const F4Frag& a = A[p >> 1];
+        const F4Frag& b = B[p & 1];
+        gxx[p] = mfma_f4(a.x, b.x, gxx[p]);
+        if (DOM) {
+            gxh[p] = mfma_f4<E8M0_ONE, E8M0_HALF>(a.x, b.h, gxh[p]);
+            ghx[p] = mfma_f4<E8M0_HALF, E8M0_ONE>(a.h, b.x, ghx[p]);
+        }
+    }
+    constexpr int n_mfma = DOM ? 12 : 4;
+    constexpr int n_valu = 4 * (DOM ? 12 : 8);  // the next step's four decodes
+#pragma unroll
+    for (int m = 0; m < n_mfma; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, (n_valu + n_mfma - 1) / n_mfma, 0);
+    }
+}
+
+template <bool DOM, int S, bool KC>
+__global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
+    const uint32_t* __restrict__ geno, int pitch_words, int n_it, const SnpConst* __restrict__ cst,
+    const int4* __restrict__ items, const int2* __restrict__ rows, int nblk, const double* __restrict__ pos,
+    const int* __restrict__ Lw, const int* __restrict__ Rw, const uint8_t* __restrict__ sflags, int n_snp,
+    double ld_wind, double n_org, double rsq_thr, int own_lo, int own_hi, double* __restrict__ l2_acc,
+    double* __restrict__ l2d_acc, int* __restrict__ ws_acc, int xcd, const uint8_t* __restrict__ blk_rep,
+    const uint8_t* __restrict__ blk_miss) {
+    static_assert(S >= 2, "ring of at least two stages");
+    __shared__ QLds<S> sh;
+    const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
+    const int I4 = it.x, J4 = it.y;
+    const bool dsup = I4 == J4;  // diagonal super-item: the column strips are the row strips
+    auto strip_blk = [&](int s) { return s < 4 ? 4 * I4 + s : 4 * J4 + s - 4; };  // (may be >= nblk: no SNPs)
+    if (KC || blk_rep != nullptr) {  // a super-item with a replayed SNP runs whole in the KC launch
+        bool rep = false;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) rep |= blk_rep[min(strip_blk(s), nblk - 1)] != 0;
+        if (KC ? !rep : rep) return;
+    }
+    if (!q_routed(blk_miss, I4, J4, nblk)) return;  // the single-block kernel's
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
+    {
+        const int b = strip_blk(tid >> 5);
+        const int g = b * 32 + (tid & 31);
+        SnpSlot si;
+        si.g = g;
+        if (g < n_snp) {
+            si.pos = pos[g]; si.L = Lw[g]; si.R = Rw[g]; si.fl = sflags[g];
+        } else {
+            si.pos = 0.0; si.L = -1; si.R = -2; si.fl = 0;
+        }
+        sh.info[tid] = si;
+        sh.cst[tid] = b < nblk ? cst[g] : SnpConst{};
+    }
+    // this wave's block pairs p = 2a + b: row block 4 I4 + 2 (w >> 1) + a, column block 4 J4 + 2 (w & 1) + b
+    const int rs = 2 * (w >> 1), cs = dsup ? 2 * (w & 1) : 4 + 2 * (w & 1);  // first row / column strip
+    bool need[4];
+    bool any = false;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int rb = strip_blk(rs + (p >> 1)), cb = 4 * J4 + 2 * (w & 1) + (p & 1);
+        need[p] = rb < nblk && cb < nblk;
+        if (need[p]) {
+            const int2 r = rows[rb];
+            need[p] = cb - rb >= r.x && cb - rb <= r.y;
+        }
+        any |= need[p];
+    }
+    // loads: wave w streams strips 2w, 2w + 1 (none for waves 2, 3 of a diagonal super-item)
+    const bool loads = !(dsup && w >= 2);
+    const uint4* src0 = reinterpret_cast<const uint4*>(
+        geno + (size_t)(min(strip_blk(2 * w), nblk - 1) * 32 + i) * (size_t)pitch_words) + h;
+    const uint4* src1 = reinterpret_cast<const uint4*>(
+        geno + (size_t)(min(strip_blk(2 * w + 1), nblk - 1) * 32 + i) * (size_t)pitch_words) + h;
+    const int n_st = n_it >> 1;
+    auto issue = [&](int t) {
+        const int tc = min(t, n_st - 1);
+        if (loads) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const uint32_t dst = __builtin_amdgcn_readfirstlane(
+                        (uint32_t)(size_t)(__attribute__((address_space(3))) void*)&sh.stage[t % S][2 * w + k][c][0]);
+                    uint32_t keep;
+                    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                                 "s_mov_b32 m0, %0"
+                                 : "=&s"(keep)
+                                 : "v"((k ? src1 : src0) + 4 * tc + 2 * c), "s"(dst)
+                                 : "memory");
+                }
+        }
+    };
+    __syncthreads();  // slot tables written; nothing in flight yet
+#pragma unroll
+    for (int t = 0; t < S; ++t) issue(t);
+
+    f32x16v gxx[4], gxh[4], ghx[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) gxx[p] = gxh[p] = ghx[p] = f32x16v{};
+    // as the 2 x 2 kernel's ring: stage t read into registers one stage ahead, S - 1 stages in flight
+    auto read_stage = [&](int t, uint4 (&ra)[2][2], uint4 (&rb)[2][2]) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                ra[k][c] = sh.stage[t % S][rs + k][c][lane];
+                rb[k][c] = sh.stage[t % S][cs + k][c][lane];
+            }
+    };
+    auto kloop = [&](auto ACTc) {
+        constexpr bool ACT = decltype(ACTc)::value;
+        uint4 ra[2][2], rb[2][2];
+        wait_vmcnt<4 * (S - 1)>();  // stage 0 landed (this wave's loads)
+        __builtin_amdgcn_s_barrier();  // every wave's
+        asm volatile("" ::: "memory");
+        if constexpr (ACT) read_stage(0, ra, rb);
+        for (int t = 0; t < n_st; ++t) {
+            wait_vmcnt<4 * (S - 2)>();  // this wave's loads of stage t + 1 have landed
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // its reads of stage t are in registers
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            issue(t + S);
+            if constexpr (ACT) {
+                uint4 na[2][2], nb[2][2];
+                read_stage(t + 1, na, nb);  // past the last stage: a buffer of surplus bytes, never used
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    F4Frag A[2], B[2];
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        A[k] = decode_f4<false>(ra[k][c].x, ra[k][c].y);
+                        B[k] = decode_f4<false>(rb[k][c].x, rb[k][c].y);
+                    }
+                    q_step<DOM>(A, B, gxx, gxh, ghx);
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        A[k] = decode_f4<false>(ra[k][c].z, ra[k][c].w);
+                        B[k] = decode_f4<false>(rb[k][c].z, rb[k][c].w);
+                    }
+                    q_step<DOM>(A, B, gxx, gxh, ghx);
+                }
+#pragma unroll
+                for (int k = 0; k < 2; ++k)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) { ra[k][c] = na[k][c]; rb[k][c] = nb[k][c]; }
+            }
+        }
+    };
+    if (any) kloop(std::true_type{});
+    else kloop(std::false_type{});
+    wait_vmcnt<0>();  // the tail's surplus loads
+    if (!any) return;  // no barrier follows
+    const f32x16v z = {};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        if (!need[p]) continue;
+        const int rb = strip_blk(rs + (p >> 1)), cb = 4 * J4 + 2 * (w & 1) + (p & 1);
+        // (missing-free: the m products are 0, as in the single-block kernel's RM = CM = false loop)
+        pair_epilogue<DOM, f32x16v, true, KC>(sh.info, sh.cst, 32 * (rs + (p >> 1)), 32 * (cs + (p & 1)), rb == cb, i,
+                                              h, gxx[p], z, z, z, gxh[p], z, ghx[p], z, ld_wind, n_org, rsq_thr, n_org,
+                                              own_lo, own_hi, n_snp, l2_acc, l2d_acc, ws_acc);
+    }
+}
+
+// ---- routed single-block items, compacted (order kept) ----
+// With super-item routing, the single-block kernel runs only the items no super-item kernel takes.  Listing them
+// apart (instead of every item returning at once when routed) sizes its launches — the round launches, the K-split
+// tail — by the work it really has: missing-free data leaves it none, where round launches of all-routed items were
+// thousands of empty launches.  Three passes over 1024-item chunks: per-chunk counts, their exclusive scan (one
+// workgroup; meta_out = the total), the scatter.
+constexpr int COMPACT_CHUNK = 1024;
+__device__ __forceinline__ bool keep_item(const int4* items, int t, const uint8_t* blk_miss, int route_shift, int nblk) {
+    const int4 it = items[t];
+    return !routed_item(blk_miss, route_shift, it.x, it.y, nblk);
+}
+
+__global__ void __launch_bounds__(1024) compact_count_kernel(const int4* __restrict__ items, int n_items,
+                                                             const uint8_t* __restrict__ blk_miss, int route_shift,
+                                                             int nblk, int* __restrict__ chunk_counts) {
+    const int t = blockIdx.x * COMPACT_CHUNK + threadIdx.x;
+    const int keep = t < n_items && keep_item(items, t, blk_miss, route_shift, nblk);
+    const int n = __syncthreads_count(keep);
+    if (threadIdx.x == 0) chunk_counts[blockIdx.x] = n;
+}
+
+__global__ void __launch_bounds__(1024) compact_scatter_kernel(const int4* __restrict__ items, int n_items,
+                                                               const uint8_t* __restrict__ blk_miss, int route_shift,
+                                                               int nblk, const int* __restrict__ chunk_offsets,
+                                                               int4* __restrict__ out) {
+    __shared__ int wave_base[COMPACT_CHUNK / 64];
+    const int t = blockIdx.x * COMPACT_CHUNK + threadIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const bool keep = t < n_items && keep_item(items, t, blk_miss, route_shift, nblk);
+    const unsigned long long ballot = __ballot(keep);
+    const int before = __popcll(ballot & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_base[wv] = __popcll(ballot);
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive scan of the 16 wave counts
+        int run = 0;
+        for (int k = 0; k < COMPACT_CHUNK / 64; ++k) {
+            const int c = wave_base[k];
+            wave_base[k] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    if (keep) out[chunk_offsets[blockIdx.x] + wave_base[wv] + before] = items[t];
+}
+
 // Matrix-core work the band kernels issued (32x32 block products over the whole K range), counted per work item
 // exactly as each kernel decides it: kind 2 fp4 single-block items (mfmas_v: 1 + cm + rm + rm cm + dom (2 + rm +
 // cm), the transposed products skipped on diagonal blocks; items the 2 x 2 kernel takes skipped when `routed`),
@@ -1774,14 +2132,17 @@ __global__ void __launch_bounds__(256, 2) band_f4_t2_kernel(
 // rm / cm = blk_miss of the row / column block.  out[0] += products.
 __global__ void issued_products_kernel(const int4* __restrict__ items, int n_items, const int4* __restrict__ items2,
                                        int n_items2, const int2* __restrict__ rows, const uint8_t* __restrict__ blk_miss,
-                                       int nblk, int kind, int dom, int routed, unsigned long long* __restrict__ out) {
+                                       int nblk, int kind, int dom, int routed, int route_shift,
+                                       unsigned long long* __restrict__ out) {
+    // routed bit 0: single items the routing sends to a super-item kernel are not counted here (an uncompacted
+    // list); bit 1: super-items count only when routed to their kernel
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long n = 0;
     if (t < n_items) {
         const int4 it = items[t];
         const bool diag = it.x == it.y;
         if (kind == 2) {
-            if (!(routed && t2_routed(blk_miss, it.x >> 1, it.y >> 1, nblk))) {
+            if (!((routed & 1) && routed_item(blk_miss, route_shift, it.x, it.y, nblk))) {
                 const int rm = blk_miss[it.x] != 0, cm = blk_miss[it.y] != 0, nd = !diag;
                 n = 1 + cm + rm * nd + rm * cm + (dom ? 1 + nd + rm + cm * nd : 0);
             }
@@ -1790,9 +2151,22 @@ __global__ void issued_products_kernel(const int4* __restrict__ items, int n_ite
         } else {
             for (int b = 0; b < it.z; ++b) n += 1 + (dom ? (it.y + b == it.x ? 1 : 2) : 0);
         }
+    } else if (items2 != nullptr && t < n_items + n_items2 && route_shift == 2) {
+        // quad super-items (missing-free): a wave with any needed block pair issues all four pairs' products
+        const int4 it = items2[t - n_items];
+        if (!(routed & 2) || q_routed(blk_miss, it.x, it.y, nblk)) {
+            for (int w = 0; w < 4; ++w) {
+                bool any = false;
+                for (int p = 0; p < 4; ++p) {
+                    const int rb = 4 * it.x + 2 * (w >> 1) + (p >> 1), cb = 4 * it.y + 2 * (w & 1) + (p & 1);
+                    any |= rb < nblk && cb < nblk && cb - rb >= rows[rb].x && cb - rb <= rows[rb].y;
+                }
+                n += any ? 4 * (dom ? 3 : 1) : 0;
+            }
+        }
     } else if (items2 != nullptr && t < n_items + n_items2) {
         const int4 it = items2[t - n_items];
-        if (!(routed && !t2_routed(blk_miss, it.x, it.y, nblk))) {
+        if (!((routed & 2) && !t2_routed(blk_miss, it.x, it.y, nblk))) {
             for (int w = 0; w < 4; ++w) {
                 const int rb = 2 * it.x + (w >> 1), cb = 2 * it.y + (w & 1);
                 if (rb >= nblk || cb >= nblk || cb - rb < rows[rb].x || cb - rb > rows[rb].y) continue;
@@ -1805,25 +2179,22 @@ __global__ void issued_products_kernel(const int4* __restrict__ items, int n_ite
     if ((threadIdx.x & 63) == 0 && n) atomicAdd(out, n);
 }
 
-// blk_miss[b] = 1 if block b holds a SNP with a missing call (flag bit 2) — zeroed before
-__global__ void block_missing_kernel(const uint8_t* __restrict__ sflags, int n_snp, uint8_t* __restrict__ blk_miss) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < n_snp && (sflags[j] & 4)) blk_miss[j >> 5] = 1;
-}
 
 // super-item rows: per row super-block I2 (row blocks 2 I2, 2 I2 + 1) the super-column offsets [d0, d1] covering both
 // blocks' needed columns; meta[0] = max d1 + 1, meta[2] = diagonal super-items (plan_count / scan / emit then run on
 // these rows as on the single-block ones)
-__global__ void plan_rows2_kernel(const int2* __restrict__ rows, int nblk, int2* __restrict__ rows2,
+// (shift 1: 2 x 2 super-items of the 2 x 2 kernel; shift 2: 4 x 4 super-items of the quad kernel)
+__global__ void plan_rows2_kernel(const int2* __restrict__ rows, int nblk, int shift, int2* __restrict__ rows2,
                                   int* __restrict__ meta) {
-    const int I2 = blockIdx.x * blockDim.x + threadIdx.x, nblk2 = (nblk + 1) / 2;
+    const int F = 1 << shift;
+    const int I2 = blockIdx.x * blockDim.x + threadIdx.x, nblk2 = (nblk + F - 1) >> shift;
     if (I2 >= nblk2) return;
     int lo = INT_MAX, hi = -1;
-    for (int b = 2 * I2; b < min(nblk, 2 * I2 + 2); ++b) {
+    for (int b = F * I2; b < min(nblk, F * I2 + F); ++b) {
         const int2 r = rows[b];
         if (r.x <= r.y) { lo = min(lo, b + r.x); hi = max(hi, b + r.y); }
     }
-    const int2 r2 = hi >= 0 ? make_int2((lo >> 1) - I2, (hi >> 1) - I2) : make_int2(1, 0);
+    const int2 r2 = hi >= 0 ? make_int2((lo >> shift) - I2, (hi >> shift) - I2) : make_int2(1, 0);
     rows2[I2] = r2;
     if (r2.x <= r2.y) {
         atomicMax(&meta[0], r2.y + 1);
@@ -1844,13 +2215,13 @@ __global__ void __launch_bounds__(64, 2) band_f4_part_kernel(const uint32_t* __r
                                                            const int* __restrict__ Rw,
                                                            const uint8_t* __restrict__ sflags, int n_snp, int P,
                                                            float* __restrict__ gram,
-                                                           const uint8_t* __restrict__ blk_miss) {
+                                                           const uint8_t* __restrict__ blk_miss, int route_shift) {
     __shared__ BandI8Lds sh;
     __shared__ float tr[32 * 33];
     const int u = xcd_slot(blockIdx.x, gridDim.x), item = u / P, piece = u % P;
     const int4 it = items[item];
-    // blk_miss: the 2 x 2 kernel runs the missing-free super-items (band_f4_epi_kernel skips the same items)
-    if (blk_miss != nullptr && t2_routed(blk_miss, it.x >> 1, it.y >> 1, (n_snp + 31) >> 5)) return;
+    // blk_miss: a super-item kernel runs the missing-free super-items (band_f4_epi_kernel skips the same items)
+    if (blk_miss != nullptr && routed_item(blk_miss, route_shift, it.x, it.y, (n_snp + 31) >> 5)) return;
     const int t_lo = (int)(((long long)piece * n_it / P) & ~1LL);
     const int t_hi = piece == P - 1 ? n_it : (int)(((long long)(piece + 1) * n_it / P) & ~1LL);
     float* part = gram + (size_t)u * 8192;
@@ -1872,12 +2243,12 @@ __global__ void __launch_bounds__(64, 2) band_f4_epi_kernel(const SnpConst* __re
                                                           double* __restrict__ l2d_acc, int* __restrict__ ws_acc,
                                                           const uint8_t* __restrict__ blk_rep, int P,
                                                           const float* __restrict__ gram,
-                                                          const uint8_t* __restrict__ blk_miss) {
+                                                          const uint8_t* __restrict__ blk_miss, int route_shift) {
     __shared__ BandI8Lds sh;
     __shared__ float tr[32 * 33];
     const int4 it = items[blockIdx.x];
     if (skip_item<KC>(blk_rep, it)) return;
-    if (blk_miss != nullptr && t2_routed(blk_miss, it.x >> 1, it.y >> 1, (n_snp + 31) >> 5)) return;
+    if (blk_miss != nullptr && routed_item(blk_miss, route_shift, it.x, it.y, (n_snp + 31) >> 5)) return;
     const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
     const int I = it.x, J = it.y;
     const bool diag = I == J;
@@ -2087,6 +2458,23 @@ hipError_t launch_reference_residuals(const uint8_t* img, int row_bytes, int n_o
     return hipGetLastError();
 }
 
+hipError_t launch_row_missing(const uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes,
+                              uint32_t keep_compat, uint32_t keep_strict, uint8_t* row_miss, hipStream_t st) {
+    if (n_snp <= 0) return hipSuccess;
+    hipLaunchKernelGGL(row_missing_kernel, dim3(n_snp), dim3(256), 0, st, img, last, n_snp, nb, row_bytes, keep_compat,
+                       keep_strict, row_miss);
+    return hipGetLastError();
+}
+
+hipError_t launch_block_missing_rows(const uint8_t* row_miss, int n_snp, int order, uint8_t* blk_miss,
+                                     hipStream_t st) {
+    const int nblk = (n_snp + 31) / 32;
+    if (nblk <= 0) return hipSuccess;
+    hipLaunchKernelGGL(block_missing_rows_kernel, dim3((nblk + 255) / 256), dim3(256), 0, st, row_miss, n_snp, order,
+                       blk_miss);
+    return hipGetLastError();
+}
+
 hipError_t launch_orient_rows(uint8_t* img, uint8_t* last, int n_snp, int row_bytes, uint8_t* flip, hipStream_t st) {
     if (n_snp <= 0) return hipSuccess;
     hipLaunchKernelGGL(orient_rows_kernel, dim3(n_snp), dim3(256), 0, st, img, last, n_snp, row_bytes, flip);
@@ -2151,27 +2539,20 @@ hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* gen
     return hipGetLastError();
 }
 
-hipError_t launch_plan_super(int n, const int2* rows, int2* rows2, int* counts2, int* meta2, hipStream_t st) {
-    const int nblk = (n + 31) / 32, nblk2 = (nblk + 1) / 2;
+hipError_t launch_plan_super(int n, const int2* rows, int2* rows2, int* counts2, int* meta2, int shift, hipStream_t st) {
+    const int nblk = (n + 31) / 32, nblk2 = (nblk + (1 << shift) - 1) >> shift;
     hipError_t e = hipMemsetAsync(meta2, 0, 4 * sizeof(int), st);
     if (e != hipSuccess || n <= 0) return e;
-    hipLaunchKernelGGL(plan_rows2_kernel, dim3((nblk2 + 255) / 256), dim3(256), 0, st, rows, nblk, rows2, meta2);
+    hipLaunchKernelGGL(plan_rows2_kernel, dim3((nblk2 + 255) / 256), dim3(256), 0, st, rows, nblk, shift, rows2, meta2);
     hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, counts2);
     hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts2, nblk2, meta2);
     return hipGetLastError();
 }
 
-hipError_t launch_block_missing(const uint8_t* sflags, int n_snp, uint8_t* blk_miss, hipStream_t st) {
-    if (n_snp <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(blk_miss, 0, (size_t)(n_snp + 31) / 32, st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(block_missing_kernel, dim3((n_snp + 255) / 256), dim3(256), 0, st, sflags, n_snp, blk_miss);
-    return hipGetLastError();
-}
 
 hipError_t launch_plan_emit_super(int n, const int2* rows2, const int* meta2, const int* offsets2, int4* items2,
-                                  hipStream_t st) {
-    const int nblk2 = ((n + 31) / 32 + 1) / 2;
+                                  int shift, hipStream_t st) {
+    const int nblk2 = ((n + 31) / 32 + (1 << shift) - 1) >> shift;
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, offsets2, items2);
     return hipGetLastError();
@@ -2195,24 +2576,42 @@ hipError_t launch_band_f4_t2(bool dom, int n_items2, const uint32_t* geno, int p
     return hipGetLastError();
 }
 
+hipError_t launch_band_f4_q(bool dom, int n_items4, const uint32_t* geno, int pitch_words, int n_it,
+                            const SnpConst* cst, const int4* items4, const int2* rows, int nblk, const double* pos,
+                            const int* Lw, const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind,
+                            double n_org, double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
+                            int* ws_acc, bool xcd, const uint8_t* blk_rep, const uint8_t* blk_miss, int which,
+                            hipStream_t st) {
+    if (n_items4 <= 0) return hipSuccess;
+    if (n_it > F4_SEG_CHUNKS || n_it < 2 || (n_it & 1) || blk_miss == nullptr) return hipErrorInvalidValue;
+#define NLDSC_BAND(DOM_, KC_)                                                                                       \
+    hipLaunchKernelGGL((band_f4_q_kernel<DOM_, Q_STAGES, KC_>), dim3(n_items4), dim3(256), 0, st, geno,             \
+                       pitch_words, n_it, cst, items4, rows, nblk, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,      \
+                       rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss)
+    if (which & 1) { if (dom) NLDSC_BAND(true, false); else NLDSC_BAND(false, false); }
+    if (blk_rep && (which & 2)) { if (dom) NLDSC_BAND(true, true); else NLDSC_BAND(false, true); }
+#undef NLDSC_BAND
+    return hipGetLastError();
+}
+
 hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                                 const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                                 const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr,
                                 int own_lo, int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc,
                                 const uint8_t* blk_rep, float* gram, int which, hipStream_t st,
-                                const uint8_t* blk_miss) {
+                                const uint8_t* blk_miss, int route_shift) {
     if (n_items <= 0) return hipSuccess;
     if (n_it > F4_SEG_CHUNKS || P < 1 || 2 * P > n_it) return hipErrorInvalidValue;
     const dim3 grid_p((unsigned)n_items * (unsigned)P);
     if (!(which & 1)) goto kc;  // the partial tiles of every item come from the main launch
     if (dom) hipLaunchKernelGGL((band_f4_part_kernel<true>), grid_p, dim3(64), 0, st, geno, pitch_words, n_it, cst,
-                                items, pos, Lw, Rw, sflags, n_snp, P, gram, blk_miss);
+                                items, pos, Lw, Rw, sflags, n_snp, P, gram, blk_miss, route_shift);
     else hipLaunchKernelGGL((band_f4_part_kernel<false>), grid_p, dim3(64), 0, st, geno, pitch_words, n_it, cst,
-                            items, pos, Lw, Rw, sflags, n_snp, P, gram, blk_miss);
+                            items, pos, Lw, Rw, sflags, n_snp, P, gram, blk_miss, route_shift);
 #define NLDSC_EPI(DOM_, KC_)                                                                                        \
     hipLaunchKernelGGL((band_f4_epi_kernel<DOM_, KC_>), dim3(n_items), dim3(64), 0, st, cst, items, pos, Lw, Rw,    \
                        sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, blk_rep, P, gram, \
-                       blk_miss)
+                       blk_miss, route_shift)
     if (dom) NLDSC_EPI(true, false); else NLDSC_EPI(false, false);
 kc:
     if (blk_rep && (which & 2)) { if (dom) NLDSC_EPI(true, true); else NLDSC_EPI(false, true); }
@@ -2224,7 +2623,8 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
-                          int which, hipStream_t st, const uint8_t* blk_miss, int round_items) {
+                          int which, hipStream_t st, const uint8_t* blk_miss, int round_items, int route_shift,
+                          hipStream_t st2) {
     if (n_items <= 0) return hipSuccess;
     if (max_nc != 1) return hipErrorInvalidValue;  // single block-pair items
     if (blk_miss != nullptr && n_it > F4_SEG_CHUNKS) return hipErrorInvalidValue;  // routing: unsegmented rows only
@@ -2232,10 +2632,11 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
     // not the KC launch (items holding a replayed rare variant: few, the others return at once)
     int chunk = round_items > 0 ? round_items : n_items;
 #define NLDSC_BAND(DOM_, WPS_, SEG_, KC_)                                                                           \
-    for (int o = 0; o < n_items; o += chunk)                                                                      \
-    hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_, KC_>), dim3(std::min(chunk, n_items - o)), dim3(64), 0, st, geno, pitch_words,  \
+    for (int o = 0, r = 0; o < n_items; o += chunk, ++r)                                                          \
+    hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_, KC_>), dim3(std::min(chunk, n_items - o)), dim3(64), 0,    \
+                       (st2 != nullptr && (r & 1)) ? st2 : st, geno, pitch_words,                                   \
                        n_it, cst, items + o, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi,       \
-                       l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss)
+                       l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss, route_shift)
 #define NLDSC_PICK(KC_)                                                                                              \
     if (n_it > F4_SEG_CHUNKS) { if (dom) NLDSC_BAND(true, 1, F4_SEG_CHUNKS, KC_); else NLDSC_BAND(false, 2, F4_SEG_CHUNKS, KC_); } \
     else if (dom) NLDSC_BAND(true, 2, 0, KC_);                                                                       \
@@ -2243,6 +2644,7 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
     // segmented kernel: the add+dom variant needs more than 256 registers (2 waves / SIMD would spill)
     if (which & 1) { NLDSC_PICK(false); }
     chunk = n_items;
+    st2 = nullptr;
     if (blk_rep && (which & 2)) { NLDSC_PICK(true); }
 #undef NLDSC_PICK
 #undef NLDSC_BAND
@@ -2259,12 +2661,24 @@ hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2
 }
 
 hipError_t launch_issued_products(const int4* items, int n_items, const int4* items2, int n_items2, const int2* rows,
-                                 const uint8_t* blk_miss, int nblk, int kind, bool dom, bool routed,
+                                 const uint8_t* blk_miss, int nblk, int kind, bool dom, int routed, int route_shift,
                                  unsigned long long* out, hipStream_t st) {
     const int n = n_items + (items2 != nullptr ? n_items2 : 0);
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(issued_products_kernel, dim3((n + 255) / 256), dim3(256), 0, st, items, n_items, items2,
-                       n_items2, rows, blk_miss, nblk, kind, dom ? 1 : 0, routed ? 1 : 0, out);
+                       n_items2, rows, blk_miss, nblk, kind, dom ? 1 : 0, routed, route_shift, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact_items(const int4* items, int n_items, const uint8_t* blk_miss, int route_shift, int nblk,
+                                int* chunk_counts, int* total, int4* out, hipStream_t st) {
+    const int n_chunks = (n_items + COMPACT_CHUNK - 1) / COMPACT_CHUNK;
+    if (n_items <= 0) return hipMemsetAsync(total, 0, sizeof(int), st);
+    hipLaunchKernelGGL(compact_count_kernel, dim3(n_chunks), dim3(COMPACT_CHUNK), 0, st, items, n_items, blk_miss,
+                       route_shift, nblk, chunk_counts);
+    hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(1024), 0, st, chunk_counts, n_chunks, total);
+    hipLaunchKernelGGL(compact_scatter_kernel, dim3(n_chunks), dim3(COMPACT_CHUNK), 0, st, items, n_items, blk_miss,
+                       route_shift, nblk, chunk_counts, out);
     return hipGetLastError();
 }
 

@@ -14,7 +14,8 @@ import numpy as np
 from . import _lib
 
 # nldsc_engine_band_kernel codes (include/nldsc_ld.h NLDSC_BAND_*)
-BAND_KERNELS = {0: "f32", 1: "i8", 2: "f4", 3: "f4_seg", 4: "f4_ksplit", 5: "f4_2x2", 6: "f4_routed"}
+BAND_KERNELS = {0: "f32", 1: "i8", 2: "f4", 3: "f4_seg", 4: "f4_ksplit", 5: "f4_2x2", 6: "f4_routed",
+                7: "f4_quad"}
 
 
 class Engine:

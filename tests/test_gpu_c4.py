@@ -106,7 +106,7 @@ def test_c4_genome_one_rank_vs_oracle_and_truth(c4):
             np.testing.assert_array_equal(sub[k], truth[k], err_msg=f"chr{c} {k}")
         # every SNP: C4-sized windows, finite scores, L2 >= 1 - a rounding margin of the adjusted r^2
         assert np.isfinite(got["l2"]).all() and np.isfinite(got["l2d"]).all()
-        assert (got["l2_ws"] > 100).all() and got["l2_ws"].max() > 250, c
+        assert (got["l2_ws"] > 100).all() and got["l2_ws"].max() >= min(250, m - 1), c
         assert (got["l2d_ws"] <= got["l2_ws"]).all() and (got["l2d_wse"] <= got["l2d_ws"]).all()
         progress(f"c4 chr{c}: {m} SNPs checked")
     record("c4_genome", report)

@@ -591,22 +591,57 @@ def test_missing_free_blocks_skip_m_products(engine, N):
                                       maf=(0.0, 0.0)), label=f"missing-free blocks N={N}")
 
 
-@pytest.mark.parametrize("t2", ["0", "1"])
+@pytest.mark.parametrize("strict", [False, True])
+@pytest.mark.parametrize("t2", ["1", "3"])
+def test_routing_reads_this_runs_individual_slots(engine, strict, t2):
+    """The routing predicate (blk_miss, from the load-time per-row missing flags of both sample orders) must equal the
+    band kernels' own (a missing call among this run's individual slots): a missing-free super-item runs the
+    missing-free decode.  N % 4 = 3: a 01 call in the last byte's low pair (PLINK's sample 1000) is an individual for
+    the PLINK order only, one in the high pair (padding for PLINK) for the reference's order only; everything else
+    is missing-free.  Bitwise the single-block kernel's results and the fp64 truth in both orders."""
+    from nldsc_amd import _lib, synth
+    from nldsc_amd.engine import Engine
+    N, M = 1003, 640
+    spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=6.0, seed=91, missing=0.0)
+    rows = synth.pack_bed_rows(synth.genotypes(spec)).copy()
+    nb = rows.shape[1]
+    rows[5, nb - 1] = (rows[5, nb - 1] & 0xFC) | 0x01     # PLINK sample 1000 missing (low pair)
+    rows[200, nb - 1] = (rows[200, nb - 1] & 0x3F) | 0x40  # the padding pair (high) reads 01
+    pos = synth.positions_cm(spec)
+    flags = MODES["f4"] | _lib_flag("FLAG_EXACT_RARE") | (_lib.FLAG_STRICT_PLINK_ORDER if strict else 0)
+    args = (1.0, 0.01, 1e-5, 1.0 / M, pos)
+
+    def fresh():
+        with Engine(0) as e:
+            e.load_bed_bytes(synth.bed_bytes(rows), M, N)
+            return e.run(*args, flags=flags)
+    got = _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", t2, fresh))
+    ref = _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", "0", fresh))
+    for k in got:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    exp = O.run_f64(rows, N, *args, strict=strict)
+    assert_ld_close(got, exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
+                                       maf=(0.0, 0.0)), label=f"routing strict={strict}")
+
+
+@pytest.mark.parametrize("t2", ["0", "1", "3"])
 @pytest.mark.parametrize("dom", [True, False])
 def test_issued_products_counted_per_item(engine, t2, dom):
     """flop_issued (the bench's mfma_pipe_frac) counts what each kernel issues per work item: fp4 single-block items
     1 + cm + rm + rm cm + dom (2 + rm + cm) 32x32 block products over all K, less the transposed ones of diagonal
     blocks; items the routing sends to the 2 x 2 kernel (missing-free super-items) 1 + 2 dom; int8 4 + dom (2 + 2
-    !diag); fp32 1 + dom (2 - diag).  Blocks alternate between missing-free, one missing call and 2 % missing."""
+    !diag); fp32 1 + dom (2 - diag); with the quad kernel ($NLDSC_T2=3) every wave of a routed 4 x 4 super-item that
+    needs one of its four block pairs issues all four (4 (1 + 2 dom)).  Groups of four blocks alternate between
+    missing-free, one missing call and 2 % missing."""
     from nldsc_amd import _lib, synth
     from nldsc_amd.engine import Engine
     N, M = 1003, 800
     spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=8.0, seed=77, missing=0.02)
     g = synth.genotypes(spec)
     clean = synth.genotypes(synth.SynthSpec(n_org=N, n_snp=M, length_cm=8.0, seed=77, missing=0.0))
-    blk = np.arange(M) // 32
-    g[blk % 3 != 2] = clean[blk % 3 != 2]
-    g[(blk % 3 == 1) & (np.arange(M) % 32 == 5), N // 2] = -1
+    grp = np.arange(M) // 128
+    g[grp % 3 != 2] = clean[grp % 3 != 2]
+    g[(grp % 3 == 1) & (np.arange(M) % 128 == 5), N // 2] = -1
     rows = synth.pack_bed_rows(g)
     pos = synth.positions_cm(spec)
     nblk = (M + 31) // 32
@@ -615,13 +650,24 @@ def test_issued_products_counted_per_item(engine, t2, dom):
     I, J = items[:, 0], items[:, 1]
     rm, cm, nd = miss[I], miss[J], (I != J).astype(int)
     f4 = 1 + cm + rm * nd + rm * cm + (1 + nd + rm + cm * nd if dom else 0)
+    mb = lambda b: miss[np.minimum(b, nblk - 1)]  # noqa: E731
     if t2 == "1":  # super-items whose four (clamped) blocks are missing-free run in the 2 x 2 kernel
-        mb = lambda b: miss[np.minimum(b, nblk - 1)]  # noqa: E731
         routed = ~(mb(I & ~1) | mb((I & ~1) + 1) | mb(J & ~1) | mb((J & ~1) + 1)).astype(bool)
         assert routed.any() and not routed.all()
         f4 = np.where(routed, 1 + (2 if dom else 0), f4)
-    expect = {"f4": int(f4.sum()), "i8": int((4 + (2 + 2 * nd if dom else 0)).sum()),
-              "f32": int((1 + (2 - (1 - nd) if dom else 0)).sum())}
+    if t2 == "3":  # 4 x 4 super-items whose eight blocks are missing-free run in the quad kernel
+        routed = ~np.any([mb(4 * (I >> 2) + k) | mb(4 * (J >> 2) + k) for k in range(4)], axis=0).astype(bool)
+        assert routed.any() and not routed.all()
+        needed = set(zip(I.tolist(), J.tolist()))
+        quad = 0
+        for I4, J4 in sorted(set(zip((I[routed] >> 2).tolist(), (J[routed] >> 2).tolist()))):
+            for w in range(4):
+                pairs = [(4 * I4 + 2 * (w >> 1) + a, 4 * J4 + 2 * (w & 1) + b) for a in (0, 1) for b in (0, 1)]
+                quad += 4 * (3 if dom else 1) if any(p in needed for p in pairs) else 0
+        f4 = np.append(np.where(routed, 0, f4), quad)
+    i8 = 4 + (2 + 2 * nd if dom else 0 * nd)
+    f32 = 1 + (1 + nd if dom else 0 * nd)
+    expect = {"f4": int(f4.sum()), "i8": int(i8.sum()), "f32": int(f32.sum())}
     row_bytes = -(-((N + 3) // 4) // 64) * 64
     flags = _lib_flag("FLAG_EXACT_RARE") | (0 if dom else _lib_flag("FLAG_ADDITIVE_ONLY"))
 
@@ -767,10 +813,16 @@ T2_CASES = {
     "rare_replay": (50_001, 400, None, 1.0, None, True, None, True),
     # missing calls in every third block only: the routed default splits the band between both kernels
     "mixed_blocks": (5003, 1300, 8.0, 1.0, "mixed", True, None, False),
+    # ... in every third group of four blocks: the quad kernel's 4 x 4 super-items beside single-block items
+    "mixed_groups": (5003, 1700, 8.0, 1.0, "mixed4", True, None, False),
+    # missing-free: a block count not a multiple of four (clamped strips), an owned range, additive only
+    "missing_free_odd": (4099, 1090, 12.0, 0.5, 0.0, True, None, False),
+    "missing_free_owned": (3001, 1400, 10.0, 1.0, 0.0, True, (333, 1001), False),
+    "missing_free_additive": (4096, 1025, 8.0, 1.0, 0.0, False, None, False),
 }
 
 
-@pytest.mark.parametrize("t2", ["2", "1"])
+@pytest.mark.parametrize("t2", ["2", "1", "3"])
 @pytest.mark.parametrize("case", sorted(T2_CASES))
 def test_2x2_workgroups_bitwise_single_block(engine, case, t2):
     """The 2 x 2 block-pair workgroups (LDS-shared strips) — for every super-item ($NLDSC_T2=2) or, the default,
@@ -786,12 +838,13 @@ def test_2x2_workgroups_bitwise_single_block(engine, case, t2):
         M = len(pos)
     else:
         spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=length, seed=N + M,
-                               missing=0.0 if missing == "mixed" else missing)
+                               missing=0.0 if isinstance(missing, str) else missing)
         g = synth.genotypes(spec)
-        if missing == "mixed":
+        if isinstance(missing, str):  # "mixed": every third block; "mixed4": every third group of four blocks
             rng = np.random.default_rng(M)
-            for b in range(0, (M + 31) // 32, 3):
-                j = 32 * b + rng.integers(0, min(32, M - 32 * b))
+            span = 128 if missing == "mixed4" else 32
+            for b in range(0, (M + span - 1) // span, 3):
+                j = span * b + rng.integers(0, min(span, M - span * b))
                 g[j, rng.choice(N, 20, replace=False)] = -1
         rows = synth.pack_bed_rows(g)
         pos = synth.positions_cm(spec)
@@ -806,7 +859,7 @@ def test_2x2_workgroups_bitwise_single_block(engine, case, t2):
             assert e.timings()["band_kernel"] == kernel
             return r
     got = _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", t2, lambda: fresh(
-        {"2": "f4_2x2", "1": "f4_routed"}[t2])))
+        {"2": "f4_2x2", "1": "f4_routed", "3": "f4_quad"}[t2])))
     ref = _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", "0", lambda: fresh("f4")))
     for k in got:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{case} {k}")

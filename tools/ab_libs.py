@@ -24,7 +24,8 @@ WORKLOADS = {  # name: (N, M, length_cm, window, missing, additive_only)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--libs", nargs="+", required=True, help="name=path.so")
+    ap.add_argument("--libs", nargs="+", required=True,
+                    help="name=path.so[,ENV=VALUE...] (engine knobs are read when an engine is created)")
     ap.add_argument("--workload", nargs="+", default=["c3"], choices=sorted(WORKLOADS))
     ap.add_argument("--runs", type=int, default=8)
     ap.add_argument("--c5-snp", type=int, default=300_000)
@@ -44,28 +45,44 @@ def main():
             pos = np.round(pos)
         flags = _lib.FLAG_ADDITIVE_ONLY if add else 0
         engines = {}
-        for name, path in libs.items():
-            e = Engine(0, lib_path=path)
+        for name, spec in libs.items():
+            path, *envs = spec.split(",")
+            old = {k: os.environ.get(k) for k, _ in (x.split("=", 1) for x in envs)}
+            os.environ.update(dict(x.split("=", 1) for x in envs))
+            try:
+                e = Engine(0, lib_path=path)
+            finally:
+                for k, v in old.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
             e.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
             engines[name] = e
         del buf
         torch.cuda.empty_cache()
-        res = {name: {"band": [], "total": []} for name in libs}
+        stages = ("count_ms", "stats_ms", "schedule_ms", "band_ms", "finalize_ms", "total_ms")
+        res = {name: {"band": [], "total": [], "kernel": None, "stages": {k: [] for k in stages}} for name in libs}
         ref = None
         for r in range(a.runs + 1):
             for name, e in engines.items():
                 got = e.run(w, 1e-4, 1e-5, 1.0 / M, pos, flags=flags)
                 t = e.timings()
+                res[name]["kernel"] = t.get("band_kernel")
                 if r > 0:  # run 0 is the warmup
                     res[name]["band"].append(t["band_ms"])
                     res[name]["total"].append(t["total_ms"])
+                    for k in stages:
+                        res[name]["stages"][k].append(t[k])
                 if ref is None:
                     ref = got
                 else:  # every build must agree on the integer outputs
                     for k in ("l2_ws", "l2d_ws"):
                         assert np.array_equal(got[k], ref[k]), (wl, name, k)
         out[wl] = {name: {"band_ms_median": float(np.median(v["band"])), "band_ms_min": float(np.min(v["band"])),
-                          "total_ms_median": float(np.median(v["total"])), "runs": len(v["band"])}
+                          "total_ms_median": float(np.median(v["total"])), "runs": len(v["band"]),
+                          "band_kernel": v["kernel"],
+                          "stages_ms_median": {k: round(float(np.median(x)), 4) for k, x in v["stages"].items()}}
                    for name, v in res.items()}
         print(json.dumps({wl: out[wl]}), file=sys.stderr, flush=True)
         for e in engines.values():
