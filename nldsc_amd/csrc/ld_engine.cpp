@@ -137,10 +137,14 @@ struct nldsc_engine {
     int last_ksplit = 1;
     int last_round_items = 0;
     int last_tail_ksplit = 1;
-    // fp4 band kernels on the GPU plan ($NLDSC_T2): 1 (default) missing-free 2 x 2 super-items in the 2 x 2
-    // block-pair workgroups, the rest in the single-block kernel; 3 the same with missing-free 4 x 4 super-items in
-    // the quad workgroups (64 x 64 tiles per wave); 2 everything in the 2 x 2 workgroups; 0 single-block only
-    int t2_mode = 1;
+    // fp4 band kernels on the GPU plan ($NLDSC_T2): 3 (default) missing-free 4 x 4 super-items in the quad
+    // workgroups (64 x 64 tiles per wave), the rest in the single-block kernel (C5 slice band -25 % against 1, the
+    // others unchanged: profiles/r03_ab_t2_quad.json); 1 the same with missing-free 2 x 2 super-items in the 2 x 2
+    // block-pair workgroups; 2 everything in the 2 x 2 workgroups; 0 single-block only
+    int t2_mode = 3;
+    // additive-only fp4 band in 32 x 64 tiles (column-block pair items, the row strip decoded once for two column
+    // blocks; $NLDSC_F4_NC2)
+    bool f4_nc2 = false;
     // single-block fp4 band in launches of one round of wave slots ($NLDSC_BAND_ROUNDS=0: one launch)
     bool band_rounds = true;
     // round launches alternated over two streams ($NLDSC_BAND_STREAMS=2): round k + 1's workgroups take the wave
@@ -301,6 +305,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_BAND_STREAMS")) e->band_streams = std::atoi(v) == 2 ? 2 : 1;
     if (const char* v = std::getenv("NLDSC_COMPACT")) e->compact = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_DEBUG_TIMING")) e->debug_timing = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_F4_NC2")) e->f4_nc2 = std::atoi(v) != 0;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
@@ -549,6 +554,9 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                           std::all_of(p->positions, p->positions + M, [](double x) { return x >= 0.0; });
     // the 2 x 2 block-pair workgroups: fp4, unsegmented rows, GPU plan, and no K-split (choose_ksplit below)
     const bool t2_cand = e->t2_mode > 0 && gpu_plan && use_f4 && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 2;
+    // additive-only fp4 items of two column blocks (GPU plan, unsegmented rows; no K-split: its partial kernel takes
+    // single block pairs)
+    const bool nc2 = e->f4_nc2 && gpu_plan && use_f4 && !dom && n_it <= nldsc::F4_SEG_CHUNKS;
     const bool routed = e->t2_mode == 1 || e->t2_mode == 3;
     const bool quad = e->t2_mode == 3;
     const int route_shift = quad ? 2 : 1;  // super-items of 2^route_shift blocks a side
@@ -559,7 +567,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // shard of C3, 3 300 items, band 3.35 -> 3.01 ms; a 1/2 shard, 13 000 items, P = 5 made it 7.5 % slower).
     auto choose_ksplit = [&](int n_items) {
         int ksplit = 1;
-        if (use_f4 && n_items > 0 && n_it <= nldsc::F4_SEG_CHUNKS && e->ksplit_ok) {
+        if (use_f4 && !nc2 && n_items > 0 && n_it <= nldsc::F4_SEG_CHUNKS && e->ksplit_ok) {
             const double slots = 8.0 * (double)e->n_cu, t_round = 0.67e-6 * n_it;
             auto cost = [&](int P) {
                 return std::ceil((double)n_items * P / slots) / P * t_round +
@@ -602,7 +610,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         HIPCHK(hipEventRecord(e->ev_pos, st));
         HIPCHK(hipStreamWaitEvent(e->plan_stream, e->ev_pos, 0));
         HIPCHK(nldsc::launch_plan(e->pos.p, M, p->ld_wind, own_begin, own_end, e->Aw.p, e->Ew.p, e->Rw.p,
-                                  e->plan_rows.p, e->plan_counts.p, e->plan_meta.p, e->plan_stream));
+                                  e->plan_rows.p, e->plan_counts.p, e->plan_meta.p, e->plan_stream, nc2));
         if (t2_cand)
             HIPCHK(nldsc::launch_plan_super(M, e->plan_rows.p, e->plan_rows2.p, e->plan_counts2.p, e->plan_meta.p + 4,
                                             route_shift,
@@ -658,7 +666,8 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         if (!use_t2 || routed) {
             HIPCHK(e->items.ensure(std::max<size_t>((size_t)n_items, 1)));
             if (n_items > 0)
-                HIPCHK(nldsc::launch_plan_emit(M, e->plan_rows.p, e->plan_meta.p, e->plan_counts.p, e->items.p, ps));
+                HIPCHK(nldsc::launch_plan_emit(M, e->plan_rows.p, e->plan_meta.p, e->plan_counts.p, e->items.p, ps,
+                                               nc2));
         }
         if (use_f4) {  // per 32-SNP block: holds a missing call (the kernels' m-product predicate: routing, issued count)
             HIPCHK(e->blk_miss.ensure((size_t)nblk));
@@ -789,7 +798,9 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
             e->ws_acc.p, true, blk_rep, routed ? e->blk_miss.p : nullptr, which, st);
     };
     // (uncompacted routed list, $NLDSC_COMPACT=0: the kernels skip the items a super-item kernel takes)
-    const uint8_t* single_miss = use_t2 && routed && !compact ? e->blk_miss.p : nullptr;
+    // (column-block pair items: the compaction keeps an item while one of its blocks is unrouted, the kernel drops
+    // the other)
+    const uint8_t* single_miss = use_t2 && routed && (!compact || nc2) ? e->blk_miss.p : nullptr;
     auto launch_single = [&](int which) -> hipError_t {
         if (use_f4 && ksplit > 1)
             return nldsc::launch_band_f4_split(dom, ksplit, n_single, geno, pitch_words, n_it, e->cst.p, single,
@@ -804,7 +815,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                 if (r == hipSuccess) r = hipStreamWaitEvent(e->band_stream2, e->ev_fork, 0);
                 if (r != hipSuccess) return r;
             }
-            hipError_t r = nldsc::launch_band_f4(dom, max_nc, n_full, geno, pitch_words, n_it, e->cst.p, single,
+            hipError_t r = nldsc::launch_band_f4(dom, nc2 ? 2 : 1, n_full, geno, pitch_words, n_it, e->cst.p, single,
                                                  e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N,
                                                  p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                                  e->ws_acc.p, true, blk_rep, which, st, single_miss, round_items,

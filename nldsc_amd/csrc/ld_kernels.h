@@ -38,7 +38,14 @@ hipError_t launch_snp_stats(const int* counts, const uint8_t* flip, const double
 // residual std, residual-pass flag bit 2, exact constants and fp32 table of the reference's fp32 residual,
 // replayed in its arithmetic (ld_kernels.hip reference_residual_kernel)
 constexpr int REF_RESIDUAL_MIN_CLASS = 16;
-// blk_rep[block] = 1 for blocks holding such SNPs (cheap; first), then the replay itself (long, few waves)
+// blk_rep[block] = 1 for blocks holding such SNPs (cheap; first), then the replay itself (long, few waves).
+// Concurrency invariant: the replay runs on the plan stream beside the main stream's band launches and rewrites
+// sflags[j] bit 1 (residual pass; a plain byte read-modify-write) and cst[j] / lut[j] of replayed SNPs j only.
+// Until ev_replay, main-stream readers may touch sflags bits 0 and 2 (left_pointer_kernel, the host flag copy)
+// and never bit 1, cst or lut of a replayed SNP: the non-KC band launches (single-block, 2 x 2, quad, K-split
+// epilogue) drop the items / super-items that hold a block with blk_rep set (skip_item); the K-split partial
+// kernel runs every item but uses flag bit 2 alone (the missing-block test; band_f4_body with PART); the KC
+// launches, the K-split epilogue of KC items and finalize wait on ev_replay.
 hipError_t launch_replay_flags(const int* counts, const uint8_t* flip, const uint8_t* sflags, int n_snp,
                               uint8_t* blk_rep, hipStream_t st);
 hipError_t launch_reference_residuals(const uint8_t* img, int row_bytes, int n_org, bool strict, const int* counts,
@@ -59,10 +66,12 @@ hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const doubl
 // band schedule on the GPU for non-negative sorted positions: all-pass left pointers A, window edges E,
 // right pointers R, per-row-block offset ranges `rows` (nblk), tile item offsets `counts` (capacity
 // ceil(nblk/16) * ceil(nblk/16)); meta[1] = items, meta[2] = diagonal items (read after the stream
-// reaches it), then plan_emit writes the items (16 row blocks x 16 offsets tile order)
+// reaches it), then plan_emit writes the items (16 row blocks x 16 offsets tile order).  pair: items of two
+// neighbouring column blocks (I, J, 2) (the additive-only fp4 kernel's 32 x 64 tiles; a row's odd last one (I, J, 1))
 hipError_t launch_plan(const double* pos, int n, double w, int own_lo, int own_hi, int* A, int* E, int* R,
-                       int2* rows, int* counts, int* meta, hipStream_t st);
-hipError_t launch_plan_emit(int n, const int2* rows, const int* meta, const int* offsets, int4* items, hipStream_t st);
+                       int2* rows, int* counts, int* meta, hipStream_t st, bool pair = false);
+hipError_t launch_plan_emit(int n, const int2* rows, const int* meta, const int* offsets, int4* items, hipStream_t st,
+                            bool pair = false);
 hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                        const float2* lut, const int4* items, const double* pos, const int* Lw, const int* Rw,
                        const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
@@ -75,7 +84,8 @@ hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* gen
 // K-loop chunks (128 samples each) per fp32 accumulation segment of the fp4 path: rows longer than this
 // (N > 2^19) run the segmented kernel, which folds the fp32 Gram into int32 after every segment
 constexpr int F4_SEG_CHUNKS = 4096;
-// exact path on fp4 MFMAs (N < 2^27), items (I, J0, 1, 0) (max_nc must be 1).  blk_rep (or nullptr): per 32-SNP
+// exact path on fp4 MFMAs (N < 2^27), items (I, J0, 1, 0) (max_nc 1), or for additive-only unsegmented rows also
+// (I, J0, 2, 0) column-block pairs (max_nc 2; blk_miss then drops routed column blocks per block).  blk_rep (or nullptr): per 32-SNP
 // block, 1 if a SNP carries replayed fp32 vectors (ka / kr != 0): its items run in a second launch (the exact
 // kernels' KC instantiation).  which: 1 the main launch (items of other blocks), 2 the KC launch, 3 both
 hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* geno, int pitch_words, int n_it,

@@ -681,16 +681,17 @@ __global__ void plan_rows_kernel(const int* __restrict__ E, const int* __restric
 
 __device__ __forceinline__ int plan_n_c(const int* meta) { return (meta[0] + PLAN_C - 1) / PLAN_C; }
 
-// per tile (T, c) of PLAN_R row blocks x PLAN_C offsets, in (T, c) order: its item count
+// per tile (T, c) of PLAN_R row blocks x PLAN_C offsets, in (T, c) order: its item count (pair: items of two
+// neighbouring column blocks, (I, J, 2), the last of a row's run in a tile possibly (I, J, 1))
 __global__ void plan_count_kernel(const int2* __restrict__ rows, int nblk, const int* __restrict__ meta,
-                                  int* __restrict__ counts) {
+                                  int* __restrict__ counts, int pair) {
     const int n_t = (nblk + PLAN_R - 1) / PLAN_R, n_c = plan_n_c(meta);
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n_t * n_c; k += gridDim.x * blockDim.x) {
         const int T = k / n_c, c = k % n_c;
         int cnt = 0;
         for (int I = T * PLAN_R; I < min(nblk, T * PLAN_R + PLAN_R); ++I) {
             const int a = max(rows[I].x, c * PLAN_C), b = min(rows[I].y, c * PLAN_C + PLAN_C - 1);
-            if (a <= b) cnt += b - a + 1;
+            if (a <= b) cnt += pair ? (b - a + 2) / 2 : b - a + 1;
         }
         counts[k] = cnt;
     }
@@ -746,14 +747,14 @@ __global__ void __launch_bounds__(1024) scan_counts_kernel(int* __restrict__ cou
 }
 
 __global__ void plan_emit_kernel(const int2* __restrict__ rows, int nblk, const int* __restrict__ meta,
-                                 const int* __restrict__ offsets, int4* __restrict__ items) {
+                                 const int* __restrict__ offsets, int4* __restrict__ items, int pair) {
     const int n_t = (nblk + PLAN_R - 1) / PLAN_R, n_c = plan_n_c(meta);
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n_t * n_c; k += gridDim.x * blockDim.x) {
         const int T = k / n_c, c = k % n_c;
         int o = offsets[k];
         for (int I = T * PLAN_R; I < min(nblk, T * PLAN_R + PLAN_R); ++I) {
             const int a = max(rows[I].x, c * PLAN_C), b = min(rows[I].y, c * PLAN_C + PLAN_C - 1);
-            for (int d = a; d <= b; ++d) items[o++] = make_int4(I, I + d, 1, 0);
+            for (int d = a; d <= b; d += 1 + pair) items[o++] = make_int4(I, I + d, pair ? min(2, b - d + 1) : 1, 0);
         }
     }
 }
@@ -1404,42 +1405,6 @@ __device__ __forceinline__ F4Frag decode_f4(uint32_t wa, uint32_t wb) {
 template <bool WM>
 constexpr int H_SCALE = WM ? E8M0_ONE : E8M0_HALF;
 
-// Parity-grouped decode (study variant, NLDSC_PARITY_DECODE=1): one K step takes the even codes of a chunk's four
-// words, the next the odd codes, so every dword of an operand has the same bit placement and each plane sits where
-// one shift (shared by v and the planes of that parity) puts it: even v = (w << 1) & 0x66.., h = w & 0x22.. (1.0;
-// missing-free blocks (w << 1) & 0x44.. = 2.0), m = (w << 1) & ~w & 0x22.. (1.0); odd v = (w >> 1) & 0x66..,
-// h = (w >> 1) & 0x44.. (2.0), m = w & ~(w >> 1) & 0x44.. (2.0) — 8 VALU per word with missing calls instead of 9.
-// Scales per step: h and m planes at 2.0 take the E8M0 scale 2^-1.
-#ifndef NLDSC_PARITY_DECODE
-#define NLDSC_PARITY_DECODE 0
-#endif
-template <bool WM, int PAR>  // PAR 1: even codes, 2: odd codes
-__device__ __forceinline__ F4Frag decode_f4_par(const uint4& c) {
-    constexpr uint32_t M = 0x22222222u, K6 = 0x66666666u, M4 = 0x44444444u;
-    F4Frag f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t w = k == 0 ? c.x : k == 1 ? c.y : k == 2 ? c.z : c.w;
-        if constexpr (PAR == 1) {
-            const uint32_t s1 = w << 1;
-            f.x[k] = (int)(s1 & K6);
-            f.h[k] = (int)(WM ? (w & M) : (s1 & M4));
-            f.o[k] = WM ? (int)(s1 & ~w & M) : 0;
-        } else {
-            const uint32_t s2 = w >> 1;
-            f.x[k] = (int)(s2 & K6);
-            f.h[k] = (int)(s2 & M4);
-            f.o[k] = WM ? (int)(w & ~s2 & M4) : 0;
-        }
-    }
-    return f;
-}
-// E8M0 scales of the h / m planes of decode_f4_par<WM, PAR> (PAR 0: decode_f4<WM>)
-template <bool WM, int PAR>
-constexpr int PAR_H_SCALE = PAR == 2 ? E8M0_HALF : H_SCALE<WM>;
-template <int PAR>
-constexpr int PAR_M_SCALE = PAR == 2 ? E8M0_HALF : E8M0_ONE;
-
 // SA / SB: E8M0 block scales of the A / B operand (H_SCALE for an h plane)
 template <int SA = E8M0_ONE, int SB = E8M0_ONE>
 __device__ __forceinline__ f32x16v mfma_f4(const i32x4& a, const i32x4& b, const f32x16v& c) {
@@ -1493,23 +1458,21 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         colp[c] = reinterpret_cast<const uint4*>(geno + (size_t)((J0 + c) * 32 + i) * (size_t)pitch_words) + h;
     // RM / CM: the row / column block holds missing calls.  A block without any has an all-zero m plane,
     // so the products with it are skipped (imputed hard calls: 3 of the 8 MFMAs remain).
-    auto mfmas_v = [&](const F4Frag& a, const F4Frag (&b)[NC], auto RMc, auto CMc, auto PARc) {
+    auto mfmas_v = [&](const F4Frag& a, const F4Frag (&b)[NC], auto RMc, auto CMc) {
         constexpr bool RM = decltype(RMc)::value, CM = decltype(CMc)::value;
-        constexpr int PAR = decltype(PARc)::value;  // 0: decode_f4; 1 / 2: decode_f4_par even / odd codes
-        constexpr int hA = PAR_H_SCALE<RM, PAR>, hB = PAR_H_SCALE<CM, PAR>, mS = PAR_M_SCALE<PAR>;
         // Issue order xx, xo, xh, ox, hx, oo, oh, ho: the order alone moves the band kernel by up to 12 %
         // (decode interleave, register assignment); this one measured best of 18 orders in round 1.  On a
         // diagonal block m.x and h.x are the transposes of x.m and x.h (skipped).
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             gxx[c] = mfma_f4(a.x, b[c].x, gxx[c]);
-            if (CM) gxo[c] = mfma_f4<E8M0_ONE, mS>(a.x, b[c].o, gxo[c]);
-            if (DOM) gxh[c] = mfma_f4<E8M0_ONE, hB>(a.x, b[c].h, gxh[c]);
-            if (RM && !(DIAG0 && c == 0)) gox[c] = mfma_f4<mS, E8M0_ONE>(a.o, b[c].x, gox[c]);
-            if (DOM && !(DIAG0 && c == 0)) ghx[c] = mfma_f4<hA, E8M0_ONE>(a.h, b[c].x, ghx[c]);
-            if (RM && CM) goo[c] = mfma_f4<mS, mS>(a.o, b[c].o, goo[c]);
-            if (DOM && RM) goh[c] = mfma_f4<mS, hB>(a.o, b[c].h, goh[c]);
-            if (DOM && CM && !(DIAG0 && c == 0)) gho[c] = mfma_f4<hA, mS>(a.h, b[c].o, gho[c]);
+            if (CM) gxo[c] = mfma_f4(a.x, b[c].o, gxo[c]);
+            if (DOM) gxh[c] = mfma_f4<E8M0_ONE, H_SCALE<CM>>(a.x, b[c].h, gxh[c]);
+            if (RM && !(DIAG0 && c == 0)) gox[c] = mfma_f4(a.o, b[c].x, gox[c]);
+            if (DOM && !(DIAG0 && c == 0)) ghx[c] = mfma_f4<H_SCALE<RM>, E8M0_ONE>(a.h, b[c].x, ghx[c]);
+            if (RM && CM) goo[c] = mfma_f4(a.o, b[c].o, goo[c]);
+            if (DOM && RM) goh[c] = mfma_f4<E8M0_ONE, H_SCALE<CM>>(a.o, b[c].h, goh[c]);
+            if (DOM && CM && !(DIAG0 && c == 0)) gho[c] = mfma_f4<H_SCALE<RM>, E8M0_ONE>(a.h, b[c].o, gho[c]);
         }
         // full 8-product steps: F4_VPM VALU after each MFMA; otherwise (additive-only items, missing-free
         // blocks) the decode is spread evenly over the MFMAs there are (additive-only C2: -6.6 % band time)
@@ -1521,7 +1484,7 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
             }
         } else {
             constexpr int n_mfma = NC * (1 + CM + RM + (RM && CM) + (DOM ? 2 + RM + CM : 0));
-            constexpr int n_valu = NC * (RM ? 9 : 6) * 2 + NC * (CM ? 9 : 6) * 2;
+            constexpr int n_valu = (RM ? 9 : 6) * 2 + NC * (CM ? 9 : 6) * 2;  // the row strip decoded once
 #pragma unroll
             for (int m = 0; m < n_mfma; ++m) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -1533,55 +1496,44 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     // even chunks, Q odd ones; each is reloaded right after its last word is decoded and read again two K
     // steps later, with no register copies of loads in flight (those would force vmcnt(0)).
     auto kloop = [&](auto RMc, auto CMc, const int t_lo, const int t_hi) {
-        constexpr bool PD = NLDSC_PARITY_DECODE != 0;
-        // set 0 holds a chunk's words 0-1 (PD: its even codes), set 1 words 2-3 (PD: its odd codes)
-        auto dec0 = [](const uint4& w, auto WMc) {
-            constexpr bool WM = decltype(WMc)::value;
-            if constexpr (PD) return decode_f4_par<WM, 1>(w);
-            else return decode_f4<WM>(w.x, w.y);
-        };
-        auto dec1 = [](const uint4& w, auto WMc) {
-            constexpr bool WM = decltype(WMc)::value;
-            if constexpr (PD) return decode_f4_par<WM, 2>(w);
-            else return decode_f4<WM>(w.z, w.w);
-        };
-        const auto P0 = std::integral_constant<int, PD ? 1 : 0>{};
-        const auto P1 = std::integral_constant<int, PD ? 2 : 0>{};
+        constexpr bool RM = decltype(RMc)::value, CM = decltype(CMc)::value;
         const int last = t_hi - 1;
         uint4 pr = rowp[2 * t_lo], qr = rowp[2 * t_lo + 2], pc[NC], qc[NC];
 #pragma unroll
         for (int c = 0; c < NC; ++c) { pc[c] = colp[c][2 * t_lo]; qc[c] = colp[c][2 * t_lo + 2]; }
         // two named fragment sets: set 1 is decoded while set 0 feeds the MFMAs and vice versa, so no
         // fragment is copied (a single rotating set costs ~12 v_mov per K step)
-        F4Frag a0 = dec0(pr, RMc), a1, b0[NC], b1[NC];
+        F4Frag a0 = decode_f4<RM>(pr.x, pr.y), a1, b0[NC], b1[NC];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) b0[c] = dec0(pc[c], CMc);
+        for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(pc[c].x, pc[c].y);
         for (int t = t_lo; t < t_hi; t += 2) {
-            a1 = dec1(pr, RMc);
+            a1 = decode_f4<RM>(pr.z, pr.w);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b1[c] = dec1(pc[c], CMc);
-            mfmas_v(a0, b0, RMc, CMc, P0);  // K step 2t   (chunk t, words 0-1)
+            for (int c = 0; c < NC; ++c) b1[c] = decode_f4<CM>(pc[c].z, pc[c].w);
+            mfmas_v(a0, b0, RMc, CMc);  // K step 2t   (chunk t, words 0-1)
             pr = rowp[2 * min(t + 2, last)];
 #pragma unroll
             for (int c = 0; c < NC; ++c) pc[c] = colp[c][2 * min(t + 2, last)];
-            a0 = dec0(qr, RMc);
+            a0 = decode_f4<RM>(qr.x, qr.y);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b0[c] = dec0(qc[c], CMc);
-            mfmas_v(a1, b1, RMc, CMc, P1);  // K step 2t+1 (chunk t, words 2-3)
-            a1 = dec1(qr, RMc);
+            for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(qc[c].x, qc[c].y);
+            mfmas_v(a1, b1, RMc, CMc);  // K step 2t+1 (chunk t, words 2-3)
+            a1 = decode_f4<RM>(qr.z, qr.w);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b1[c] = dec1(qc[c], CMc);
-            mfmas_v(a0, b0, RMc, CMc, P0);  // K step 2t+2 (chunk t+1, words 0-1)
+            for (int c = 0; c < NC; ++c) b1[c] = decode_f4<CM>(qc[c].z, qc[c].w);
+            mfmas_v(a0, b0, RMc, CMc);  // K step 2t+2 (chunk t+1, words 0-1)
             qr = rowp[2 * min(t + 3, last)];
 #pragma unroll
             for (int c = 0; c < NC; ++c) qc[c] = colp[c][2 * min(t + 3, last)];
-            a0 = dec0(pr, RMc);
+            a0 = decode_f4<RM>(pr.x, pr.y);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b0[c] = dec0(pc[c], CMc);
-            mfmas_v(a1, b1, RMc, CMc, P1);  // K step 2t+3 (chunk t+1, words 2-3)
+            for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(pc[c].x, pc[c].y);
+            mfmas_v(a1, b1, RMc, CMc);  // K step 2t+3 (chunk t+1, words 2-3)
         }
     };
-    // wave-uniform: does the row block / do the column blocks hold a missing call (flag bit 2)?
+    // wave-uniform: does the row block / do the column blocks hold a missing call (flag bit 2)?  With PART this
+    // is the only SNP state used (sh.cst and the other flag bits may be rewritten by a concurrent replay:
+    // launch_reference_residuals in ld_kernels.h)
     const bool rm = __any(lane < 32 && (sh.info[lane].fl & 4));
     const bool cm = __any(32 + lane < NS && (sh.info[32 + lane].fl & 4));
     auto run = [&](const int t_lo, const int t_hi) {
@@ -1699,7 +1651,10 @@ __device__ __forceinline__ bool routed_item(const uint8_t* blk_miss, int route_s
 }
 
 // One block pair per item.  WPS 2, except the segmented add+dom kernel (its int32 fold registers need 1).
-template <bool DOM, int WPS, int SEG, bool KC>
+// NCX 2 (additive-only, unsegmented): items (I, J, 2) pair column blocks J and J + 1 in one wave (a 32 x 64 tile: the
+// row strip decoded once for both), as the plan emits them with pairing; a column block the super-item routing sends
+// elsewhere (blk_miss) is dropped from its item here.
+template <bool DOM, int WPS, int SEG, bool KC, int NCX = 1>
 __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
                                                         const SnpConst* __restrict__ cst, const int4* __restrict__ items,
                                                         const double* __restrict__ pos, const int* __restrict__ Lw,
@@ -1713,12 +1668,28 @@ __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __rest
     __shared__ float tr[32 * 33];
     const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
     if (skip_item<KC>(blk_rep, it)) return;
+#define NLDSC_BODY(NC_, DIAG_, IT_)                                                                                   \
+    band_f4_body<DOM, NC_, DIAG_, SEG, KC>(sh, IT_, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, \
+                                           n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, tr)
+    if constexpr (NCX == 2) {
+        static_assert(!DOM && SEG == 0, "column-block pairs: additive-only, unsegmented rows");
+        if (it.z == 2) {
+            const int nblk = (n_snp + 31) >> 5;
+            const bool r0 = blk_miss != nullptr && routed_item(blk_miss, route_shift, it.x, it.y, nblk);
+            const bool r1 = blk_miss != nullptr && routed_item(blk_miss, route_shift, it.x, it.y + 1, nblk);
+            if (r0 && r1) return;
+            if (r0 || r1) {  // one column block left: the single-block body on it
+                const int4 one = make_int4(it.x, it.y + (r0 ? 1 : 0), 1, 0);
+                if (one.y == one.x) NLDSC_BODY(1, true, one); else NLDSC_BODY(1, false, one);
+                return;
+            }
+            if (it.y == it.x) NLDSC_BODY(2, true, it); else NLDSC_BODY(2, false, it);
+            return;
+        }
+    }
     // blk_miss: a super-item kernel runs the missing-free super-items
     if (blk_miss != nullptr && routed_item(blk_miss, route_shift, it.x, it.y, (n_snp + 31) >> 5)) return;
-#define NLDSC_BODY(DIAG_)                                                                                             \
-    band_f4_body<DOM, 1, DIAG_, SEG, KC>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind,  \
-                                         n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, tr)
-    if (it.y == it.x) NLDSC_BODY(true); else NLDSC_BODY(false);
+    if (it.y == it.x) NLDSC_BODY(1, true, it); else NLDSC_BODY(1, false, it);
 #undef NLDSC_BODY
 }
 
@@ -2089,7 +2060,8 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
 constexpr int COMPACT_CHUNK = 1024;
 __device__ __forceinline__ bool keep_item(const int4* items, int t, const uint8_t* blk_miss, int route_shift, int nblk) {
     const int4 it = items[t];
-    return !routed_item(blk_miss, route_shift, it.x, it.y, nblk);
+    return !routed_item(blk_miss, route_shift, it.x, it.y, nblk) ||
+           (it.z == 2 && !routed_item(blk_miss, route_shift, it.x, it.y + 1, nblk));
 }
 
 __global__ void __launch_bounds__(1024) compact_count_kernel(const int4* __restrict__ items, int n_items,
@@ -2141,10 +2113,12 @@ __global__ void issued_products_kernel(const int4* __restrict__ items, int n_ite
     if (t < n_items) {
         const int4 it = items[t];
         const bool diag = it.x == it.y;
-        if (kind == 2) {
-            if (!((routed & 1) && routed_item(blk_miss, route_shift, it.x, it.y, nblk))) {
-                const int rm = blk_miss[it.x] != 0, cm = blk_miss[it.y] != 0, nd = !diag;
-                n = 1 + cm + rm * nd + rm * cm + (dom ? 1 + nd + rm + cm * nd : 0);
+        if (kind == 2) {  // (it.z == 2: additive-only column-block pairs, one product set per column block)
+            for (int c = 0; c < it.z; ++c) {
+                const int J = it.y + c;
+                if ((routed & 1) && routed_item(blk_miss, route_shift, it.x, J, nblk)) continue;
+                const int rm = blk_miss[it.x] != 0, cm = blk_miss[J] != 0, nd = it.x != J;
+                n += 1 + cm + rm * nd + rm * cm + (dom ? 1 + nd + rm + cm * nd : 0);
             }
         } else if (kind == 1) {
             n = 4 + (dom ? (diag ? 2 : 4) : 0);
@@ -2488,7 +2462,7 @@ hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const doubl
 }
 
 hipError_t launch_plan(const double* pos, int n, double w, int own_lo, int own_hi, int* A, int* E, int* R,
-                       int2* rows, int* counts, int* meta, hipStream_t st) {
+                       int2* rows, int* counts, int* meta, hipStream_t st, bool pair) {
     const int nblk = (n + 31) / 32;
     hipError_t e = hipMemsetAsync(meta, 0, 4 * sizeof(int), st);
     if (e != hipSuccess || n <= 0 || own_hi <= own_lo) return e;
@@ -2496,15 +2470,16 @@ hipError_t launch_plan(const double* pos, int n, double w, int own_lo, int own_h
     hipLaunchKernelGGL(plan_right_kernel, dim3(1), dim3(1024), 0, st, E, n, R);
     hipLaunchKernelGGL(plan_rows_kernel, dim3((nblk + 255) / 256), dim3(256), 0, st, E, A, n, nblk, own_lo, own_hi,
                        rows, meta);
-    hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, counts);
+    hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, counts, pair ? 1 : 0);
     hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts, nblk, meta);
     return hipGetLastError();
 }
 
-hipError_t launch_plan_emit(int n, const int2* rows, const int* meta, const int* offsets, int4* items, hipStream_t st) {
+hipError_t launch_plan_emit(int n, const int2* rows, const int* meta, const int* offsets, int4* items, hipStream_t st,
+                            bool pair) {
     const int nblk = (n + 31) / 32;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, offsets, items);
+    hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, offsets, items, pair ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -2544,7 +2519,7 @@ hipError_t launch_plan_super(int n, const int2* rows, int2* rows2, int* counts2,
     hipError_t e = hipMemsetAsync(meta2, 0, 4 * sizeof(int), st);
     if (e != hipSuccess || n <= 0) return e;
     hipLaunchKernelGGL(plan_rows2_kernel, dim3((nblk2 + 255) / 256), dim3(256), 0, st, rows, nblk, shift, rows2, meta2);
-    hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, counts2);
+    hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, counts2, 0);
     hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts2, nblk2, meta2);
     return hipGetLastError();
 }
@@ -2554,7 +2529,7 @@ hipError_t launch_plan_emit_super(int n, const int2* rows2, const int* meta2, co
                                   int shift, hipStream_t st) {
     const int nblk2 = ((n + 31) / 32 + (1 << shift) - 1) >> shift;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, offsets2, items2);
+    hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, offsets2, items2, 0);
     return hipGetLastError();
 }
 
@@ -2626,20 +2601,23 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           int which, hipStream_t st, const uint8_t* blk_miss, int round_items, int route_shift,
                           hipStream_t st2) {
     if (n_items <= 0) return hipSuccess;
-    if (max_nc != 1) return hipErrorInvalidValue;  // single block-pair items
+    // single block-pair items, or (additive-only, unsegmented rows) column-block pairs
+    if (max_nc != 1 && !(max_nc == 2 && !dom && n_it <= F4_SEG_CHUNKS)) return hipErrorInvalidValue;
     if (blk_miss != nullptr && n_it > F4_SEG_CHUNKS) return hipErrorInvalidValue;  // routing: unsegmented rows only
     // round_items > 0: the items go in launches of that many (one round of the wave slots each), see ld_engine.cpp;
     // not the KC launch (items holding a replayed rare variant: few, the others return at once)
     int chunk = round_items > 0 ? round_items : n_items;
-#define NLDSC_BAND(DOM_, WPS_, SEG_, KC_)                                                                           \
+#define NLDSC_BAND_NC(DOM_, WPS_, SEG_, KC_, NCX_)                                                                  \
     for (int o = 0, r = 0; o < n_items; o += chunk, ++r)                                                          \
-    hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_, KC_>), dim3(std::min(chunk, n_items - o)), dim3(64), 0,    \
+    hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_, KC_, NCX_>), dim3(std::min(chunk, n_items - o)), dim3(64), 0, \
                        (st2 != nullptr && (r & 1)) ? st2 : st, geno, pitch_words,                                   \
                        n_it, cst, items + o, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi,       \
                        l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss, route_shift)
+#define NLDSC_BAND(DOM_, WPS_, SEG_, KC_) NLDSC_BAND_NC(DOM_, WPS_, SEG_, KC_, 1)
 #define NLDSC_PICK(KC_)                                                                                              \
     if (n_it > F4_SEG_CHUNKS) { if (dom) NLDSC_BAND(true, 1, F4_SEG_CHUNKS, KC_); else NLDSC_BAND(false, 2, F4_SEG_CHUNKS, KC_); } \
     else if (dom) NLDSC_BAND(true, 2, 0, KC_);                                                                       \
+    else if (max_nc == 2) NLDSC_BAND_NC(false, 2, 0, KC_, 2);                                                        \
     else NLDSC_BAND(false, 2, 0, KC_)
     // segmented kernel: the add+dom variant needs more than 256 registers (2 waves / SIMD would spill)
     if (which & 1) { NLDSC_PICK(false); }
@@ -2648,6 +2626,7 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
     if (blk_rep && (which & 2)) { NLDSC_PICK(true); }
 #undef NLDSC_PICK
 #undef NLDSC_BAND
+#undef NLDSC_BAND_NC
     return hipGetLastError();
 }
 

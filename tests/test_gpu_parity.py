@@ -877,6 +877,62 @@ def test_2x2_workgroups_bitwise_single_block(engine, case, t2):
                                        maf=(0.0, 0.0)), label=f"2x2 {case} T2={t2}")
 
 
+NC2_CASES = {
+    # additive-only: (T2_CASES key, $NLDSC_T2); pairs with one column block routed to a super-item kernel, diagonal
+    # pairs, odd last items of a row, owned ranges, the KC launch of replayed rare variants
+    "additive_single": ("additive_only", "0"),
+    "additive_routed": ("additive_only", "1"),
+    "mixed_blocks_routed": ("mixed_blocks", "1"),
+    "mixed_groups_quad": ("mixed_groups", "3"),
+    "missing_free_quad": ("missing_free_additive", "3"),
+    "owned_range": ("owned_range", "1"),
+    "odd_blocks_narrow": ("odd_blocks_narrow", "0"),
+    "rare_replay": ("rare_replay", "1"),
+}
+
+
+@pytest.mark.parametrize("case", sorted(NC2_CASES))
+def test_f4_column_block_pairs_bitwise_single_blocks(engine, case):
+    """Additive-only fp4 items of two column blocks ($NLDSC_F4_NC2=1: 32 x 64 tiles, the row strip decoded once for
+    both; a block the super-item routing takes is dropped from its item) give bitwise the single-block items' results
+    and the same issued-product count."""
+    from conftest import rare_variant_set
+    from nldsc_amd import synth
+    from nldsc_amd.engine import Engine
+    key, t2 = NC2_CASES[case]
+    N, M, length, wind, missing, _, own, rare = T2_CASES[key]
+    if rare:
+        rows, pos = rare_variant_set(N)
+        M = len(pos)
+    else:
+        spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=length, seed=N + M,
+                               missing=0.0 if isinstance(missing, str) else missing)
+        g = synth.genotypes(spec)
+        if isinstance(missing, str):
+            rng = np.random.default_rng(M)
+            span = 128 if missing == "mixed4" else 32
+            for b in range(0, (M + span - 1) // span, 3):
+                j = span * b + rng.integers(0, min(span, M - span * b))
+                g[j, rng.choice(N, 20, replace=False)] = -1
+        rows = synth.pack_bed_rows(g)
+        pos = synth.positions_cm(spec)
+    flags = MODES["f4"] | _lib_flag("FLAG_ADDITIVE_ONLY") | (0 if rare else _lib_flag("FLAG_EXACT_RARE"))
+    args = (wind, 1e-5, 1e-5, 1.0 / M, pos)
+
+    def fresh():
+        with Engine(0) as e:
+            e.load_bed_bytes(synth.bed_bytes(rows), M, N)
+            r = e.run(*args, flags=flags, own=own)
+            return r, e.timings()
+    run = lambda nc2: _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", t2, lambda: _env_run(  # noqa: E731
+        "NLDSC_F4_NC2", nc2, fresh)))
+    (got, tg), (ref, tr) = run("1"), run("0")
+    assert tg["band_items"] < tr["band_items"], (tg["band_items"], tr["band_items"])  # the plan paired them
+    assert tg["flop_issued"] == tr["flop_issued"], (tg["flop_issued"], tr["flop_issued"])
+    for k in got:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{case} {k}")
+
+
 ROUND_CASES = {
     # (N, M, length cM, dom, tail K-split required): ~9 400-9 700 items in 2 048-item rounds; the cost model K-splits
     # the partial last round at both lengths (N = 131 101: 1 025 K chunks; N = 315 599: C3 rows)

@@ -34,6 +34,10 @@ pmc() {  # <label> <workload string> <alg-bytes spec> <bench args>
   timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU --kernel-trace -d $P/sq -o s --output-format csv -- $B > /dev/null 2> $P.s.err && \
   timeout -s KILL 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d $P/l2 -o l --output-format csv -- $B > /dev/null 2> $P.l.err \
     || { echo "pmc $label failed"; tail $P.*.err; return 1; }
+  if [ -n "$LDS_PASS" ]; then
+    timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE --kernel-trace -d $P/lds -o d --output-format csv -- $B > /dev/null 2> $P.d.err \
+      || { echo "pmc $label lds failed"; tail $P.d.err; return 1; }
+  fi
   python3 tools/pmc_summary.py $P --workload "$wl" --alg-bytes $alg > $O/pmc_$label.json
 }
 step pmc c3
@@ -41,7 +45,7 @@ pmc c3 "C3 bench: N=315599 M=80000 missing=0.01 add+dom 1 cM" band_f4_kernel=631
 step pmc c2
 pmc c2 "C2 bench: N=50000 M=80000 missing=0.01 additive-only 1 cM" band_f4_kernel=1003520000 --n-org 50000 --additive-only || exit 1
 step pmc c5
-pmc c5 "C5 slice bench: N=315599 M=1250000 missing=0 add+dom 1000 kb" band_f4_q_kernel=98640000000 --workload c5 || exit 1
+LDS_PASS=1 pmc c5 "C5 slice bench: N=315599 M=1250000 missing=0 add+dom 1000 kb" band_f4_q_kernel=98640000000 --workload c5 || exit 1
 step bench c2 c5
 timeout -k 10 300 python bench.py --no-cpu --no-file --steps 10 --n-org 50000 --additive-only > $O/bench_c2.json 2> $O/bench_c2.err || { tail $O/bench_c2.err; exit 1; }
 timeout -k 10 400 python bench.py --no-cpu --no-file --steps 2 --workload c5 > $O/bench_c5.json 2> $O/bench_c5.err || { tail $O/bench_c5.err; exit 1; }

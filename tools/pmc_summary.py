@@ -8,6 +8,8 @@
         -d <dir>/sq -o s --output-format csv -- python3 bench.py ...
 
     rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d <dir>/l2 -o l --output-format csv -- ...  (optional)
+    rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE --kernel-trace \
+        -d <dir>/lds -o d --output-format csv -- ...  (optional)
 
     python tools/pmc_summary.py <dir> --workload "..." --alg-bytes band_f4_kernel=6312960000 > profiles/rNN_pmc.json
 
@@ -60,7 +62,8 @@ def main():
     ap.add_argument("--alg-bytes", action="append", default=[], help="kernel=bytes algorithmic bytes per launch")
     args = ap.parse_args()
     alg = dict((k, float(v)) for k, v in (a.split("=") for a in args.alg_bytes))
-    fetch, write, sq, l2 = (read_counters(os.path.join(args.dir, p)) for p in ("fetch", "write", "sq", "l2"))
+    fetch, write, sq, l2, lds = (read_counters(os.path.join(args.dir, p))
+                                 for p in ("fetch", "write", "sq", "l2", "lds"))
     # engine runs in the profiled command: finalize_kernel runs once per run (the band may take several launches)
     runs = len(fetch.get("finalize_kernel", {}).get("FETCH_SIZE", [])) or None
     kernels = {}
@@ -95,6 +98,12 @@ def main():
         hit, miss = mean(l2.get(name, {}).get("TCC_HIT_sum", [])), mean(l2.get(name, {}).get("TCC_MISS_sum", []))
         if hit is not None and miss is not None:
             k.update(l2_hit=hit, l2_miss=miss, l2_hit_rate=hit / max(hit + miss, 1.0))
+        for c in ("SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_INST_LDS", "SQ_LDS_IDX_ACTIVE"):
+            v = mean(lds.get(name, {}).get(c, []))
+            if v is not None:
+                k[c.lower()] = v
+        if k.get("sq_lds_idx_active"):
+            k["lds_bank_conflict_frac"] = k.get("sq_lds_bank_conflict", 0.0) / k["sq_lds_idx_active"]
         kernels[name] = k
     import hashlib
     src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "nldsc_amd", "csrc", "ld_kernels.hip")
