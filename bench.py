@@ -45,17 +45,19 @@ PATHS = {
 def band_kernel_name(variant: str, dom: bool, default: str) -> str:
     """The band kernel that ran (Engine.timings()['band_kernel']) as rocprof names it, with what it issues."""
     d = "true" if dom else "false"
+    # the single-block kernel: additive-only runs pair neighbouring column blocks per wave ($NLDSC_F4_NC2, default)
+    single = ("band_f4_kernel<true, 2, 0, false> (one wave per 32x32 block pair)" if dom else
+              "band_f4_kernel<false, 2, 0, false, 2> (one wave per 32x64 pair of column blocks)")
     names = {
         "f4_2x2": f"band_f4_t2_kernel<{d}, 4, false> (4-wave workgroups over 2x2 block pairs sharing their strips "
                   "through LDS, global_load_lds ring; v_mfma_scale_f32_32x32x64_f8f6f4, e2m1 operands, exact integer "
                   "Gram in fp32)",
         "f4_routed": f"band_f4_t2_kernel<{d}, 4, false> for missing-free 2x2 super-items (4-wave workgroups sharing "
-                     f"their strips through LDS) + band_f4_kernel<{d}, 2, 0, false> for the rest (one wave per 32x32 "
-                     "block pair); v_mfma_scale_f32_32x32x64_f8f6f4, e2m1 operands, exact integer Gram in fp32",
+                     f"their strips through LDS) + {single} for the rest; v_mfma_scale_f32_32x32x64_f8f6f4, e2m1 "
+                     "operands, exact integer Gram in fp32",
         "f4_quad": f"band_f4_q_kernel<{d}, 4, false> for missing-free 4x4 super-items (4-wave workgroups, one 64x64 "
-                   f"SNP tile of 2x2 block pairs per wave, strips shared through an LDS ring) + band_f4_kernel<{d}, 2, 0, "
-                   "false> for the rest (one wave per 32x32 block pair); v_mfma_scale_f32_32x32x64_f8f6f4, e2m1 "
-                   "operands, exact integer Gram in fp32",
+                   f"SNP tile of 2x2 block pairs per wave, strips shared through an LDS ring) + {single} for the "
+                   "rest; v_mfma_scale_f32_32x32x64_f8f6f4, e2m1 operands, exact integer Gram in fp32",
         "f4": f"band_f4_kernel<{d}, 2, 0, false> (one wave per 32x32 block pair; v_mfma_scale_f32_32x32x64_f8f6f4, "
               "e2m1 operands, exact integer Gram in fp32)",
         "f4_ksplit": f"band_f4_part_kernel<{d}> + band_f4_epi_kernel (K-split; v_mfma_scale_f32_32x32x64_f8f6f4)",

@@ -133,6 +133,7 @@ struct nldsc_engine {
     DevBuf<uint8_t> blk_rep;  // per 32-SNP block: holds a rare variant with replayed fp32 vectors (KC items)
     DevBuf<float> gram;       // K-split partial Gram tiles
     bool ksplit_ok = true;    // $NLDSC_KSPLIT=0 disables the K-split
+    int tail_ksplit = 0;      // $NLDSC_TAIL_KSPLIT=P > 0 forces the round launches' tail split (study knob; 0: model)
     bool replay_overlap = true;  // $NLDSC_REPLAY_OVERLAP=0 runs the rare-variant replay in line on the main stream
     int last_ksplit = 1;
     int last_round_items = 0;
@@ -143,8 +144,8 @@ struct nldsc_engine {
     // block-pair workgroups; 2 everything in the 2 x 2 workgroups; 0 single-block only
     int t2_mode = 3;
     // additive-only fp4 band in 32 x 64 tiles (column-block pair items, the row strip decoded once for two column
-    // blocks; $NLDSC_F4_NC2)
-    bool f4_nc2 = false;
+    // blocks; $NLDSC_F4_NC2=0 turns it off): C2 band 2.85 -> 2.78 ms, one engine per process (r03_c2_nc2.json)
+    bool f4_nc2 = true;
     // single-block fp4 band in launches of one round of wave slots ($NLDSC_BAND_ROUNDS=0: one launch)
     bool band_rounds = true;
     // round launches alternated over two streams ($NLDSC_BAND_STREAMS=2): round k + 1's workgroups take the wave
@@ -299,6 +300,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_GPU_PLAN")) e->gpu_plan = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_ORIENT")) e->orient = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_KSPLIT")) e->ksplit_ok = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_TAIL_KSPLIT")) e->tail_ksplit = std::max(0, std::min(8, std::atoi(v)));
     if (const char* v = std::getenv("NLDSC_REPLAY_OVERLAP")) e->replay_overlap = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_T2")) e->t2_mode = std::max(0, std::min(3, std::atoi(v)));
     if (const char* v = std::getenv("NLDSC_BAND_ROUNDS")) e->band_rounds = std::atoi(v) != 0;
@@ -786,6 +788,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                       n_single >= 4 * slots ? slots : 0;
         const int tail = round_items > 0 ? n_single % round_items : 0;
         tail_p = tail > 0 ? choose_ksplit(tail) : 1;
+        if (tail > 0 && e->tail_ksplit > 0 && !nc2 && 2 * e->tail_ksplit <= n_it) tail_p = e->tail_ksplit;
         n_full = tail_p > 1 ? n_single - tail : n_single;
         e->last_round_items = round_items;
         e->last_tail_ksplit = tail_p;
