@@ -224,6 +224,9 @@ def main():
     ap.add_argument("--no-file", action="store_true",
                     help="skip the wall clock from a PLINK file (rank 0, N = 1: the synthetic .bed written to "
                          "$TMPDIR, then _ldscore.calculate timed from the file)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="create the process group and run the sharded path (owned range, device table, collective "
+                         "gather) even with one rank: the RCCL code of an N-GPU run rehearsed on one GPU")
     ap.add_argument("--concurrent", type=int, default=3,
                     help="c4: chromosomes computed at once per GPU (host threads, one engine stream each)")
     args = ap.parse_args()
@@ -244,7 +247,11 @@ def main():
     if args.backend == "gloo":
         local = 0  # rehearsal: every rank shares GPU 0
     torch.cuda.set_device(local)
-    if world > 1:
+    use_dist = world > 1 or args.force_dist
+    if use_dist and "MASTER_ADDR" not in os.environ:  # --force-dist without a launcher: a group of one
+        from nldsc_amd.launch import free_port
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1")
+    if use_dist:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
@@ -274,7 +281,7 @@ def main():
         if world > 1:
             raise SystemExit("--rehearse is a single-process mode")
         s_rank, s_world = (int(x) for x in args.rehearse.split("/"))
-    split = s_world > 1 and not args.weak
+    split = (s_world > 1 or (args.force_dist and not args.rehearse)) and not args.weak
     buf, pos = synth.device_bed(M, N, seed=7 if split else 7 + rank, length_cm=args.length_cm,
                                 missing=args.missing, device=local)
     eng = Engine(local)
@@ -292,15 +299,15 @@ def main():
         own, own_rel, pos = (lo, hi), (lo - a, hi - a), pos[a:b]
         # the owned slice of the score table stays in HBM ([7, width] fp64 block, nldsc_engine_run_device); the
         # blocks are gathered device to device (RCCL) and only rank 0 copies the gathered table to the host
-        spans = gather_spans(own, device=coll) if world > 1 else [own]  # the sharding is fixed across steps
+        spans = gather_spans(own, device=coll) if use_dist else [own]  # the sharding is fixed across steps
         table = torch.empty((len(RESULT_KEYS), table_width(spans)), dtype=torch.float64, device=f"cuda:{local}")
         gbuf = torch.empty(world * table.numel(), dtype=torch.float64,
-                           device=table.device if coll == "cuda" else "cpu") if world > 1 else None
+                           device=table.device if coll == "cuda" else "cpu") if use_dist else None
     else:
         eng.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
     bed_host = None
-    want_file = rank == 0 and world == 1 and not args.no_file and args.workload == "c3"
-    if rank == 0 and world == 1 and (not args.no_cpu or want_file):
+    want_file = rank == 0 and not use_dist and not args.no_file and args.workload == "c3"
+    if rank == 0 and not use_dist and (not args.no_cpu or want_file):
         bed_host = buf.cpu().numpy().tobytes()
     del buf
     torch.cuda.empty_cache()
@@ -315,7 +322,7 @@ def main():
             eng.run_device(w, args.maf, args.std_thr, rsq, pos, table, own=own_rel, flags=flags)
             tim = eng.timings()
             tg = time.perf_counter()
-            if world > 1:
+            if use_dist:
                 full = gather_table(table if coll == "cuda" else table.cpu(), spans, M, out=gbuf)
                 out = full if full is not None else out
             else:  # rehearsal of one rank: its slice to the host
@@ -333,18 +340,18 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     tims = [step() for _ in range(args.steps)]
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     el = torch.tensor([elapsed], dtype=torch.float64, device=coll)
     pairs_step = torch.tensor([tims[-1]["pairs"]], dtype=torch.float64, device=coll)
-    if world > 1:
+    if use_dist:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(pairs_step, op=dist.ReduceOp.SUM)
     t_max = float(el.item())
@@ -355,7 +362,7 @@ def main():
                          float(np.mean([x["total_ms"] for x in tims])), float(tims[-1]["pairs"]),
                          float(own[1] - own[0])], dtype=torch.float64, device=coll)
     per_rank = [mine]
-    if world > 1:
+    if use_dist:
         per_rank = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(per_rank, mine)
 
@@ -457,7 +464,7 @@ def main():
     if rank == 0:
         print(json.dumps(res), flush=True)
     eng.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

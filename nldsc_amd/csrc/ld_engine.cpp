@@ -33,7 +33,8 @@ constexpr int ROW_ALIGN_BYTES = 64;
 // item order of the single-block-pair schedule: tiles of TILE_R row blocks x TILE_C diagonal offsets
 constexpr int TILE_R = 16, TILE_C = 16;
 
-// resident layout of a .bed image: row j of ceil(N/4) bytes at j * row_bytes, n_rows = M rounded up to 32
+// resident layout of a .bed image: rows of ceil(N/4) bytes padded to row_bytes, n_rows = M rounded up to 32, the rows of
+// each 32-SNP block interleaved in 32-byte chunks (ld_kernels.hip tile_off)
 int row_pitch(int32_t n_org) {
     const int nb = n_org / 4 + (n_org % 4 > 0);
     return (nb + ROW_ALIGN_BYTES - 1) / ROW_ALIGN_BYTES * ROW_ALIGN_BYTES;
@@ -117,7 +118,8 @@ struct nldsc_engine {
     hipEvent_t ev_stats = nullptr;   // SNP constants and replay flags written (the replay's inputs)
     hipEvent_t ev_replay = nullptr;  // replayed constants written (the KC launch and finalize wait on it)
     // resident .bed image
-    DevBuf<uint8_t> bed;
+    DevBuf<uint8_t> bed;      // resident rows, block-interleaved (ld_kernels.hip tile_off)
+    DevBuf<uint8_t> stage_dev;  // loads: rows of the .bed layout on their way into `bed` (released after the load)
     DevBuf<uint8_t> lastb;  // each row's original last byte (the per-run count kernel masks a copy of it)
     DevBuf<uint8_t> flip;   // per SNP: resident row stores the swapped (00 <-> 11) coding
     DevBuf<uint8_t> row_miss;  // per SNP: bit 0 / 1 = a missing call among the reference's / PLINK's individual slots
@@ -186,7 +188,7 @@ struct nldsc_engine {
 
     ~nldsc_engine() {
         (void)hipSetDevice(device);
-        bed.release(); lastb.release(); flip.release(); row_miss.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
+        bed.release(); stage_dev.release(); lastb.release(); flip.release(); row_miss.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
         ws3.release(); lut.release(); cst.release(); sflags.release(); pos.release(); maf.release(); rstd.release();
         l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release(); gram.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
@@ -349,9 +351,17 @@ int nldsc_engine_load_bed_host(nldsc_engine* e, const uint8_t* bed, size_t len, 
     HIPCHK(hipSetDevice(e->device));
     const size_t nb = (size_t)(n_org / 4 + (n_org % 4 > 0));
     HIPCHK(alloc_image(e, n_snp, n_org));
-    HIPCHK(hipMemcpy2DAsync(e->bed.p, (size_t)row_pitch(n_org), bed + 3, nb, nb, (size_t)n_snp, hipMemcpyHostToDevice,
-                            e->stream));
+    // rows go up in slices of ~64 MiB into a device staging buffer, then into the resident layout (load_rows_kernel);
+    // the stream orders each slice's kernel before the next copy over the same staging bytes
+    const size_t rows_per = std::max<size_t>(1, (size_t(64) << 20) / nb);
+    HIPCHK(e->stage_dev.ensure(std::min(rows_per, (size_t)n_snp) * nb));
+    for (size_t r0 = 0; r0 < (size_t)n_snp; r0 += rows_per) {
+        const size_t nr = std::min(rows_per, (size_t)n_snp - r0);
+        HIPCHK(hipMemcpyAsync(e->stage_dev.p, bed + 3 + r0 * nb, nr * nb, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(nldsc::launch_load_rows(e->stage_dev.p, (int)nb, (int)r0, (int)nr, e->bed.p, row_pitch(n_org), e->stream));
+    }
     HIPCHK(finish_image(e, n_snp, n_org));
+    e->stage_dev.release();
     return NLDSC_OK;
 }
 
@@ -371,8 +381,8 @@ int nldsc_engine_load_bed_device(nldsc_engine* e, const void* bed, size_t len, i
         return set_err(err, errlen, NLDSC_E_SIZE, "BED image too short: %zu bytes, expected at least %zu", len, need);
     const size_t nb = (size_t)(n_org / 4 + (n_org % 4 > 0));
     HIPCHK(alloc_image(e, n_snp, n_org));
-    HIPCHK(hipMemcpy2DAsync(e->bed.p, (size_t)row_pitch(n_org), static_cast<const uint8_t*>(bed) + 3, nb, nb,
-                            (size_t)n_snp, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(nldsc::launch_load_rows(static_cast<const uint8_t*>(bed) + 3, (int)nb, 0, n_snp, e->bed.p, row_pitch(n_org),
+                                   e->stream));
     HIPCHK(finish_image(e, n_snp, n_org));
     return NLDSC_OK;
 }
@@ -410,9 +420,8 @@ int nldsc_engine_load_bed_file_range(nldsc_engine* e, const char* path, int32_t 
     if (fsize < 0 || (size_t)fsize < need) return too_short(fsize < 0 ? 0 : (size_t)fsize);
     if (fseeko(f, (off_t)first, SEEK_SET) != 0) return too_short((size_t)fsize);
     HIPCHK(hipSetDevice(e->device));
-    // rows stream through two pinned 64 MiB slots: the read into one slot overlaps the H2D copy out of
-    // the other (an event per slot marks its copy done)
-    const size_t pitch = (size_t)row_pitch(n_org);
+    // rows stream through two pinned 64 MiB slots: the read into one slot overlaps the H2D copy out of the other
+    // into its device staging slot and the kernel that places the slot's rows (an event per slot marks both done)
     const size_t rows_per = std::max<size_t>(1, (size_t(64) << 20) / nb), CH = rows_per * nb;  // ~64 MiB of rows
     uint8_t* stage = nullptr;
     hipEvent_t done[2] = {nullptr, nullptr};
@@ -424,6 +433,7 @@ int nldsc_engine_load_bed_file_range(nldsc_engine* e, const char* path, int32_t 
     if (he == hipSuccess) he = hipEventCreateWithFlags(&done[1], hipEventDisableTiming);
     const int32_t n_snp = snp_end - snp_begin;
     if (he == hipSuccess) he = alloc_image(e, n_snp, n_org);
+    if (he == hipSuccess) he = e->stage_dev.ensure(2 * CH);
     bool pending[2] = {false, false};
     size_t off = 0, short_at = 0;
     bool short_read = false;
@@ -438,8 +448,11 @@ int nldsc_engine_load_bed_file_range(nldsc_engine* e, const char* path, int32_t 
             short_at = first + off + r;
             break;
         }
-        he = hipMemcpy2DAsync(e->bed.p + (off / nb) * pitch, pitch, buf, nb, nb, n / nb, hipMemcpyHostToDevice,
-                              e->stream);
+        uint8_t* dslot = e->stage_dev.p + (size_t)slot * CH;
+        he = hipMemcpyAsync(dslot, buf, n, hipMemcpyHostToDevice, e->stream);
+        if (he == hipSuccess)
+            he = nldsc::launch_load_rows(dslot, (int)nb, (int)(off / nb), (int)(n / nb), e->bed.p, row_pitch(n_org),
+                                         e->stream);
         if (he == hipSuccess) he = hipEventRecord(done[slot], e->stream);
         pending[slot] = true;
         off += n;
@@ -449,6 +462,7 @@ int nldsc_engine_load_bed_file_range(nldsc_engine* e, const char* path, int32_t 
     for (hipEvent_t ev : done)
         if (ev) (void)hipEventDestroy(ev);
     (void)hipHostFree(stage);
+    e->stage_dev.release();
     if (short_read) return too_short(short_at);
     std::fclose(f);
     if (he != hipSuccess) return set_err(err, errlen, NLDSC_E_HIP, "HIP error %s loading BED", hipGetErrorString(he));

@@ -22,7 +22,11 @@ struct SnpConst {
     double isa, is;
 };
 
-// resident rows: after a load, save each row's last byte and fill the pitch padding (rows >= n_snp all 0x55)
+// resident rows (block-interleaved, ld_kernels.hip tile_off): rows [row0, row0 + n_rows) of a .bed image (row r of nb
+// bytes at src + r * nb) into place, with the pitch padding as 0x55
+hipError_t launch_load_rows(const uint8_t* src, int nb, int row0, int n_rows, uint8_t* img, int row_bytes,
+                            hipStream_t st);
+// after a load, save each row's last byte (rows >= n_snp all 0x55)
 hipError_t launch_pad_rows(uint8_t* img, uint8_t* last, int n_snp, int n_rows, int nb, int row_bytes,
                            hipStream_t st);
 // per run: set each row's non-individual slots (last byte outside tail_keep, pitch padding) to `pad`

@@ -31,13 +31,26 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // ------------------------------------------------------------------------------------------
 // 1. resident row layout + per-run count
 // ------------------------------------------------------------------------------------------
-// The engine keeps the .bed rows in HBM at a pitch of row_bytes = ceil(nb / 64) * 64 (the loaders
-// place them there with pitched copies, so nothing is repacked per run).  Byte p of a row keeps the
-// .bed byte (4 samples, first sample in bits 7:6 per the reference's unpack order — any fixed slot
-// order is fine for dot products as long as every SNP uses the same one).  Bytes past the row are
-// 01 pairs ("missing"), and each run rewrites the last byte from its saved original so that only the
-// bit pairs that are individuals for that run's order (reference: high pairs first; PLINK: low
-// pairs) stay and the rest read as missing — which contributes nothing to any dot product.
+// Resident layout ("block-interleaved rows").  A row is the .bed row of nb = ceil(N / 4) bytes padded to
+// row_bytes = ceil(nb / 64) * 64; the rows of each 32-SNP block b are interleaved in 32-byte chunks: byte k of chunk
+// t of row 32 b + i sits at (b * 32 * row_bytes) + t * 1024 + i * 32 + k (tile_off).  One chunk of a block — what a
+// band wave consumes per K step pair, 32 rows x 128 samples — is then 1 KiB contiguous (eight whole 128-byte lines)
+// instead of 32 pieces of 32 bytes a row pitch apart, whose lines the band kernels fetched from L2 up to four times
+// (C2 band -18 %, C3 -3.5 %, C5 -6 % measured against the row-major layout: profiles/r03_ab_tiled_layout.json).
+// Byte p of a row keeps the .bed byte (4 samples, first sample in bits 7:6 per the reference's unpack order — any
+// fixed slot order is fine for dot products as long as every SNP uses the same one).  Bytes past the row are 01 pairs
+// ("missing"), and each run rewrites the last byte from its saved original so that only the bit pairs that are
+// individuals for that run's order (reference: high pairs first; PLINK: low pairs) stay and the rest read as missing
+// — which contributes nothing to any dot product.  Rows past n_snp (the last block's padding) are all 0x55.
+__device__ __forceinline__ size_t tile_off(int r, int b, int row_bytes) {
+    return (size_t)(r >> 5) * 32 * (size_t)row_bytes + (size_t)(b >> 5) * 1024 + (size_t)(r & 31) * 32 + (b & 31);
+}
+// the band kernels' view: uint4 index of row r's chunk 0 (a lane's half h adds h) and the uint4 stride of chunks
+constexpr int CHUNK_U4 = 64;
+__device__ __forceinline__ size_t row_u4(int r, int pitch_words) {
+    return (size_t)(r >> 5) * 8 * (size_t)pitch_words + (size_t)(r & 31) * 2;
+}
+
 __device__ __forceinline__ void count_codes(uint32_t word, int& c0, int& c1, int& c2) {
     const uint32_t hi = (word >> 1) & 0x55555555u, lo = word & 0x55555555u;
     c0 += __popc(~hi & ~lo & 0x55555555u);  // 00 hom A1
@@ -45,18 +58,66 @@ __device__ __forceinline__ void count_codes(uint32_t word, int& c0, int& c1, int
     c2 += __popc(hi & lo);                  // 11 hom A2
 }
 
-// After a load: save every row's last byte and fill the padding bytes [nb, row_bytes) with 0x55;
-// rows [n_snp, n_rows) (the last 32-SNP block's padding SNPs) are all 0x55.  One thread per row.
+// Loads: rows [row0, row0 + n_rows) of a .bed image (src: row r at r * nb bytes, any alignment) into the resident
+// layout, the pitch padding [nb, row_bytes) as 0x55.  One thread per 16-byte unit, in source order (coalesced byte
+// reads; each thread writes one whole 16-byte unit).
+__global__ void __launch_bounds__(256) load_rows_kernel(const uint8_t* __restrict__ src, int nb, int row0, int n_rows,
+                                                        uint8_t* __restrict__ img, int row_bytes) {
+    const int units = row_bytes >> 4;
+    const size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= (size_t)n_rows * units) return;
+    const int r = (int)(g / units), u = (int)(g % units);
+    const uint8_t* s = src + (size_t)r * nb;
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int p = 16 * u + 4 * q + k;
+            v |= (uint32_t)(p < nb ? s[p] : 0x55u) << (8 * k);
+        }
+        w[q] = v;
+    }
+    *reinterpret_cast<uint4*>(img + tile_off(row0 + r, 16 * u, row_bytes)) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// After a load: save every row's last byte; rows [n_snp, n_rows) (the last 32-SNP block's padding SNPs) all 0x55.
+// One thread per row.
 __global__ void pad_rows_kernel(uint8_t* __restrict__ img, uint8_t* __restrict__ last, int n_snp, int n_rows, int nb,
                                 int row_bytes) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_rows) return;
-    uint8_t* row = img + (size_t)j * (size_t)row_bytes;
     if (j < n_snp) {
-        last[j] = row[nb - 1];
-        for (int p = nb; p < row_bytes; ++p) row[p] = 0x55;
+        last[j] = img[tile_off(j, nb - 1, row_bytes)];
     } else {
-        for (int p = 0; p < row_bytes; ++p) row[p] = 0x55;
+        const uint4 m = make_uint4(0x55555555u, 0x55555555u, 0x55555555u, 0x55555555u);
+        for (int p = 0; p < row_bytes; p += 16) *reinterpret_cast<uint4*>(img + tile_off(j, p, row_bytes)) = m;
+    }
+}
+
+// Block sweeps of the resident layout: a workgroup of 4 waves takes 32-SNP block b; per chunk t a wave reads the
+// chunk's 1 KiB with one 16-byte load per lane — lane l always lands on row l / 2 (half l % 2 of its 32 bytes), so
+// per-row sums stay in the lane and meet its partner's (l ^ 1) and the other waves' at the end.  Wave w takes chunks
+// t = w, w + 4, ... of [t_lo, t_hi).
+struct BlockRed {
+    int v[4][32][3];
+};
+// sums c[0..2] of lanes l and l ^ 1 (one row), then over the 4 waves: row i's totals on thread i (< 32) in out[]
+__device__ __forceinline__ void block_row_sums(BlockRed& sh, const int (&c)[3], int (&out)[3]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int t[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t[k] = c[k] + __shfl_xor(c[k], 1, 64);
+    if ((lane & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sh.v[w][lane >> 1][k] = t[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) out[k] = sh.v[0][threadIdx.x][k] + sh.v[1][threadIdx.x][k] + sh.v[2][threadIdx.x][k] +
+                                             sh.v[3][threadIdx.x][k];
     }
 }
 
@@ -65,45 +126,53 @@ __global__ void pad_rows_kernel(uint8_t* __restrict__ img, uint8_t* __restrict__
 // missing 01 unchanged; the saved last byte too) and flip[j] = 1.  The exact kernels' operands are then
 // mostly zero whatever the file's allele order (PLINK usually writes A1 = minor, so A2 = major), which
 // keeps the matrix cores' power, and the chip's clock, where the synthetic A2-minor data has it.
+// One workgroup per block: count every byte of the rows, then swap the rows that need it.
 __global__ void __launch_bounds__(256) orient_rows_kernel(uint8_t* __restrict__ img, uint8_t* __restrict__ last,
                                                           int n_snp, int row_bytes, uint8_t* __restrict__ flip) {
-    const int j = blockIdx.x;
-    if (j >= n_snp) return;
-    uint32_t* row = reinterpret_cast<uint32_t*>(img + (size_t)j * (size_t)row_bytes);
-    const int n_words = row_bytes / 4;
-    int c0 = 0, c1 = 0, c2 = 0;
-    for (int w = threadIdx.x; w < n_words; w += blockDim.x) count_codes(row[w], c0, c1, c2);
-    for (int o = 32; o > 0; o >>= 1) {
-        c0 += __shfl_down(c0, o, 64);
-        c2 += __shfl_down(c2, o, 64);
+    __shared__ BlockRed red;
+    __shared__ int swap[32];
+    const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int n_ch = row_bytes >> 5, j = 32 * b + (lane >> 1);
+    uint4* blk = reinterpret_cast<uint4*>(img + (size_t)b * 32 * (size_t)row_bytes);
+    int c[3] = {0, 0, 0};
+    for (int t = w; t < n_ch; t += 4) {
+        const uint4 v = blk[(size_t)t * 64 + lane];
+        count_codes(v.x, c[0], c[1], c[2]);
+        count_codes(v.y, c[0], c[1], c[2]);
+        count_codes(v.z, c[0], c[1], c[2]);
+        count_codes(v.w, c[0], c[1], c[2]);
     }
-    __shared__ int red[2][4];
-    __shared__ int swap;
-    const int wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { red[0][wv] = c0; red[1][wv] = c2; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int a = 0, b = 0;
-        for (int q = 0; q < (int)(blockDim.x >> 6); ++q) { a += red[0][q]; b += red[1][q]; }
-        swap = b > a;
-        flip[j] = (uint8_t)swap;
-        if (swap) {
-            const uint32_t lb = last[j], t = ~(lb ^ (lb >> 1)) & 0x55u;
-            last[j] = (uint8_t)(lb ^ (t | (t << 1)));
+    int tot[3];
+    block_row_sums(red, c, tot);
+    if (threadIdx.x < 32) {
+        const int jj = 32 * b + threadIdx.x;
+        const int sw = jj < n_snp && tot[2] > tot[0];
+        swap[threadIdx.x] = sw;
+        if (jj < n_snp) {
+            flip[jj] = (uint8_t)sw;
+            if (sw) {
+                const uint32_t lb = last[jj], q = ~(lb ^ (lb >> 1)) & 0x55u;
+                last[jj] = (uint8_t)(lb ^ (q | (q << 1)));
+            }
         }
     }
     __syncthreads();
-    if (!swap) return;
-    for (int w = threadIdx.x; w < n_words; w += blockDim.x) {
-        const uint32_t v = row[w], t = ~(v ^ (v >> 1)) & 0x55555555u;  // pairs 00 or 11
-        row[w] = v ^ (t | (t << 1));
+    if (j >= n_snp || !swap[lane >> 1]) return;
+    auto sw4 = [](uint32_t v) {
+        const uint32_t q = ~(v ^ (v >> 1)) & 0x55555555u;  // pairs 00 or 11
+        return v ^ (q | (q << 1));
+    };
+    for (int t = w; t < n_ch; t += 4) {
+        const uint4 v = blk[(size_t)t * 64 + lane];
+        blk[(size_t)t * 64 + lane] = make_uint4(sw4(v.x), sw4(v.y), sw4(v.z), sw4(v.w));
     }
 }
 
 // After a load: which rows hold a missing call (code 01) among the individual slots of each sample order —
 // row_miss[j] bit 0 for the reference's order (the last byte keeps its high N % 4 pairs), bit 1 for PLINK's (the low
 // pairs); the other slots of the last byte and the pitch padding are not individuals.  It does not depend on the run's
-// parameters, so the fp4 band's routing (blk_miss) is known before the per-run count kernel finishes.
+// parameters, so the fp4 band's routing (blk_miss) is known before the per-run count kernel finishes.  One workgroup
+// per block; bytes [0, nb - 1) in the sweep, the last byte from its saved copy.
 __device__ __forceinline__ int count_missing(uint32_t word) {
     return __popc(~(word >> 1) & word & 0x55555555u);  // pairs 01
 }
@@ -111,18 +180,31 @@ __global__ void __launch_bounds__(256) row_missing_kernel(const uint8_t* __restr
                                                           const uint8_t* __restrict__ last, int n_snp, int nb,
                                                           int row_bytes, uint32_t keep_compat, uint32_t keep_strict,
                                                           uint8_t* __restrict__ row_miss) {
-    const int j = blockIdx.x;
-    if (j >= n_snp) return;
-    const uint8_t* row = img + (size_t)j * (size_t)row_bytes;
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(row);
-    const int full_words = (nb - 1) / 4;  // whole words before the last byte
-    int m = 0;
-    for (int q = threadIdx.x; q < full_words; q += blockDim.x) m += count_missing(w[q]);
-    for (int p = 4 * full_words + threadIdx.x; p < nb - 1; p += blockDim.x) m += count_missing(row[p]);
-    m = __syncthreads_or(m);
-    if (threadIdx.x == 0) {
+    __shared__ BlockRed red;
+    const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int h = lane & 1;
+    const uint4* blk = reinterpret_cast<const uint4*>(img + (size_t)b * 32 * (size_t)row_bytes);
+    const int n_full = (nb - 1) >> 5;  // chunks wholly before the last byte
+    int c[3] = {0, 0, 0};
+    for (int t = w; t < n_full; t += 4) {
+        const uint4 v = blk[(size_t)t * 64 + lane];
+        c[0] += count_missing(v.x) + count_missing(v.y) + count_missing(v.z) + count_missing(v.w);
+    }
+    if (w == 0 && 32 * n_full < nb - 1) {  // the chunk holding the last byte: its bytes before it
+        const uint4 v = blk[(size_t)n_full * 64 + lane];
+        const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (32 * n_full + 16 * h + 4 * q + k < nb - 1) c[0] += count_missing((wd[q] >> (8 * k)) & 0xFFu);
+    }
+    int tot[3];
+    block_row_sums(red, c, tot);
+    const int j = 32 * b + threadIdx.x;
+    if (threadIdx.x < 32 && j < n_snp) {
         const uint32_t lb = last[j];
-        const int mc = m | count_missing(lb & keep_compat), ms = m | count_missing(lb & keep_strict);
+        const int mc = tot[0] | count_missing(lb & keep_compat), ms = tot[0] | count_missing(lb & keep_strict);
         row_miss[j] = (uint8_t)((mc ? 1 : 0) | (ms ? 2 : 0));
     }
 }
@@ -137,68 +219,72 @@ __global__ void block_missing_rows_kernel(const uint8_t* __restrict__ row_miss, 
     blk_miss[b] = m;
 }
 
-// Per run: genotype-code counts of every row (one workgroup per SNP, 16-byte non-temporal loads, 8 in
-// flight per thread) after setting the row's non-individual slots — the last byte's bit pairs that are
-// not individuals for this run's sample order, (saved byte & keep) | (pad & ~keep), and the pitch padding
-// — to this run's pad code: 0x55 ("missing": x = h = o = 0 for the int8 / fp32 kernels) or 0x00 for the
-// fp4 kernel, whose missing-indicator plane m must be 0 there so that SNPs without missing calls have
-// an all-zero m plane (their m products are skipped); its epilogue counts o = 1 - m over the n_org
-// individual slots only.  The chunks before the last byte's are counted in the loop; after the barrier
-// one thread rebuilds, writes and counts the tail chunks, discounting 00-coded padding (n_pad00 slots).
+// Per run: genotype-code counts of every row after setting the row's non-individual slots — the last byte's bit
+// pairs that are not individuals for this run's sample order, (saved byte & keep) | (pad & ~keep), and the pitch
+// padding — to this run's pad code: 0x55 ("missing": x = h = o = 0 for the int8 / fp32 kernels) or 0x00 for the
+// fp4 kernel, whose missing-indicator plane m must be 0 there so that SNPs without missing calls have an all-zero m
+// plane (their m products are skipped); its epilogue counts o = 1 - m over the n_org individual slots.
+// Grid: (block, part): part p of P sweeps chunks [p n_tail / P, (p + 1) n_tail / P) of the chunks before the last
+// byte's (16-byte non-temporal loads, 8 in flight per lane); part P - 1's wave 0 also rebuilds, writes and counts the
+// tail chunks (the last byte's and the padding after it), discounting 00-coded padding (n_pad00 slots).  Partial
+// counts go to `counts` (zeroed first) by atomics.
 typedef uint32_t u32x4nt __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void count_chunk(const u32x4nt o, int& c0, int& c1, int& c2) {
-    count_codes(o.x, c0, c1, c2);
-    count_codes(o.y, c0, c1, c2);
-    count_codes(o.z, c0, c1, c2);
-    count_codes(o.w, c0, c1, c2);
+__device__ __forceinline__ void count_chunk(const u32x4nt o, int (&c)[3]) {
+    count_codes(o.x, c[0], c[1], c[2]);
+    count_codes(o.y, c[0], c[1], c[2]);
+    count_codes(o.z, c[0], c[1], c[2]);
+    count_codes(o.w, c[0], c[1], c[2]);
 }
 
 __global__ void __launch_bounds__(256) count_rows_kernel(uint8_t* __restrict__ img, const uint8_t* __restrict__ last,
                                                          int n_snp, int nb, int row_bytes, uint32_t tail_keep,
-                                                         uint32_t pad, int n_pad00, int* __restrict__ counts) {
-    const int j = blockIdx.x;
-    if (j >= n_snp) return;
-    uint8_t* row = img + (size_t)j * (size_t)row_bytes;
-    const u32x4nt* src = reinterpret_cast<const u32x4nt*>(row);
-    const int c_last = (nb - 1) / 16, T = blockDim.x;
-    int c0 = 0, c1 = 0, c2 = 0;
-    int c = threadIdx.x;
-    for (; c + 7 * T < c_last; c += 8 * T) {
+                                                         uint32_t pad, int n_pad00, int P, int* __restrict__ counts) {
+    __shared__ BlockRed red;
+    const int b = blockIdx.x / P, part = blockIdx.x % P, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int h = lane & 1, j = 32 * b + (lane >> 1);
+    uint8_t* bbase = img + (size_t)b * 32 * (size_t)row_bytes;
+    const u32x4nt* blk = reinterpret_cast<const u32x4nt*>(bbase);
+    const int n_ch = row_bytes >> 5, tc0 = (nb - 1) >> 5;  // chunks [tc0, n_ch) hold the last byte and padding
+    const int t_lo = (int)((long long)tc0 * part / P), t_hi = (int)((long long)tc0 * (part + 1) / P);
+    int c[3] = {0, 0, 0};
+    int t = t_lo + w;
+    for (; t + 28 < t_hi; t += 32) {
         u32x4nt v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(src + c + u * T);
+        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(blk + (size_t)(t + 4 * u) * 64 + lane);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) count_chunk(v[u], c0, c1, c2);
+        for (int u = 0; u < 8; ++u) count_chunk(v[u], c);
     }
-    for (; c < c_last; c += T) count_chunk(__builtin_nontemporal_load(src + c), c0, c1, c2);
-    // block reduction (4 waves of 64)
-    for (int o = 32; o > 0; o >>= 1) {
-        c0 += __shfl_down(c0, o, 64);
-        c1 += __shfl_down(c1, o, 64);
-        c2 += __shfl_down(c2, o, 64);
-    }
-    __shared__ int red[3][4];
-    const int wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { red[0][wv] = c0; red[1][wv] = c1; red[2][wv] = c2; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int s0 = 0, s1 = 0, s2 = 0;
-        for (int q = 0; q < (int)(blockDim.x >> 6); ++q) { s0 += red[0][q]; s1 += red[1][q]; s2 += red[2][q]; }
+    for (; t < t_hi; t += 4) count_chunk(__builtin_nontemporal_load(blk + (size_t)t * 64 + lane), c);
+    if (part == P - 1 && w == 0 && j < n_snp) {
         const uint32_t lb = ((uint32_t)last[j] & tail_keep) | (pad & ~tail_keep & 0xFFu);
-        uint32_t* w = reinterpret_cast<uint32_t*>(row);
-        for (int q = 4 * c_last; q < row_bytes / 4; ++q) {  // the tail chunks, word by word
-            uint32_t v = 0;
-            for (int k = 0; k < 4; ++k) {
-                const int p = 4 * q + k;
-                const uint32_t byte = p < nb - 1 ? row[p] : p == nb - 1 ? lb : (pad & 0xFFu);
-                v |= byte << (8 * k);
+        for (int tt = tc0; tt < n_ch; ++tt) {
+            uint4* unit = reinterpret_cast<uint4*>(bbase + (size_t)tt * 1024 + (size_t)(lane >> 1) * 32 + 16 * h);
+            const uint4 v = *unit;
+            uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t o = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int p = 32 * tt + 16 * h + 4 * q + k;
+                    const uint32_t byte = p < nb - 1 ? (wd[q] >> (8 * k)) & 0xFFu : p == nb - 1 ? lb : (pad & 0xFFu);
+                    o |= byte << (8 * k);
+                }
+                wd[q] = o;
+                count_codes(o, c[0], c[1], c[2]);
             }
-            w[q] = v;
-            count_codes(v, s0, s1, s2);
+            *unit = make_uint4(wd[0], wd[1], wd[2], wd[3]);
         }
-        counts[(size_t)j * 4 + 0] = s0 - n_pad00;
-        counts[(size_t)j * 4 + 1] = s1;
-        counts[(size_t)j * 4 + 2] = s2;
+        if (h == 0) c[0] -= n_pad00;
+    }
+    int tot[3];
+    block_row_sums(red, c, tot);
+    const int jj = 32 * b + threadIdx.x;
+    if (threadIdx.x < 32 && jj < n_snp) {
+        atomicAdd(counts + (size_t)jj * 4 + 0, tot[0]);
+        atomicAdd(counts + (size_t)jj * 4 + 1, tot[1]);
+        atomicAdd(counts + (size_t)jj * 4 + 2, tot[2]);
     }
 }
 
@@ -348,10 +434,19 @@ struct RefPass {
     bool two_dots, two_means, means;
 };
 
+// One resident row in the block-interleaved layout (tile_off): 16-byte vector v and byte k of the row.
+struct TiledRow {
+    const uint8_t* base;  // the row's bytes of chunk 0
+    __device__ __forceinline__ uint4 u4(int v) const {
+        return *reinterpret_cast<const uint4*>(base + (size_t)(v >> 1) * 1024 + 16 * (v & 1));
+    }
+    __device__ __forceinline__ uint32_t byte(int k) const { return base[(size_t)(k >> 5) * 1024 + (k & 31)]; }
+};
+
 // One pass over the n samples of `row` in the reference's order; codes are read as stored (values are given per
 // stored code, the file's coding folded in).  Returns the lane's sdot accumulators (x.y, u.v) and, on lanes 0-3,
 // its mean accumulator.
-__device__ void ref_pass(const uint8_t* row, int n, int row_bytes, bool strict, const RefPass& P, uint32_t* buf,
+__device__ void ref_pass(const TiledRow row, int n, int row_bytes, bool strict, const RefPass& P, uint32_t* buf,
                          float2* tab, float& acc_d, float& acc_e, float& acc_m) {
 #pragma clang fp contract(off)
     const int lane = threadIdx.x & 63;
@@ -368,12 +463,11 @@ __device__ void ref_pass(const uint8_t* row, int n, int row_bytes, bool strict, 
     }
     const int n64 = (n & -32) & ~63;
     const int n_bytes = (n + 3) >> 2;
-    const uint4* src = reinterpret_cast<const uint4*>(row);
     const int n_vec = row_bytes >> 4;  // 16-byte vectors in the row (never read past it)
     constexpr int PER = REF_CHUNK / 16 / 64;  // 16-byte vectors per lane per chunk
     uint4 nxt[PER];
 #pragma unroll
-    for (int u = 0; u < PER; ++u) nxt[u] = (u * 64 + lane < n_vec) ? src[u * 64 + lane] : make_uint4(0, 0, 0, 0);
+    for (int u = 0; u < PER; ++u) nxt[u] = (u * 64 + lane < n_vec) ? row.u4(u * 64 + lane) : make_uint4(0, 0, 0, 0);
     const int par = lane & 1;
     const Vals4 M = lane < 2 ? P.mv : P.mw;  // the tail samples
     const bool my_mean = P.means && (lane < 2 || (P.two_means && lane < 4));
@@ -386,7 +480,7 @@ __device__ void ref_pass(const uint8_t* row, int n, int row_bytes, bool strict, 
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int v = (b1 >> 4) + u * 64 + lane;
-            nxt[u] = (b1 < n_bytes && v < n_vec) ? src[v] : make_uint4(0, 0, 0, 0);
+            nxt[u] = (b1 < n_bytes && v < n_vec) ? row.u4(v) : make_uint4(0, 0, 0, 0);
         }
         const uint8_t* bb = reinterpret_cast<const uint8_t*>(buf);
         // sdots: sample t = 4 b0 + 64 s + lane, byte 16 s + lane / 4
@@ -424,10 +518,10 @@ __device__ void ref_pass(const uint8_t* row, int n, int row_bytes, bool strict, 
 // the lanes' sdot accumulators -> arma::dot (oracle/ldscore_oracle.c dot_f): lanes folded (k, k + 8), one
 // 32-sample FMA step if n1 % 64 = 32, summed, then the tail in double.  n <= 32: Armadillo's two FMA
 // accumulators.  On every lane.
-__device__ float ref_dot_finish(const uint8_t* row, int n, bool strict, float acc, Vals4 X, Vals4 Y, float* sh) {
+__device__ float ref_dot_finish(const TiledRow row, int n, bool strict, float acc, Vals4 X, Vals4 Y, float* sh) {
 #pragma clang fp contract(off)
     const int lane = threadIdx.x & 63;
-    auto code = [&](int t) { return (row[t >> 2] >> (strict ? 2 * (t & 3) : 6 - 2 * (t & 3))) & 3; };
+    auto code = [&](int t) { return (int)((row.byte(t >> 2) >> (strict ? 2 * (t & 3) : 6 - 2 * (t & 3))) & 3); };
     __syncthreads();
     sh[lane] = acc;
     __syncthreads();
@@ -509,7 +603,7 @@ __global__ void __launch_bounds__(64) reference_residual_kernel(const uint8_t* _
     __shared__ uint32_t buf[REF_CHUNK / 4];
     __shared__ float2 tab[4 * 256];
     __shared__ float sh[72];
-    const uint8_t* row = img + (size_t)j * (size_t)row_bytes;
+    const TiledRow row{img + tile_off(j, 0, row_bytes)};
     const bool st = strict != 0;
     const double nn = (double)n_org, n_obs = (double)(c0 + c1 + c2);
     // per STORED code (00, 01, 10, 11): the file's code is 3, 1, 2, 0 when the row is stored flipped
@@ -929,11 +1023,10 @@ __device__ __forceinline__ void band_body(BandLds& sh, const int4 it, const uint
         }
     }
 
-    const uint4* rowp = reinterpret_cast<const uint4*>(geno + (size_t)(I * 32 + i) * (size_t)pitch_words) + h;
+    const uint4* rowp = reinterpret_cast<const uint4*>(geno) + row_u4(I * 32 + i, pitch_words) + h;
     const uint4* colp[NC];
 #pragma unroll
-    for (int b = 0; b < NC; ++b)
-        colp[b] = reinterpret_cast<const uint4*>(geno + (size_t)((J0 + b) * 32 + i) * (size_t)pitch_words) + h;
+    for (int b = 0; b < NC; ++b) colp[b] = reinterpret_cast<const uint4*>(geno) + row_u4((J0 + b) * 32 + i, pitch_words) + h;
 
     const char* tabc = reinterpret_cast<const char*>(&tab[0][0]);
     const uint32_t rbase = (uint32_t)i * 8u;
@@ -951,9 +1044,9 @@ __device__ __forceinline__ void band_body(BandLds& sh, const int4 it, const uint
 #pragma unroll
         for (int b = 0; b < NC; ++b) wc4[b] = nc[b];
         if (t + 1 < n_it) {  // prefetch the next 32-byte chunk of every row
-            nr = rowp[2 * (t + 1)];
+            nr = rowp[CHUNK_U4 * (t + 1)];
 #pragma unroll
-            for (int b = 0; b < NC; ++b) nc[b] = colp[b][2 * (t + 1)];
+            for (int b = 0; b < NC; ++b) nc[b] = colp[b][CHUNK_U4 * (t + 1)];
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1251,11 +1344,10 @@ __device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const
     for (int b = 0; b < NC; ++b) {
         gxx[b] = gxo[b] = gox[b] = goo[b] = gxh[b] = goh[b] = ghx[b] = gho[b] = i32x16{};
     }
-    const uint4* rowp = reinterpret_cast<const uint4*>(geno + (size_t)(I * 32 + i) * (size_t)pitch_words) + h;
+    const uint4* rowp = reinterpret_cast<const uint4*>(geno) + row_u4(I * 32 + i, pitch_words) + h;
     const uint4* colp[NC];
 #pragma unroll
-    for (int b = 0; b < NC; ++b)
-        colp[b] = reinterpret_cast<const uint4*>(geno + (size_t)((J0 + b) * 32 + i) * (size_t)pitch_words) + h;
+    for (int b = 0; b < NC; ++b) colp[b] = reinterpret_cast<const uint4*>(geno) + row_u4((J0 + b) * 32 + i, pitch_words) + h;
     auto word_of = [](const uint4& w, int q) { return q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w; };
     uint4 wr4 = rowp[0], wc4[NC];
 #pragma unroll
@@ -1270,9 +1362,9 @@ __device__ __forceinline__ void band_i8_body(BandI8Lds& sh, const int4 it, const
 #pragma unroll
         for (int b = 0; b < NC; ++b) ncl[b] = wc4[b];
         if (t + 1 < n_it) {
-            nr = rowp[2 * (t + 1)];
+            nr = rowp[CHUNK_U4 * (t + 1)];
 #pragma unroll
-            for (int b = 0; b < NC; ++b) ncl[b] = colp[b][2 * (t + 1)];
+            for (int b = 0; b < NC; ++b) ncl[b] = colp[b][CHUNK_U4 * (t + 1)];
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1451,11 +1543,10 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     f32x16v gxx[NC], gxo[NC], gox[NC], goo[NC], gxh[NC], goh[NC], ghx[NC], gho[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) gxx[c] = gxo[c] = gox[c] = goo[c] = gxh[c] = goh[c] = ghx[c] = gho[c] = f32x16v{};
-    const uint4* rowp = reinterpret_cast<const uint4*>(geno + (size_t)(I * 32 + i) * (size_t)pitch_words) + h;
+    const uint4* rowp = reinterpret_cast<const uint4*>(geno) + row_u4(I * 32 + i, pitch_words) + h;
     const uint4* colp[NC];
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
-        colp[c] = reinterpret_cast<const uint4*>(geno + (size_t)((J0 + c) * 32 + i) * (size_t)pitch_words) + h;
+    for (int c = 0; c < NC; ++c) colp[c] = reinterpret_cast<const uint4*>(geno) + row_u4((J0 + c) * 32 + i, pitch_words) + h;
     // RM / CM: the row / column block holds missing calls.  A block without any has an all-zero m plane,
     // so the products with it are skipped (imputed hard calls: 3 of the 8 MFMAs remain).
     auto mfmas_v = [&](const F4Frag& a, const F4Frag (&b)[NC], auto RMc, auto CMc) {
@@ -1498,9 +1589,9 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     auto kloop = [&](auto RMc, auto CMc, const int t_lo, const int t_hi) {
         constexpr bool RM = decltype(RMc)::value, CM = decltype(CMc)::value;
         const int last = t_hi - 1;
-        uint4 pr = rowp[2 * t_lo], qr = rowp[2 * t_lo + 2], pc[NC], qc[NC];
+        uint4 pr = rowp[CHUNK_U4 * t_lo], qr = rowp[CHUNK_U4 * (t_lo + 1)], pc[NC], qc[NC];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) { pc[c] = colp[c][2 * t_lo]; qc[c] = colp[c][2 * t_lo + 2]; }
+        for (int c = 0; c < NC; ++c) { pc[c] = colp[c][CHUNK_U4 * t_lo]; qc[c] = colp[c][CHUNK_U4 * (t_lo + 1)]; }
         // two named fragment sets: set 1 is decoded while set 0 feeds the MFMAs and vice versa, so no
         // fragment is copied (a single rotating set costs ~12 v_mov per K step)
         F4Frag a0 = decode_f4<RM>(pr.x, pr.y), a1, b0[NC], b1[NC];
@@ -1511,9 +1602,9 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
 #pragma unroll
             for (int c = 0; c < NC; ++c) b1[c] = decode_f4<CM>(pc[c].z, pc[c].w);
             mfmas_v(a0, b0, RMc, CMc);  // K step 2t   (chunk t, words 0-1)
-            pr = rowp[2 * min(t + 2, last)];
+            pr = rowp[CHUNK_U4 * min(t + 2, last)];
 #pragma unroll
-            for (int c = 0; c < NC; ++c) pc[c] = colp[c][2 * min(t + 2, last)];
+            for (int c = 0; c < NC; ++c) pc[c] = colp[c][CHUNK_U4 * min(t + 2, last)];
             a0 = decode_f4<RM>(qr.x, qr.y);
 #pragma unroll
             for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(qc[c].x, qc[c].y);
@@ -1522,9 +1613,9 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
 #pragma unroll
             for (int c = 0; c < NC; ++c) b1[c] = decode_f4<CM>(qc[c].z, qc[c].w);
             mfmas_v(a0, b0, RMc, CMc);  // K step 2t+2 (chunk t+1, words 0-1)
-            qr = rowp[2 * min(t + 3, last)];
+            qr = rowp[CHUNK_U4 * min(t + 3, last)];
 #pragma unroll
-            for (int c = 0; c < NC; ++c) qc[c] = colp[c][2 * min(t + 3, last)];
+            for (int c = 0; c < NC; ++c) qc[c] = colp[c][CHUNK_U4 * min(t + 3, last)];
             a0 = decode_f4<RM>(pr.x, pr.y);
 #pragma unroll
             for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(pc[c].x, pc[c].y);
@@ -1783,7 +1874,7 @@ __global__ void __launch_bounds__(256, 2) band_f4_t2_kernel(
     const int sA = w >> 1, sB = dsup ? (w & 1) : 2 + (w & 1);
     const int my_blk = w == 0 ? b0 : w == 1 ? b1 : w == 2 ? b2 : b3;
     const bool loads = !(dsup && w >= 2);
-    const uint4* src = reinterpret_cast<const uint4*>(geno + (size_t)(my_blk * 32 + i) * (size_t)pitch_words) + h;
+    const uint4* src = reinterpret_cast<const uint4*>(geno) + row_u4(my_blk * 32 + i, pitch_words) + h;
     const int n_st = n_it >> 1;  // two-chunk stages (rows are padded to 64 bytes)
     // stage t (clamped to the last: the surplus loads of the tail rewrite the last stage's bytes into buffers no one
     // reads again) -> buffer t % S
@@ -1800,7 +1891,7 @@ __global__ void __launch_bounds__(256, 2) band_f4_t2_kernel(
                 asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
                              "s_mov_b32 m0, %0"
                              : "=&s"(keep)
-                             : "v"(src + 4 * tc + 2 * c), "s"(dst)
+                             : "v"(src + CHUNK_U4 * (2 * tc + c)), "s"(dst)
                              : "memory");
             }
         }
@@ -1955,10 +2046,8 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
     }
     // loads: wave w streams strips 2w, 2w + 1 (none for waves 2, 3 of a diagonal super-item)
     const bool loads = !(dsup && w >= 2);
-    const uint4* src0 = reinterpret_cast<const uint4*>(
-        geno + (size_t)(min(strip_blk(2 * w), nblk - 1) * 32 + i) * (size_t)pitch_words) + h;
-    const uint4* src1 = reinterpret_cast<const uint4*>(
-        geno + (size_t)(min(strip_blk(2 * w + 1), nblk - 1) * 32 + i) * (size_t)pitch_words) + h;
+    const uint4* src0 = reinterpret_cast<const uint4*>(geno) + row_u4(min(strip_blk(2 * w), nblk - 1) * 32 + i, pitch_words) + h;
+    const uint4* src1 = reinterpret_cast<const uint4*>(geno) + row_u4(min(strip_blk(2 * w + 1), nblk - 1) * 32 + i, pitch_words) + h;
     const int n_st = n_it >> 1;
     auto issue = [&](int t) {
         const int tc = min(t, n_st - 1);
@@ -1973,7 +2062,7 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
                     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
                                  "s_mov_b32 m0, %0"
                                  : "=&s"(keep)
-                                 : "v"((k ? src1 : src0) + 4 * tc + 2 * c), "s"(dst)
+                                 : "v"((k ? src1 : src0) + CHUNK_U4 * (2 * tc + c)), "s"(dst)
                                  : "memory");
                 }
         }
@@ -2396,11 +2485,26 @@ hipError_t launch_pad_rows(uint8_t* img, uint8_t* last, int n_snp, int n_rows, i
     return hipGetLastError();
 }
 
+hipError_t launch_load_rows(const uint8_t* src, int nb, int row0, int n_rows, uint8_t* img, int row_bytes,
+                            hipStream_t st) {
+    if (n_rows <= 0) return hipSuccess;
+    const size_t n = (size_t)n_rows * (size_t)(row_bytes / 16);
+    hipLaunchKernelGGL(load_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, nb, row0, n_rows,
+                       img, row_bytes);
+    return hipGetLastError();
+}
+
 hipError_t launch_count_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
                              uint32_t pad, int n_pad00, int* counts, hipStream_t st) {
     if (n_snp <= 0) return hipSuccess;
-    hipLaunchKernelGGL(count_rows_kernel, dim3(n_snp), dim3(256), 0, st, img, last, n_snp, nb, row_bytes, tail_keep,
-                       pad, n_pad00, counts);
+    hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * 4 * (size_t)n_snp, st);
+    if (e != hipSuccess) return e;
+    // parts per block: about 16 k workgroups in all (8 resident per CU: several rounds, small tails), at least 8
+    // chunks each
+    const int nblk = (n_snp + 31) / 32, tc0 = (nb - 1) >> 5;
+    const int P = std::max(1, std::min(std::max(tc0 / 8, 1), (16384 + nblk - 1) / nblk));
+    hipLaunchKernelGGL(count_rows_kernel, dim3(nblk * P), dim3(256), 0, st, img, last, n_snp, nb, row_bytes, tail_keep,
+                       pad, n_pad00, P, counts);
     return hipGetLastError();
 }
 
@@ -2435,7 +2539,7 @@ hipError_t launch_reference_residuals(const uint8_t* img, int row_bytes, int n_o
 hipError_t launch_row_missing(const uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes,
                               uint32_t keep_compat, uint32_t keep_strict, uint8_t* row_miss, hipStream_t st) {
     if (n_snp <= 0) return hipSuccess;
-    hipLaunchKernelGGL(row_missing_kernel, dim3(n_snp), dim3(256), 0, st, img, last, n_snp, nb, row_bytes, keep_compat,
+    hipLaunchKernelGGL(row_missing_kernel, dim3((n_snp + 31) / 32), dim3(256), 0, st, img, last, n_snp, nb, row_bytes, keep_compat,
                        keep_strict, row_miss);
     return hipGetLastError();
 }
@@ -2451,7 +2555,7 @@ hipError_t launch_block_missing_rows(const uint8_t* row_miss, int n_snp, int ord
 
 hipError_t launch_orient_rows(uint8_t* img, uint8_t* last, int n_snp, int row_bytes, uint8_t* flip, hipStream_t st) {
     if (n_snp <= 0) return hipSuccess;
-    hipLaunchKernelGGL(orient_rows_kernel, dim3(n_snp), dim3(256), 0, st, img, last, n_snp, row_bytes, flip);
+    hipLaunchKernelGGL(orient_rows_kernel, dim3((n_snp + 31) / 32), dim3(256), 0, st, img, last, n_snp, row_bytes, flip);
     return hipGetLastError();
 }
 

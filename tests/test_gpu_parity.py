@@ -755,9 +755,8 @@ def test_rare_variants_reference_residual(engine, mode, n_org, strict):
 def test_ksplit_equals_single_pass(engine, N, M, dom):
     """Launches too small to fill the GPU (a rank's shard) split every item's K loop into P pieces whose exact
     integer Gram tiles are summed by an epilogue kernel: every output is bitwise the single-pass one
-    ($NLDSC_KSPLIT=0), and both equal the fp64 truth."""
-    import os
-
+    ($NLDSC_KSPLIT=0), and both equal the fp64 truth.  Additive-only bands pair column blocks by default
+    ($NLDSC_F4_NC2), which takes no K-split: those runs here use single-block items ($NLDSC_F4_NC2=0)."""
     from nldsc_amd import synth
     from nldsc_amd.engine import Engine
     spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=6.0, seed=N + M, missing=0.02)
@@ -765,21 +764,17 @@ def test_ksplit_equals_single_pass(engine, N, M, dom):
     pos = synth.positions_cm(spec)
     flags = MODES["f4"] | _lib_flag("FLAG_EXACT_RARE") | (0 if dom else _lib_flag("FLAG_ADDITIVE_ONLY"))
     args = (1.0, 0.01, 1e-5, 1.0 / M, pos)
-    engine.load_bed_bytes(synth.bed_bytes(rows), M, N)
-    got = engine.run(*args, flags=flags)
-    assert engine.timings()["ksplit"] > 1
-    old = os.environ.get("NLDSC_KSPLIT")
-    os.environ["NLDSC_KSPLIT"] = "0"
-    try:
+
+    def fresh(split):
         with Engine(0) as e:
             e.load_bed_bytes(synth.bed_bytes(rows), M, N)
-            ref = e.run(*args, flags=flags)
-            assert e.timings()["ksplit"] == 1
-    finally:
-        if old is None:
-            os.environ.pop("NLDSC_KSPLIT")
-        else:
-            os.environ["NLDSC_KSPLIT"] = old
+            r = e.run(*args, flags=flags)
+            assert (e.timings()["ksplit"] > 1) == split
+            return r
+
+    def both():
+        return fresh(True), _env_run("NLDSC_KSPLIT", "0", lambda: fresh(False))
+    got, ref = both() if dom else _env_run("NLDSC_F4_NC2", "0", both)
     for k in got:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
     exp = O.run_f64(rows, N, *args)
@@ -948,7 +943,15 @@ def test_band_round_launches_bitwise_one_launch(engine, case):
     N >= 2^17, when the band has at least four rounds of items), with the partial last round K-split when the cost
     model prefers it, gives bitwise the results of one launch of all items ($NLDSC_BAND_ROUNDS=0): the per-SNP sums
     are order-independent fixed point, the K-split partial Gram tiles are exact integers, and every item runs once.
-    12 000 SNPs at 800 per cM, 1 % missing; a few SNPs against the exact truth."""
+    12 000 SNPs at 800 per cM, 1 % missing; a few SNPs against the exact truth.  The additive-only case runs
+    single-block items ($NLDSC_F4_NC2=0; its default column-block pairs halve the item count, here below four
+    rounds)."""
+    if not ROUND_CASES[case][3]:
+        return _env_run("NLDSC_F4_NC2", "0", lambda: _round_launch_case(case))
+    return _round_launch_case(case)
+
+
+def _round_launch_case(case):
     from nldsc_amd import synth
     from nldsc_amd.engine import Engine
     N, M, length, dom, tail = ROUND_CASES[case]

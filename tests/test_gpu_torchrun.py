@@ -67,3 +67,63 @@ def test_torchrun_whole_genome_two_ranks(tmp_path):
     for c in (1, 2, 3):
         _same_table(tmp_path / f"one_{c}.L2", tmp_path / f"two_{c}.L2")
     assert "ld rank 0" in p.stderr and "ld rank 1" in p.stderr  # each rank reports its own chromosomes
+
+
+RCCL_SCRIPT = r'''
+import json, os, sys
+sys.path.insert(0, {repo!r})
+import numpy as np
+import torch
+import torch.distributed as dist
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", device_id=torch.device("cuda:0"))
+from nldsc_amd import distributed as D
+from nldsc_amd.ldscore import _ldscore as lds
+from nldsc_amd.ldscore.common import PLINKFile
+bed, bim, fam = PLINKFile.parse({bfile!r})
+pos = np.asarray(bim.cm, dtype=np.float64)
+full = D.calculate_sharded_device(bed.data, bim.n_snp, fam.n_org, 1.0, 0.01, 1e-5, 1.0 / bim.n_snp, pos, device=0)
+p = lds.LDScoreParams(bed.data, n_snp=bim.n_snp, n_org=fam.n_org, ld_wind=1.0, maf=0.01, std_thr=1e-5,
+                      rsq_thr=1.0 / bim.n_snp, positions=pos.tolist())
+one = lds.calculate(p)
+out = {{}}
+for k in D.RESULT_KEYS:
+    a, b = np.asarray(full[k], dtype=np.float64), np.asarray(getattr(one, k), dtype=np.float64)
+    out[k] = bool(np.array_equal(a, b, equal_nan=True))
+print(json.dumps(out), flush=True)
+dist.destroy_process_group()
+'''
+
+
+def test_rccl_device_gather_one_rank(tmp_path):
+    """The RCCL ("nccl") branch of the sharded CLI path, which the 2-rank tests above (gloo: ranks share the one GPU)
+    do not reach: a process group of one over RCCL, the owned score-table block written on the device
+    (nldsc_engine_run_device), gather_spans / all_gather_into_tensor on device tensors, rank 0's copy to the host.
+    Equal bit for bit to the single-process `calculate` (one rank owns every SNP)."""
+    import json
+    script = tmp_path / "rccl1.py"
+    script.write_text(RCCL_SCRIPT.format(repo=REPO, bfile=os.path.join(GOLDEN, "n1003")))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), str(script)]
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert all(d.values()), d
+
+
+def test_bench_force_dist_rccl_one_rank():
+    """`bench.py --force-dist`: the strong-scaling bench's N-GPU code (process group, owned range + halo, device
+    table, RCCL gather every step, max-over-ranks timing) run as a group of one on the one GPU."""
+    import json
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--force-dist", "--no-cpu", "--no-file",
+                        "--steps", "2", "--warmup", "1", "--n-snp", "6000", "--n-org", "20000", "--length-cm", "21"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["n_gpus"] == 1 and d["value"] > 0 and "RCCL" in d["config"]["parallelism"], d
+    assert d["stages_ms"]["gather_ms"] >= 0 and d["per_rank"][0]["owned_snps"] == 6000

@@ -3,8 +3,10 @@
 # baseline), rocprofv3 kernel statistics of the same bench, PMC passes (HBM traffic, MFMA busy, clock, L2) of the
 # current kernels for C3, C2 and the C5 slice, their bench lines, a per-rank rehearsal of 8-GPU strong scaling and a
 # 2-rank gloo run of `bench.py --gpus 2` (the bench starting its own ranks).  Every step has its own time limit and
-# the script stops at the first failure.  Usage (from this container):
-#   gpurun --timeout 1700 -- bash tools/gpu_round3.sh <tag> [skip-tests]
+# the script stops at the first failure.  gpurun's limit (1200 s) takes it in three calls (from this container):
+#   gpurun --timeout 1200 -- bash tools/gpu_tests.sh <tag>                       (the GPU suite + smoke)
+#   gpurun --timeout 1200 -- bash tools/gpu_round3.sh <tag> skip-tests bench      (bench, rocprof stats)
+#   gpurun --timeout 1200 -- bash tools/gpu_round3.sh <tag> skip-tests pmc        (PMC passes, C2 / C5, scaling)
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 T=${1:-run}
 O=gpurun_out/$T
@@ -19,6 +21,8 @@ if [ "$2" != "skip-tests" ]; then
     || { echo smoke failed; cat $O/smoke.log; exit 1; }
   tail -1 $O/smoke.log
 fi
+PH=${3:-all}
+if [ "$PH" = all ] || [ "$PH" = bench ]; then
 step bench
 timeout -k 10 400 python bench.py > $O/bench_c3.json 2> $O/bench_c3.err || { echo bench failed; tail $O/bench_c3.err; exit 1; }
 tail -c 400 $O/bench_c3.json
@@ -26,6 +30,8 @@ step rocprof stats
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o k --output-format csv -- python3 bench.py --no-cpu --no-file --steps 5 > $O/prof_bench.json 2> $O/prof.err \
   || { echo rocprof failed; tail $O/prof.err; exit 1; }
 find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats_c3.csv \;
+[ "$PH" = bench ] && { step done; exit 0; }
+fi
 pmc() {  # <label> <workload string> <alg-bytes spec> <bench args>
   local label=$1 wl=$2 alg=$3; shift 3
   local B="python3 bench.py --no-cpu --no-file --steps 1 --warmup 0 $*" P=$O/pmc_$label
