@@ -155,6 +155,11 @@ struct nldsc_engine {
     int band_streams = 1;
     bool compact = true;  // $NLDSC_COMPACT=0: routed runs list every single-block item (routed ones return at once)
     DevBuf<uint8_t> blk_miss;
+    DevBuf<uint8_t> blk_zero;  // additive-only quad runs: the routing array of the other kernels (all super-items routed)
+    // $NLDSC_QUAD_ADD=1 (study, off): additive-only runs send every 4 x 4 super-item to the quad kernel, those holding
+    // missing calls with the four additive products per pair — C2 band 2.29 -> 4.13 ms (profiles/r03_ab_quad_add_rejected.json:
+    // short rows, one wave per SIMD, whole 64 x 64 tiles at the band edges)
+    bool quad_add = false;
     int last_band_kernel = NLDSC_BAND_F4;
     DevBuf<double> pos, maf, rstd, l2_acc, l2d_acc, l2, l2d;
     DevBuf<int4> items;
@@ -194,7 +199,7 @@ struct nldsc_engine {
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         if (ev_plan) (void)hipEventDestroy(ev_plan);
         Ew.release(); plan_counts.release(); plan_meta.release(); plan_rows.release();
-        plan_counts2.release(); plan_rows2.release(); items2.release(); blk_miss.release(); sums.release();
+        plan_counts2.release(); plan_rows2.release(); items2.release(); blk_miss.release(); blk_zero.release(); sums.release();
         if (stream) (void)hipStreamDestroy(stream);
         if (plan_stream) (void)hipStreamDestroy(plan_stream);
         if (ev_pos) (void)hipEventDestroy(ev_pos);
@@ -310,6 +315,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_COMPACT")) e->compact = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_DEBUG_TIMING")) e->debug_timing = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_F4_NC2")) e->f4_nc2 = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_QUAD_ADD")) e->quad_add = std::atoi(v) != 0;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
@@ -576,6 +582,9 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     const bool routed = e->t2_mode == 1 || e->t2_mode == 3;
     const bool quad = e->t2_mode == 3;
     const int route_shift = quad ? 2 : 1;  // super-items of 2^route_shift blocks a side
+    // ($NLDSC_QUAD_ADD=1, study) additive-only runs: every 4 x 4 super-item in the quad kernel, those holding missing
+    // calls with the four additive products in 64 x 64 tiles per wave; the other kernels get an all-zero routing array
+    const bool quad_add = quad && !dom && e->quad_add;
     // K-split (f4, unsegmented rows) when the items fill the wave slots (2 per SIMD) in few, partly empty
     // rounds — a rank's shard of one chromosome — and splitting the K loop in P pieces fills them better
     // Model: a round of items takes ~0.67 us per K chunk (C3: 2 466 chunks, 1.65 ms per round, 12.7 rounds in
@@ -689,6 +698,10 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
             HIPCHK(e->blk_miss.ensure((size_t)nblk));
             HIPCHK(nldsc::launch_block_missing_rows(e->row_miss.p, M, order, e->blk_miss.p, ps));
         }
+        if (use_t2 && quad_add) {
+            HIPCHK(e->blk_zero.ensure((size_t)nblk));
+            HIPCHK(hipMemsetAsync(e->blk_zero.p, 0, (size_t)nblk, ps));
+        }
         compact = use_t2 && routed && n_items > 0 && e->compact;
         if (compact) {
             const size_t n_chunks = ((size_t)n_items + 1023) / 1024;
@@ -696,7 +709,8 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
             HIPCHK(e->compact_tmp.ensure(n_chunks + 1));
             HIPCHK(e->h_route.ensure(sizeof(int)));
             *reinterpret_cast<volatile int*>(e->h_route.p) = -1;  // (the copy below lands the count, >= 0)
-            HIPCHK(nldsc::launch_compact_items(e->items.p, n_items, e->blk_miss.p, route_shift, nblk, e->compact_tmp.p,
+            HIPCHK(nldsc::launch_compact_items(e->items.p, n_items, quad_add ? e->blk_zero.p : e->blk_miss.p, route_shift,
+                                               nblk, e->compact_tmp.p,
                                                e->compact_tmp.p + n_chunks, e->items_u.p, ps));
             HIPCHK(hipMemcpyAsync(e->h_route.p, e->compact_tmp.p + n_chunks, sizeof(int), hipMemcpyDeviceToHost, ps));
         }
@@ -809,7 +823,12 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         return tail_p > 1 ? e->gram.ensure((size_t)tail * tail_p * 8192) : hipSuccess;
     };
     auto launch_super = [&](int which) -> hipError_t {
-        return (quad ? nldsc::launch_band_f4_q : nldsc::launch_band_f4_t2)(
+        if (quad)
+            return nldsc::launch_band_f4_q(dom, n_items2, geno, pitch_words, n_it, e->cst.p, e->items2.p,
+                                           e->plan_rows.p, nblk, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
+                                           p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p,
+                                           e->l2d_acc.p, e->ws_acc.p, true, blk_rep, e->blk_miss.p, which, st, quad_add);
+        return nldsc::launch_band_f4_t2(
             dom, n_items2, geno, pitch_words, n_it, e->cst.p, e->items2.p, e->plan_rows.p, nblk, e->pos.p, e->Lw.p,
             e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
             e->ws_acc.p, true, blk_rep, routed ? e->blk_miss.p : nullptr, which, st);
@@ -817,7 +836,8 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // (uncompacted routed list, $NLDSC_COMPACT=0: the kernels skip the items a super-item kernel takes)
     // (column-block pair items: the compaction keeps an item while one of its blocks is unrouted, the kernel drops
     // the other)
-    const uint8_t* single_miss = use_t2 && routed && (!compact || nc2) ? e->blk_miss.p : nullptr;
+    const uint8_t* single_miss =
+        use_t2 && routed && (!compact || nc2) ? (quad_add ? e->blk_zero.p : e->blk_miss.p) : nullptr;
     auto launch_single = [&](int which) -> hipError_t {
         if (use_f4 && ksplit > 1)
             return nldsc::launch_band_f4_split(dom, ksplit, n_single, geno, pitch_words, n_it, e->cst.p, single,
@@ -912,7 +932,8 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     HIPCHK(nldsc::launch_issued_products(single, run_single ? n_single : 0, use_t2 ? e->items2.p : nullptr,
                                          n_items2, gpu_plan ? e->plan_rows.p : nullptr,
                                          use_f4 ? e->blk_miss.p : nullptr, nblk, path, dom,
-                                         (use_t2 && routed ? 2 : 0) | (single_miss != nullptr ? 1 : 0),
+                                         (use_t2 && routed ? 2 : 0) | (single_miss != nullptr ? 1 : 0) |
+                                             (use_t2 && quad_add ? 4 : 0),
                                          route_shift,
                                          e->sums.p + 2, st));
     const int n_own = own_end - own_begin;

@@ -122,14 +122,16 @@ hipError_t launch_band_f4_t2(bool dom, int n_items2, const uint32_t* geno, int p
                              int* ws_acc, bool xcd, const uint8_t* blk_rep, const uint8_t* blk_miss, int which,
                              hipStream_t st);
 // 4 x 4 block-pair workgroups (the quad kernel: one wave per SIMD, 64 x 64 SNP tiles) for the missing-free 4 x 4
-// super-items (I4, J4, 1, 0) of launch_plan_super(shift 2); blk_miss required (route_shift 2 for the other kernels)
+// super-items (I4, J4, 1, 0) of launch_plan_super(shift 2); blk_miss required (route_shift 2 for the other kernels).
+// add_all (additive-only runs): every super-item, those holding missing calls with the four additive products (the
+// other kernels are then routed nothing: an all-zero routing array)
 constexpr int Q_STAGES = 4;
 hipError_t launch_band_f4_q(bool dom, int n_items4, const uint32_t* geno, int pitch_words, int n_it,
                             const SnpConst* cst, const int4* items4, const int2* rows, int nblk, const double* pos,
                             const int* Lw, const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind,
                             double n_org, double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
                             int* ws_acc, bool xcd, const uint8_t* blk_rep, const uint8_t* blk_miss, int which,
-                            hipStream_t st);
+                            hipStream_t st, bool add_all);
 // blk_miss[b] = block b holds a missing call (launch_block_missing_rows).  Passed to the fp4 kernels (unsegmented rows)
 // it routes the super-items: missing-free ones to a super-item kernel (operand-feed bound at 3 products per K step,
 // where sharing the strips pays), the block pairs of the others to the single-block kernel (MFMA bound at 8 products)

@@ -1972,22 +1972,30 @@ struct QLds {
     SnpConst cst[Q_SLOTS];
 };
 
-// one K step of a wave's four block pairs (a, b): x.x, x.h, h.x (missing-free: 2^-1-scaled h planes)
-template <bool DOM>
-__device__ __forceinline__ void q_step(const F4Frag (&A)[2], const F4Frag (&B)[2], f32x16v (&gxx)[4], f32x16v (&gxh)[4],
-                                       f32x16v (&ghx)[4]) {
+// one K step of a wave's four block pairs (a, b).  WM = false (missing-free): g0 = x.x, g1 = x.h, g2 = h.x (2^-1-scaled
+// h planes; additive-only: x.x alone).  WM (additive-only super-items holding missing calls): g0 = v.v, g1 = v.m,
+// g2 = m.v, g3 = m.m — the single-block kernel's four additive products.
+template <bool DOM, bool WM>
+__device__ __forceinline__ void q_step(const F4Frag (&A)[2], const F4Frag (&B)[2], f32x16v (&g0)[4], f32x16v (&g1)[4],
+                                       f32x16v (&g2)[4], f32x16v (&g3)[4]) {
+    static_assert(!(DOM && WM), "add+dom quad super-items are missing-free");
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         const F4Frag& a = A[p >> 1];
         const F4Frag& b = B[p & 1];
-        gxx[p] = mfma_f4(a.x, b.x, gxx[p]);
+        g0[p] = mfma_f4(a.x, b.x, g0[p]);
         if (DOM) {
-            gxh[p] = mfma_f4<E8M0_ONE, E8M0_HALF>(a.x, b.h, gxh[p]);
-            ghx[p] = mfma_f4<E8M0_HALF, E8M0_ONE>(a.h, b.x, ghx[p]);
+            g1[p] = mfma_f4<E8M0_ONE, E8M0_HALF>(a.x, b.h, g1[p]);
+            g2[p] = mfma_f4<E8M0_HALF, E8M0_ONE>(a.h, b.x, g2[p]);
+        }
+        if (WM) {
+            g1[p] = mfma_f4(a.x, b.o, g1[p]);
+            g2[p] = mfma_f4(a.o, b.x, g2[p]);
+            g3[p] = mfma_f4(a.o, b.o, g3[p]);
         }
     }
-    constexpr int n_mfma = DOM ? 12 : 4;
-    constexpr int n_valu = 4 * (DOM ? 12 : 8);  // the next step's four decodes
+    constexpr int n_mfma = DOM || WM ? (WM ? 16 : 12) : 4;
+    constexpr int n_valu = 4 * (WM ? 14 : DOM ? 12 : 8);  // the next step's four decodes
 #pragma unroll
     for (int m = 0; m < n_mfma; ++m) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -1995,7 +2003,9 @@ __device__ __forceinline__ void q_step(const F4Frag (&A)[2], const F4Frag (&B)[2
     }
 }
 
-template <bool DOM, int S, bool KC>
+// ADDM (additive-only runs): every super-item runs here (the host routes none to the single-block kernel); those whose
+// blocks hold missing calls take the four additive products of the missing basis (WM), the others x.x alone.
+template <bool DOM, int S, bool KC, bool ADDM = false>
 __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
     const uint32_t* __restrict__ geno, int pitch_words, int n_it, const SnpConst* __restrict__ cst,
     const int4* __restrict__ items, const int2* __restrict__ rows, int nblk, const double* __restrict__ pos,
@@ -2015,7 +2025,9 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
         for (int s = 0; s < 8; ++s) rep |= blk_rep[min(strip_blk(s), nblk - 1)] != 0;
         if (KC ? !rep : rep) return;
     }
-    if (!q_routed(blk_miss, I4, J4, nblk)) return;  // the single-block kernel's
+    static_assert(!(ADDM && DOM), "ADDM: additive-only runs");
+    const bool wm = ADDM && !q_routed(blk_miss, I4, J4, nblk);  // (workgroup-uniform)
+    if (!ADDM && !q_routed(blk_miss, I4, J4, nblk)) return;  // the single-block kernel's
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
     {
         const int b = strip_blk(tid >> 5);
@@ -2071,9 +2083,9 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
 #pragma unroll
     for (int t = 0; t < S; ++t) issue(t);
 
-    f32x16v gxx[4], gxh[4], ghx[4];
+    f32x16v g0[4], g1[4], g2[4], g3[4];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) gxx[p] = gxh[p] = ghx[p] = f32x16v{};
+    for (int p = 0; p < 4; ++p) g0[p] = g1[p] = g2[p] = g3[p] = f32x16v{};
     // as the 2 x 2 kernel's ring: stage t read into registers one stage ahead, S - 1 stages in flight
     auto read_stage = [&](int t, uint4 (&ra)[2][2], uint4 (&rb)[2][2]) {
 #pragma unroll
@@ -2084,8 +2096,8 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
                 rb[k][c] = sh.stage[t % S][cs + k][c][lane];
             }
     };
-    auto kloop = [&](auto ACTc) {
-        constexpr bool ACT = decltype(ACTc)::value;
+    auto kloop = [&](auto ACTc, auto WMc) {
+        constexpr bool ACT = decltype(ACTc)::value, WM = decltype(WMc)::value;
         uint4 ra[2][2], rb[2][2];
         wait_vmcnt<4 * (S - 1)>();  // stage 0 landed (this wave's loads)
         __builtin_amdgcn_s_barrier();  // every wave's
@@ -2106,16 +2118,16 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
                     F4Frag A[2], B[2];
 #pragma unroll
                     for (int k = 0; k < 2; ++k) {
-                        A[k] = decode_f4<false>(ra[k][c].x, ra[k][c].y);
-                        B[k] = decode_f4<false>(rb[k][c].x, rb[k][c].y);
+                        A[k] = decode_f4<WM>(ra[k][c].x, ra[k][c].y);
+                        B[k] = decode_f4<WM>(rb[k][c].x, rb[k][c].y);
                     }
-                    q_step<DOM>(A, B, gxx, gxh, ghx);
+                    q_step<DOM, WM>(A, B, g0, g1, g2, g3);
 #pragma unroll
                     for (int k = 0; k < 2; ++k) {
-                        A[k] = decode_f4<false>(ra[k][c].z, ra[k][c].w);
-                        B[k] = decode_f4<false>(rb[k][c].z, rb[k][c].w);
+                        A[k] = decode_f4<WM>(ra[k][c].z, ra[k][c].w);
+                        B[k] = decode_f4<WM>(rb[k][c].z, rb[k][c].w);
                     }
-                    q_step<DOM>(A, B, gxx, gxh, ghx);
+                    q_step<DOM, WM>(A, B, g0, g1, g2, g3);
                 }
 #pragma unroll
                 for (int k = 0; k < 2; ++k)
@@ -2124,8 +2136,13 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
             }
         }
     };
-    if (any) kloop(std::true_type{});
-    else kloop(std::false_type{});
+    if (!any) kloop(std::false_type{}, std::false_type{});
+    else if constexpr (ADDM) {
+        if (wm) kloop(std::true_type{}, std::true_type{});
+        else kloop(std::true_type{}, std::false_type{});
+    } else {
+        kloop(std::true_type{}, std::false_type{});
+    }
     wait_vmcnt<0>();  // the tail's surplus loads
     if (!any) return;  // no barrier follows
     const f32x16v z = {};
@@ -2133,10 +2150,16 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
     for (int p = 0; p < 4; ++p) {
         if (!need[p]) continue;
         const int rb = strip_blk(rs + (p >> 1)), cb = 4 * J4 + 2 * (w & 1) + (p & 1);
-        // (missing-free: the m products are 0, as in the single-block kernel's RM = CM = false loop)
-        pair_epilogue<DOM, f32x16v, true, KC>(sh.info, sh.cst, 32 * (rs + (p >> 1)), 32 * (cs + (p & 1)), rb == cb, i,
-                                              h, gxx[p], z, z, z, gxh[p], z, ghx[p], z, ld_wind, n_org, rsq_thr, n_org,
-                                              own_lo, own_hi, n_snp, l2_acc, l2d_acc, ws_acc);
+        // (missing-free: the m products are 0, as in the single-block kernel's RM = CM = false loop; WM: g1..g3 are
+        // v.m, m.v, m.m, all computed on a diagonal pair too)
+        if constexpr (ADDM)
+            pair_epilogue<false, f32x16v, true, KC>(sh.info, sh.cst, 32 * (rs + (p >> 1)), 32 * (cs + (p & 1)), rb == cb,
+                                                    i, h, g0[p], g1[p], g2[p], g3[p], z, z, z, z, ld_wind, n_org,
+                                                    rsq_thr, n_org, own_lo, own_hi, n_snp, l2_acc, l2d_acc, ws_acc);
+        else
+            pair_epilogue<DOM, f32x16v, true, KC>(sh.info, sh.cst, 32 * (rs + (p >> 1)), 32 * (cs + (p & 1)), rb == cb,
+                                                  i, h, g0[p], z, z, z, g1[p], z, g2[p], z, ld_wind, n_org, rsq_thr,
+                                                  n_org, own_lo, own_hi, n_snp, l2_acc, l2d_acc, ws_acc);
     }
 }
 
@@ -2196,7 +2219,8 @@ __global__ void issued_products_kernel(const int4* __restrict__ items, int n_ite
                                        int nblk, int kind, int dom, int routed, int route_shift,
                                        unsigned long long* __restrict__ out) {
     // routed bit 0: single items the routing sends to a super-item kernel are not counted here (an uncompacted
-    // list); bit 1: super-items count only when routed to their kernel
+    // list); bit 1: super-items count only when routed to their kernel; bit 2: additive-only quad run — every
+    // super-item goes to the quad kernel (4 products per pair where its blocks hold missing calls), no single item
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long n = 0;
     if (t < n_items) {
@@ -2205,7 +2229,7 @@ __global__ void issued_products_kernel(const int4* __restrict__ items, int n_ite
         if (kind == 2) {  // (it.z == 2: additive-only column-block pairs, one product set per column block)
             for (int c = 0; c < it.z; ++c) {
                 const int J = it.y + c;
-                if ((routed & 1) && routed_item(blk_miss, route_shift, it.x, J, nblk)) continue;
+                if ((routed & 1) && ((routed & 4) || routed_item(blk_miss, route_shift, it.x, J, nblk))) continue;
                 const int rm = blk_miss[it.x] != 0, cm = blk_miss[J] != 0, nd = it.x != J;
                 n += 1 + cm + rm * nd + rm * cm + (dom ? 1 + nd + rm + cm * nd : 0);
             }
@@ -2217,14 +2241,15 @@ __global__ void issued_products_kernel(const int4* __restrict__ items, int n_ite
     } else if (items2 != nullptr && t < n_items + n_items2 && route_shift == 2) {
         // quad super-items (missing-free): a wave with any needed block pair issues all four pairs' products
         const int4 it = items2[t - n_items];
-        if (!(routed & 2) || q_routed(blk_miss, it.x, it.y, nblk)) {
+        const bool wm = (routed & 4) && !q_routed(blk_miss, it.x, it.y, nblk);
+        if (!(routed & 2) || (routed & 4) || q_routed(blk_miss, it.x, it.y, nblk)) {
             for (int w = 0; w < 4; ++w) {
                 bool any = false;
                 for (int p = 0; p < 4; ++p) {
                     const int rb = 4 * it.x + 2 * (w >> 1) + (p >> 1), cb = 4 * it.y + 2 * (w & 1) + (p & 1);
                     any |= rb < nblk && cb < nblk && cb - rb >= rows[rb].x && cb - rb <= rows[rb].y;
                 }
-                n += any ? 4 * (dom ? 3 : 1) : 0;
+                n += any ? 4 * (dom ? 3 : wm ? 4 : 1) : 0;
             }
         }
     } else if (items2 != nullptr && t < n_items + n_items2) {
@@ -2660,15 +2685,24 @@ hipError_t launch_band_f4_q(bool dom, int n_items4, const uint32_t* geno, int pi
                             const int* Lw, const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind,
                             double n_org, double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
                             int* ws_acc, bool xcd, const uint8_t* blk_rep, const uint8_t* blk_miss, int which,
-                            hipStream_t st) {
+                            hipStream_t st, bool add_all) {
     if (n_items4 <= 0) return hipSuccess;
-    if (n_it > F4_SEG_CHUNKS || n_it < 2 || (n_it & 1) || blk_miss == nullptr) return hipErrorInvalidValue;
-#define NLDSC_BAND(DOM_, KC_)                                                                                       \
-    hipLaunchKernelGGL((band_f4_q_kernel<DOM_, Q_STAGES, KC_>), dim3(n_items4), dim3(256), 0, st, geno,             \
+    if (n_it > F4_SEG_CHUNKS || n_it < 2 || (n_it & 1) || blk_miss == nullptr || (add_all && dom))
+        return hipErrorInvalidValue;
+#define NLDSC_BAND(DOM_, KC_, ADDM_)                                                                                \
+    hipLaunchKernelGGL((band_f4_q_kernel<DOM_, Q_STAGES, KC_, ADDM_>), dim3(n_items4), dim3(256), 0, st, geno,      \
                        pitch_words, n_it, cst, items4, rows, nblk, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,      \
                        rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss)
-    if (which & 1) { if (dom) NLDSC_BAND(true, false); else NLDSC_BAND(false, false); }
-    if (blk_rep && (which & 2)) { if (dom) NLDSC_BAND(true, true); else NLDSC_BAND(false, true); }
+    if (which & 1) {
+        if (dom) NLDSC_BAND(true, false, false);
+        else if (add_all) NLDSC_BAND(false, false, true);
+        else NLDSC_BAND(false, false, false);
+    }
+    if (blk_rep && (which & 2)) {
+        if (dom) NLDSC_BAND(true, true, false);
+        else if (add_all) NLDSC_BAND(false, true, true);
+        else NLDSC_BAND(false, true, false);
+    }
 #undef NLDSC_BAND
     return hipGetLastError();
 }

@@ -631,7 +631,9 @@ def test_issued_products_counted_per_item(engine, t2, dom):
     1 + cm + rm + rm cm + dom (2 + rm + cm) 32x32 block products over all K, less the transposed ones of diagonal
     blocks; items the routing sends to the 2 x 2 kernel (missing-free super-items) 1 + 2 dom; int8 4 + dom (2 + 2
     !diag); fp32 1 + dom (2 - diag); with the quad kernel ($NLDSC_T2=3) every wave of a routed 4 x 4 super-item that
-    needs one of its four block pairs issues all four (4 (1 + 2 dom)).  Groups of four blocks alternate between
+    needs one of its four block pairs issues all four (4 (1 + 2 dom)); additive-only runs route every super-item
+    there with $NLDSC_QUAD_ADD=1 (the study mode, set here), 4 x 4 products per such wave where the super-item holds
+    missing calls.  Groups of four blocks alternate between
     missing-free, one missing call and 2 % missing."""
     from nldsc_amd import _lib, synth
     from nldsc_amd.engine import Engine
@@ -656,14 +658,18 @@ def test_issued_products_counted_per_item(engine, t2, dom):
         assert routed.any() and not routed.all()
         f4 = np.where(routed, 1 + (2 if dom else 0), f4)
     if t2 == "3":  # 4 x 4 super-items whose eight blocks are missing-free run in the quad kernel
-        routed = ~np.any([mb(4 * (I >> 2) + k) | mb(4 * (J >> 2) + k) for k in range(4)], axis=0).astype(bool)
-        assert routed.any() and not routed.all()
+        free = ~np.any([mb(4 * (I >> 2) + k) | mb(4 * (J >> 2) + k) for k in range(4)], axis=0).astype(bool)
+        assert free.any() and not free.all()
+        # additive-only: every super-item, 4 products per pair where its blocks hold missing calls
+        routed = free if dom else np.ones_like(free)
+        free4 = {(a >> 2, b >> 2): bool(f) for a, b, f in zip(I.tolist(), J.tolist(), free.tolist())}
         needed = set(zip(I.tolist(), J.tolist()))
         quad = 0
         for I4, J4 in sorted(set(zip((I[routed] >> 2).tolist(), (J[routed] >> 2).tolist()))):
             for w in range(4):
                 pairs = [(4 * I4 + 2 * (w >> 1) + a, 4 * J4 + 2 * (w & 1) + b) for a in (0, 1) for b in (0, 1)]
-                quad += 4 * (3 if dom else 1) if any(p in needed for p in pairs) else 0
+                per = 3 if dom else 1 if free4[(I4, J4)] else 4
+                quad += 4 * per if any(p in needed for p in pairs) else 0
         f4 = np.append(np.where(routed, 0, f4), quad)
     i8 = 4 + (2 + 2 * nd if dom else 0 * nd)
     f32 = 1 + (1 + nd if dom else 0 * nd)
@@ -679,7 +685,7 @@ def test_issued_products_counted_per_item(engine, t2, dom):
                 e.run(1.0, 0.01, 1e-5, 1.0 / M, pos, flags=flags | MODES[mode])
                 out[mode] = e.timings()["flop_issued"] / (2.0 * 32 * 32 * 4 * row_bytes)
         return out
-    got = _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", t2, run))
+    got = _env_run("NLDSC_QUAD_ADD", "1", lambda: _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", t2, run)))
     assert got == {k: float(v) for k, v in expect.items()}, (got, expect)
 
 
@@ -814,6 +820,12 @@ T2_CASES = {
     "missing_free_odd": (4099, 1090, 12.0, 0.5, 0.0, True, None, False),
     "missing_free_owned": (3001, 1400, 10.0, 1.0, 0.0, True, (333, 1001), False),
     "missing_free_additive": (4096, 1025, 8.0, 1.0, 0.0, False, None, False),
+    # additive-only with missing calls (T2=3: every super-item in the quad kernel, 4 products per pair): an owned
+    # range, odd blocks, replayed rare variants (the KC launch), blocks with and without missing calls
+    "additive_owned": (3001, 1400, 10.0, 1.0, 0.02, False, (333, 1001), False),
+    "additive_odd_narrow": (4099, 990, 30.0, 0.3, 0.02, False, None, False),
+    "additive_rare_replay": (50_001, 400, None, 1.0, None, False, None, True),
+    "additive_mixed_groups": (5003, 1700, 8.0, 1.0, "mixed4", False, None, False),
 }
 
 
@@ -853,8 +865,10 @@ def test_2x2_workgroups_bitwise_single_block(engine, case, t2):
             r = e.run(*args, flags=flags, own=own)
             assert e.timings()["band_kernel"] == kernel
             return r
-    got = _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", t2, lambda: fresh(
-        {"2": "f4_2x2", "1": "f4_routed", "3": "f4_quad"}[t2])))
+    # (additive-only with T2=3: the study mode that sends every super-item to the quad kernel, $NLDSC_QUAD_ADD=1)
+    got = _env_run("NLDSC_QUAD_ADD", "1" if not dom and t2 == "3" else "0", lambda: _env_run(
+        "NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", t2, lambda: fresh(
+            {"2": "f4_2x2", "1": "f4_routed", "3": "f4_quad"}[t2]))))
     ref = _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", "0", lambda: fresh("f4")))
     for k in got:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{case} {k}")
@@ -919,8 +933,9 @@ def test_f4_column_block_pairs_bitwise_single_blocks(engine, case):
             e.load_bed_bytes(synth.bed_bytes(rows), M, N)
             r = e.run(*args, flags=flags, own=own)
             return r, e.timings()
-    run = lambda nc2: _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", t2, lambda: _env_run(  # noqa: E731
-        "NLDSC_F4_NC2", nc2, fresh)))
+    # ($NLDSC_QUAD_ADD=0: the quad kernel keeps only the missing-free super-items, so the pairs run here)
+    run = lambda nc2: _env_run("NLDSC_QUAD_ADD", "0", lambda: _env_run("NLDSC_KSPLIT", "0", lambda: _env_run(  # noqa
+        "NLDSC_T2", t2, lambda: _env_run("NLDSC_F4_NC2", nc2, fresh))))
     (got, tg), (ref, tr) = run("1"), run("0")
     assert tg["band_items"] < tr["band_items"], (tg["band_items"], tr["band_items"])  # the plan paired them
     assert tg["flop_issued"] == tr["flop_issued"], (tg["flop_issued"], tr["flop_issued"])
@@ -944,10 +959,9 @@ def test_band_round_launches_bitwise_one_launch(engine, case):
     model prefers it, gives bitwise the results of one launch of all items ($NLDSC_BAND_ROUNDS=0): the per-SNP sums
     are order-independent fixed point, the K-split partial Gram tiles are exact integers, and every item runs once.
     12 000 SNPs at 800 per cM, 1 % missing; a few SNPs against the exact truth.  The additive-only case runs
-    single-block items ($NLDSC_F4_NC2=0; its default column-block pairs halve the item count, here below four
-    rounds)."""
+    single-block items ($NLDSC_QUAD_ADD=0 and $NLDSC_F4_NC2=0: by default its super-items all go to the quad kernel)."""
     if not ROUND_CASES[case][3]:
-        return _env_run("NLDSC_F4_NC2", "0", lambda: _round_launch_case(case))
+        return _env_run("NLDSC_QUAD_ADD", "0", lambda: _env_run("NLDSC_F4_NC2", "0", lambda: _round_launch_case(case)))
     return _round_launch_case(case)
 
 
