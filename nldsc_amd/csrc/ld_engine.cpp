@@ -8,7 +8,11 @@
 //   band correlation kernels -> finalize -> results to host.
 #include <hip/hip_runtime.h>
 
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
+#include <cerrno>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -16,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/nldsc_ld.h"
@@ -27,7 +32,8 @@
 namespace {
 
 constexpr int BLK = 32;             // SNPs per MFMA block
-constexpr int CHUNK_BYTES = 32;     // one K-loop chunk of a 2-bit row (16 B per lane half)
+constexpr int CHUNK_BYTES = 32;
+constexpr int kLoadThreads = 8;     // .bed file loads: reader threads (pread + H2D + placement per slice)     // one K-loop chunk of a 2-bit row (16 B per lane half)
 // resident row pitch: an even number of 32-byte chunks (the fp4 K loop takes two per iteration)
 constexpr int ROW_ALIGN_BYTES = 64;
 // item order of the single-block-pair schedule: tiles of TILE_R row blocks x TILE_C diagonal offsets
@@ -424,52 +430,90 @@ int nldsc_engine_load_bed_file_range(nldsc_engine* e, const char* path, int32_t 
     if (fseeko(f, 0, SEEK_END) != 0) return too_short(3);
     const off_t fsize = ftello(f);
     if (fsize < 0 || (size_t)fsize < need) return too_short(fsize < 0 ? 0 : (size_t)fsize);
-    if (fseeko(f, (off_t)first, SEEK_SET) != 0) return too_short((size_t)fsize);
     HIPCHK(hipSetDevice(e->device));
-    // rows stream through two pinned 64 MiB slots: the read into one slot overlaps the H2D copy out of the other
-    // into its device staging slot and the kernel that places the slot's rows (an event per slot marks both done)
-    const size_t rows_per = std::max<size_t>(1, (size_t(64) << 20) / nb), CH = rows_per * nb;  // ~64 MiB of rows
+    const int32_t n_snp = snp_end - snp_begin;
+    {
+        const hipError_t ha = alloc_image(e, n_snp, n_org);
+        if (ha != hipSuccess) {
+            std::fclose(f);
+            return set_err(err, errlen, NLDSC_E_HIP, "HIP error %s allocating the image", hipGetErrorString(ha));
+        }
+    }
+    // Rows stream through T reader threads, each with its own pinned slot (~32 MiB of whole rows), device staging slot
+    // and stream: thread t reads slices t, t + T, ... with pread (several reads in flight: the page cache copies and
+    // the device's queue run in parallel, where one fread loop held the load to one core's memcpy rate), then queues
+    // the slice's H2D copy and the kernel that places its rows (load_rows_kernel), and waits for both before it reuses
+    // the slot.  Slices are independent (each names its rows), so their order does not matter.
+    const int fd = fileno(f);
+    const size_t rows_per = std::max<size_t>(1, (size_t(32) << 20) / nb), CH = rows_per * nb;
+    const size_t n_slices = (bytes + CH - 1) / CH;
+    const int T = (int)std::max<size_t>(1, std::min<size_t>(n_slices, (size_t)kLoadThreads));
     uint8_t* stage = nullptr;
-    hipEvent_t done[2] = {nullptr, nullptr};
-    if (hipHostMalloc((void**)&stage, 2 * CH) != hipSuccess) {
+    if (hipHostMalloc((void**)&stage, (size_t)T * CH) != hipSuccess) {
         std::fclose(f);
         return set_err(err, errlen, NLDSC_E_OOM, "cannot allocate pinned staging buffer");
     }
-    hipError_t he = hipEventCreateWithFlags(&done[0], hipEventDisableTiming);
-    if (he == hipSuccess) he = hipEventCreateWithFlags(&done[1], hipEventDisableTiming);
-    const int32_t n_snp = snp_end - snp_begin;
-    if (he == hipSuccess) he = alloc_image(e, n_snp, n_org);
-    if (he == hipSuccess) he = e->stage_dev.ensure(2 * CH);
-    bool pending[2] = {false, false};
-    size_t off = 0, short_at = 0;
-    bool short_read = false;
-    for (int slot = 0; he == hipSuccess && off < bytes; slot ^= 1) {
-        const size_t n = std::min(CH, bytes - off);
-        uint8_t* buf = stage + (size_t)slot * CH;
-        if (pending[slot]) he = hipEventSynchronize(done[slot]);
-        if (he != hipSuccess) break;
-        const size_t r = std::fread(buf, 1, n, f);
-        if (r != n) {
-            short_read = true;
-            short_at = first + off + r;
-            break;
-        }
-        uint8_t* dslot = e->stage_dev.p + (size_t)slot * CH;
-        he = hipMemcpyAsync(dslot, buf, n, hipMemcpyHostToDevice, e->stream);
-        if (he == hipSuccess)
-            he = nldsc::launch_load_rows(dslot, (int)nb, (int)(off / nb), (int)(n / nb), e->bed.p, row_pitch(n_org),
-                                         e->stream);
-        if (he == hipSuccess) he = hipEventRecord(done[slot], e->stream);
-        pending[slot] = true;
-        off += n;
+    hipError_t he = e->stage_dev.ensure((size_t)T * CH);
+    std::vector<hipStream_t> streams(T, nullptr);
+    std::vector<hipEvent_t> done(T, nullptr);
+    for (int t = 0; t < T && he == hipSuccess; ++t) {
+        he = hipStreamCreateWithFlags(&streams[t], hipStreamNonBlocking);
+        if (he == hipSuccess) he = hipEventCreateWithFlags(&done[t], hipEventDisableTiming);
     }
-    const hipError_t hs = hipStreamSynchronize(e->stream);
-    if (he == hipSuccess) he = hs;
-    for (hipEvent_t ev : done)
-        if (ev) (void)hipEventDestroy(ev);
+    std::atomic<bool> stop{false};
+    std::atomic<size_t> short_at{SIZE_MAX};
+    std::vector<hipError_t> terr(T, hipSuccess);
+    const int dev = e->device, pitch = row_pitch(n_org);
+    uint8_t* const img = e->bed.p;
+    uint8_t* const dstage = e->stage_dev.p;
+    auto reader = [&](int t) {
+        hipError_t r = hipSetDevice(dev);
+        uint8_t* buf = stage + (size_t)t * CH;
+        uint8_t* dslot = dstage + (size_t)t * CH;
+        bool pending = false;
+        for (size_t k = (size_t)t; r == hipSuccess && k < n_slices && !stop.load(); k += (size_t)T) {
+            const size_t off = k * CH, n = std::min(CH, bytes - off);
+            if (pending) r = hipEventSynchronize(done[t]);
+            if (r != hipSuccess) break;
+            size_t got = 0;
+            while (got < n) {
+                const ssize_t q = pread(fd, buf + got, n - got, (off_t)(first + off + got));
+                if (q < 0 && errno == EINTR) continue;
+                if (q <= 0) break;
+                got += (size_t)q;
+            }
+            if (got != n) {
+                size_t cur = short_at.load();
+                while (first + off + got < cur && !short_at.compare_exchange_weak(cur, first + off + got)) {
+                }
+                stop.store(true);
+                break;
+            }
+            r = hipMemcpyAsync(dslot, buf, n, hipMemcpyHostToDevice, streams[t]);
+            if (r == hipSuccess)
+                r = nldsc::launch_load_rows(dslot, (int)nb, (int)(off / nb), (int)(n / nb), img, pitch, streams[t]);
+            if (r == hipSuccess) r = hipEventRecord(done[t], streams[t]);
+            pending = true;
+        }
+        if (r == hipSuccess && streams[t]) r = hipStreamSynchronize(streams[t]);
+        if (r != hipSuccess) stop.store(true);
+        terr[t] = r;
+    };
+    if (he == hipSuccess) {
+        std::vector<std::thread> pool;
+        for (int t = 1; t < T; ++t) pool.emplace_back(reader, t);
+        reader(0);
+        for (auto& th : pool) th.join();
+        for (hipError_t r : terr)
+            if (he == hipSuccess && r != hipSuccess) he = r;
+    }
+    for (int t = 0; t < T; ++t) {
+        if (streams[t]) (void)hipStreamDestroy(streams[t]);
+        if (done[t]) (void)hipEventDestroy(done[t]);
+    }
     (void)hipHostFree(stage);
     e->stage_dev.release();
-    if (short_read) return too_short(short_at);
+    if (short_at.load() != SIZE_MAX) return too_short(short_at.load());
     std::fclose(f);
     if (he != hipSuccess) return set_err(err, errlen, NLDSC_E_HIP, "HIP error %s loading BED", hipGetErrorString(he));
     HIPCHK(finish_image(e, n_snp, n_org));
