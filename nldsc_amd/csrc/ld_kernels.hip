@@ -59,27 +59,29 @@ __device__ __forceinline__ void count_codes(uint32_t word, int& c0, int& c1, int
 }
 
 // Loads: rows [row0, row0 + n_rows) of a .bed image (src: row r at r * nb bytes, any alignment) into the resident
-// layout, the pitch padding [nb, row_bytes) as 0x55.  One thread per 16-byte unit, in source order (coalesced byte
-// reads; each thread writes one whole 16-byte unit).
+// layout, the pitch padding [nb, row_bytes) as 0x55.  One thread per 16-byte unit in source order (coalesced byte
+// reads; each thread writes one whole 16-byte unit), grid-stride: an HSA dispatch counts its grid in work-items in 32
+// bits, so a launch of one thread per unit of a C5 slice (98.6 GB, 6.2e9 units) would wrap.
 __global__ void __launch_bounds__(256) load_rows_kernel(const uint8_t* __restrict__ src, int nb, int row0, int n_rows,
                                                         uint8_t* __restrict__ img, int row_bytes) {
     const int units = row_bytes >> 4;
-    const size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (g >= (size_t)n_rows * units) return;
-    const int r = (int)(g / units), u = (int)(g % units);
-    const uint8_t* s = src + (size_t)r * nb;
-    uint32_t w[4];
+    const size_t n = (size_t)n_rows * units, stride = (size_t)gridDim.x * 256;
+    for (size_t g = (size_t)blockIdx.x * 256 + threadIdx.x; g < n; g += stride) {
+        const int r = (int)(g / units), u = (int)(g % units);
+        const uint8_t* s = src + (size_t)r * nb;
+        uint32_t w[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        uint32_t v = 0;
+        for (int q = 0; q < 4; ++q) {
+            uint32_t v = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int p = 16 * u + 4 * q + k;
-            v |= (uint32_t)(p < nb ? s[p] : 0x55u) << (8 * k);
+            for (int k = 0; k < 4; ++k) {
+                const int p = 16 * u + 4 * q + k;
+                v |= (uint32_t)(p < nb ? s[p] : 0x55u) << (8 * k);
+            }
+            w[q] = v;
         }
-        w[q] = v;
+        *reinterpret_cast<uint4*>(img + tile_off(row0 + r, 16 * u, row_bytes)) = make_uint4(w[0], w[1], w[2], w[3]);
     }
-    *reinterpret_cast<uint4*>(img + tile_off(row0 + r, 16 * u, row_bytes)) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 // After a load: save every row's last byte; rows [n_snp, n_rows) (the last 32-SNP block's padding SNPs) all 0x55.
@@ -2514,8 +2516,9 @@ hipError_t launch_load_rows(const uint8_t* src, int nb, int row0, int n_rows, ui
                             hipStream_t st) {
     if (n_rows <= 0) return hipSuccess;
     const size_t n = (size_t)n_rows * (size_t)(row_bytes / 16);
-    hipLaunchKernelGGL(load_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, nb, row0, n_rows,
-                       img, row_bytes);
+    const size_t blocks = std::min<size_t>((n + 255) / 256, (size_t)1 << 20);  // <= 2^28 work-items per dispatch
+    hipLaunchKernelGGL(load_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, nb, row0, n_rows, img,
+                       row_bytes);
     return hipGetLastError();
 }
 
