@@ -166,6 +166,7 @@ struct nldsc_engine {
     // missing calls with the four additive products per pair — C2 band 2.29 -> 4.13 ms (profiles/r03_ab_quad_add_rejected.json:
     // short rows, one wave per SIMD, whole 64 x 64 tiles at the band edges)
     bool quad_add = false;
+    bool q_rounds = false;  // $NLDSC_Q_ROUNDS=1 (study): quad super-items in launches of one workgroup per CU
     int last_band_kernel = NLDSC_BAND_F4;
     DevBuf<double> pos, maf, rstd, l2_acc, l2d_acc, l2, l2d;
     DevBuf<int4> items;
@@ -322,6 +323,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_DEBUG_TIMING")) e->debug_timing = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_F4_NC2")) e->f4_nc2 = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_QUAD_ADD")) e->quad_add = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_Q_ROUNDS")) e->q_rounds = std::atoi(v) != 0;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
@@ -871,7 +873,8 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
             return nldsc::launch_band_f4_q(dom, n_items2, geno, pitch_words, n_it, e->cst.p, e->items2.p,
                                            e->plan_rows.p, nblk, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
                                            p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p,
-                                           e->l2d_acc.p, e->ws_acc.p, true, blk_rep, e->blk_miss.p, which, st, quad_add);
+                                           e->l2d_acc.p, e->ws_acc.p, true, blk_rep, e->blk_miss.p, which, st, quad_add,
+                                           e->q_rounds && n_items2 >= 4 * e->n_cu ? e->n_cu : 0);
         return nldsc::launch_band_f4_t2(
             dom, n_items2, geno, pitch_words, n_it, e->cst.p, e->items2.p, e->plan_rows.p, nblk, e->pos.p, e->Lw.p,
             e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,

@@ -131,7 +131,7 @@ hipError_t launch_band_f4_q(bool dom, int n_items4, const uint32_t* geno, int pi
                             const int* Lw, const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind,
                             double n_org, double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
                             int* ws_acc, bool xcd, const uint8_t* blk_rep, const uint8_t* blk_miss, int which,
-                            hipStream_t st, bool add_all);
+                            hipStream_t st, bool add_all, int round_items = 0);
 // blk_miss[b] = block b holds a missing call (launch_block_missing_rows).  Passed to the fp4 kernels (unsegmented rows)
 // it routes the super-items: missing-free ones to a super-item kernel (operand-feed bound at 3 products per K step,
 // where sharing the strips pays), the block pairs of the others to the single-block kernel (MFMA bound at 8 products)

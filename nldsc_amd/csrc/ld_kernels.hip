@@ -2688,19 +2688,24 @@ hipError_t launch_band_f4_q(bool dom, int n_items4, const uint32_t* geno, int pi
                             const int* Lw, const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind,
                             double n_org, double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
                             int* ws_acc, bool xcd, const uint8_t* blk_rep, const uint8_t* blk_miss, int which,
-                            hipStream_t st, bool add_all) {
+                            hipStream_t st, bool add_all, int round_items) {
     if (n_items4 <= 0) return hipSuccess;
     if (n_it > F4_SEG_CHUNKS || n_it < 2 || (n_it & 1) || blk_miss == nullptr || (add_all && dom))
         return hipErrorInvalidValue;
+    // round_items > 0: launches of that many super-items (one workgroup per CU each), so the workgroups on an XCD
+    // start together and stream their shared strips at nearby K offsets (not the KC launch)
+    int chunk = round_items > 0 ? round_items : n_items4;
 #define NLDSC_BAND(DOM_, KC_, ADDM_)                                                                                \
-    hipLaunchKernelGGL((band_f4_q_kernel<DOM_, Q_STAGES, KC_, ADDM_>), dim3(n_items4), dim3(256), 0, st, geno,      \
-                       pitch_words, n_it, cst, items4, rows, nblk, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org,      \
-                       rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss)
+    for (int o = 0; o < n_items4; o += chunk)                                                                        \
+    hipLaunchKernelGGL((band_f4_q_kernel<DOM_, Q_STAGES, KC_, ADDM_>), dim3(std::min(chunk, n_items4 - o)), dim3(256), \
+                       0, st, geno, pitch_words, n_it, cst, items4 + o, rows, nblk, pos, Lw, Rw, sflags, n_snp,     \
+                       ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss)
     if (which & 1) {
         if (dom) NLDSC_BAND(true, false, false);
         else if (add_all) NLDSC_BAND(false, false, true);
         else NLDSC_BAND(false, false, false);
     }
+    chunk = n_items4;
     if (blk_rep && (which & 2)) {
         if (dom) NLDSC_BAND(true, true, false);
         else if (add_all) NLDSC_BAND(false, true, true);
