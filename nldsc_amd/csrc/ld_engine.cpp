@@ -166,7 +166,10 @@ struct nldsc_engine {
     // missing calls with the four additive products per pair — C2 band 2.29 -> 4.13 ms (profiles/r03_ab_quad_add_rejected.json:
     // short rows, one wave per SIMD, whole 64 x 64 tiles at the band edges)
     bool quad_add = false;
-    bool q_rounds = false;  // $NLDSC_Q_ROUNDS=1 (study): quad super-items in launches of one workgroup per CU
+    // quad super-items in launches of one workgroup per CU when there are at least 16 such rounds ($NLDSC_Q_ROUNDS=0:
+    // one launch): the workgroups on an XCD then stream their shared strips at nearby K offsets; C5 slice band
+    // 351 -> 333 ms, C3 missing-free (6 rounds, below the threshold) 12.34 -> 12.51 ms (profiles/r03_ab_q_rounds.json)
+    bool q_rounds = true;
     int last_band_kernel = NLDSC_BAND_F4;
     DevBuf<double> pos, maf, rstd, l2_acc, l2d_acc, l2, l2d;
     DevBuf<int4> items;
@@ -874,7 +877,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                                            e->plan_rows.p, nblk, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
                                            p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p,
                                            e->l2d_acc.p, e->ws_acc.p, true, blk_rep, e->blk_miss.p, which, st, quad_add,
-                                           e->q_rounds && n_items2 >= 4 * e->n_cu ? e->n_cu : 0);
+                                           e->q_rounds && n_items2 >= 16 * e->n_cu ? e->n_cu : 0);
         return nldsc::launch_band_f4_t2(
             dom, n_items2, geno, pitch_words, n_it, e->cst.p, e->items2.p, e->plan_rows.p, nblk, e->pos.p, e->Lw.p,
             e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,

@@ -1051,3 +1051,26 @@ def test_round_launches_with_replayed_rare_variants_in_the_tail(engine):
     assert np.isfinite(exp["residuals_std"][is_rare]).all()
     np.testing.assert_array_equal(sub["residuals_std"][is_rare], exp["residuals_std"][is_rare])
     assert_ld_close(sub, exp, label="rounds + replayed rare tail vs oracle")
+
+
+def test_quad_round_launches_bitwise_one_launch(engine):
+    """Missing-free bands of many 4 x 4 super-items (a C5-shaped slice: 1000 kb windows, 288 bp per SNP) run the quad
+    kernel in launches of one workgroup per CU ($NLDSC_Q_ROUNDS, from 16 such rounds): bitwise the one-launch results
+    ($NLDSC_Q_ROUNDS=0) — the per-SNP sums are order-independent fixed point."""
+    from nldsc_amd import synth
+    from nldsc_amd.engine import Engine
+    N, M = 2053, 150_000
+    buf, pos = synth.device_bed(M, N, seed=5, length_cm=288.0 * M, missing=0.0)
+    args = (1.0e6, 1e-4, 1e-5, 1.0 / M, pos)
+
+    def fresh():
+        with Engine(0) as e:
+            e.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
+            r = e.run(*args)
+            assert e.timings()["band_kernel"] == "f4_quad"
+            return r
+    got = fresh()
+    ref = _env_run("NLDSC_Q_ROUNDS", "0", fresh)
+    for k in got:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    assert (got["l2_ws"] > 5000).all()
