@@ -106,10 +106,43 @@ def assemble(arr: np.ndarray, spans: list[tuple[int, int]], n_snp: int) -> dict:
     return full
 
 
+_ASSEMBLY: dict = {}
+
+
+def _assemble_device(blocks, spans: list[tuple[int, int]], n_snp: int) -> dict:
+    """Rank 0 with RCCL: the gathered [world, 7, width] device block -> the [7, n_snp] table in device memory (one
+    strided copy per rank), then one copy into a pinned host buffer (both buffers reused across calls), so only
+    the table itself crosses PCIe, not every rank's padded block, and no per-key host copies follow."""
+    import torch
+    key = (blocks.device, n_snp)
+    if key not in _ASSEMBLY:
+        _ASSEMBLY.clear()
+        _ASSEMBLY[key] = (torch.empty((len(RESULT_KEYS), n_snp), dtype=torch.float64, device=blocks.device),
+                          torch.empty((len(RESULT_KEYS), n_snp), dtype=torch.float64, pin_memory=True))
+    full, host = _ASSEMBLY[key]
+    covered = 0
+    for g, (a, b) in enumerate(spans):
+        if b > a:
+            full[:, a:b].copy_(blocks[g, :, : b - a])
+            covered += b - a
+    if covered != n_snp:  # (shard_ranges covers every SNP; other span sets leave the rest as not computed)
+        own = np.zeros(n_snp, bool)
+        for a, b in spans:
+            own[a:b] = True
+        idx = torch.from_numpy(np.flatnonzero(~own)).to(full.device)
+        full[:4, idx] = float("nan")
+        full[4:, idx] = -1.0
+    host.copy_(full, non_blocking=True)
+    torch.cuda.current_stream(full.device).synchronize()
+    h = host.numpy()
+    return {k: (h[i] if i < 4 else h[i].astype(np.int32)) for i, k in enumerate(RESULT_KEYS)}
+
+
 def gather_table(table, spans: list[tuple[int, int]], n_snp: int, *, out=None) -> dict | None:
     """One all_gather of every rank's [7, width] fp64 table block (torch tensor; with RCCL it stays in device
-    memory until rank 0 copies the gathered [world, 7, width] block to the host); the full result dict on rank 0,
-    None elsewhere.  `out`: a reusable flat buffer of world * 7 * width elements on the table's device."""
+    memory and rank 0 assembles the table there before one copy to pinned host memory); the full result dict on
+    rank 0, None elsewhere.  `out`: a reusable flat buffer of world * 7 * width elements on the table's device.
+    (Rank 0's float arrays are views of a pinned buffer reused by the next call.)"""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(), dist.get_rank()
@@ -118,7 +151,10 @@ def gather_table(table, spans: list[tuple[int, int]], n_snp: int, *, out=None) -
     dist.all_gather_into_tensor(out, table.reshape(-1))
     if rank != 0:
         return None
-    return assemble(out.view((world,) + tuple(table.shape)).cpu().numpy(), spans, n_snp)
+    blocks = out.view((world,) + tuple(table.shape))
+    if blocks.is_cuda:
+        return _assemble_device(blocks, spans, n_snp)
+    return assemble(blocks.numpy(), spans, n_snp)
 
 
 def gather_ranges(local: dict, own: tuple[int, int], n_snp: int, *, device=None,
