@@ -1073,4 +1073,4 @@ def test_quad_round_launches_bitwise_one_launch(engine):
     ref = _env_run("NLDSC_Q_ROUNDS", "0", fresh)
     for k in got:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
-    assert (got["l2_ws"] > 5000).all()
+    assert (got["l2_ws"] > 3000).all()  # (a half window at the chromosome ends)
