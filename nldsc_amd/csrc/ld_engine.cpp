@@ -140,6 +140,12 @@ struct nldsc_engine {
     DevBuf<uint8_t> sflags;
     DevBuf<uint8_t> blk_rep;  // per 32-SNP block: holds a rare variant with replayed fp32 vectors (KC items)
     DevBuf<float> gram;       // K-split partial Gram tiles
+    // rare-variant items of the single-block fp4 kernel, deferred: their Gram tiles (8192 floats per block pair), the
+    // block pairs, the slot counter (launch_band_f4 rep_gram; $NLDSC_DEFER_REP=0: the separate KC launch instead)
+    DevBuf<float> rep_gram;
+    DevBuf<int4> rep_items;
+    DevBuf<int> rep_count;
+    bool defer_rep = true;
     bool ksplit_ok = true;    // $NLDSC_KSPLIT=0 disables the K-split
     int tail_ksplit = 0;      // $NLDSC_TAIL_KSPLIT=P > 0 forces the round launches' tail split (study knob; 0: model)
     bool replay_overlap = true;  // $NLDSC_REPLAY_OVERLAP=0 runs the rare-variant replay in line on the main stream
@@ -206,6 +212,7 @@ struct nldsc_engine {
         bed.release(); stage_dev.release(); lastb.release(); flip.release(); row_miss.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
         ws3.release(); lut.release(); cst.release(); sflags.release(); pos.release(); maf.release(); rstd.release();
         l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release(); gram.release();
+        rep_gram.release(); rep_items.release(); rep_count.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         if (ev_plan) (void)hipEventDestroy(ev_plan);
         Ew.release(); plan_counts.release(); plan_meta.release(); plan_rows.release();
@@ -327,6 +334,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_F4_NC2")) e->f4_nc2 = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_QUAD_ADD")) e->quad_add = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_Q_ROUNDS")) e->q_rounds = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_DEFER_REP")) e->defer_rep = std::atoi(v) != 0;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
@@ -860,6 +868,10 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // 2.8 -> 5.1 ms.  The last, partial round leaves wave slots idle for a whole item length (C3: 1 458 items in
     // 2 048 slots); those items are K-split instead when the cost model finds it cheaper (C3: P = 7, 5 rounds of 1/7
     // of an item).
+    // rare-variant items of the single-block fp4 kernel run their K loops in the main launch (Gram tiles kept), their
+    // epilogues after the replay (launch_band_f4 rep_gram): unsegmented rows, no K-split of the whole band (whose
+    // partial kernel already runs every item)
+    const bool defer = replay && e->defer_rep && use_f4 && ksplit == 1 && n_it <= nldsc::F4_SEG_CHUNKS;
     auto size_single = [&]() -> hipError_t {
         round_items = use_f4 && ksplit == 1 && e->band_rounds && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 1024 &&
                       n_single >= 4 * slots ? slots : 0;
@@ -869,6 +881,14 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         n_full = tail_p > 1 ? n_single - tail : n_single;
         e->last_round_items = round_items;
         e->last_tail_ksplit = tail_p;
+        if (defer && n_full > 0) {  // slots for every block pair of the main launch (an upper bound)
+            const size_t slots = (size_t)n_full * (nc2 ? 2 : 1);
+            hipError_t r = e->rep_gram.ensure(slots * 8192);
+            if (r == hipSuccess) r = e->rep_items.ensure(slots);
+            if (r == hipSuccess) r = e->rep_count.ensure(1);
+            if (r == hipSuccess) r = hipMemsetAsync(e->rep_count.p, 0, sizeof(int), st);
+            if (r != hipSuccess) return r;
+        }
         return tail_p > 1 ? e->gram.ensure((size_t)tail * tail_p * 8192) : hipSuccess;
     };
     auto launch_super = [&](int which) -> hipError_t {
@@ -902,11 +922,19 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                 if (r == hipSuccess) r = hipStreamWaitEvent(e->band_stream2, e->ev_fork, 0);
                 if (r != hipSuccess) return r;
             }
+            const bool dfr = defer && n_full > 0;
             hipError_t r = nldsc::launch_band_f4(dom, nc2 ? 2 : 1, n_full, geno, pitch_words, n_it, e->cst.p, single,
                                                  e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N,
                                                  p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                                  e->ws_acc.p, true, blk_rep, which, st, single_miss, round_items,
-                                                 route_shift, two ? e->band_stream2 : nullptr);
+                                                 route_shift, two ? e->band_stream2 : nullptr,
+                                                 dfr ? e->rep_gram.p : nullptr, dfr ? e->rep_items.p : nullptr,
+                                                 dfr ? e->rep_count.p : nullptr);
+            if (r == hipSuccess && dfr && (which & 2))  // after the replay: the deferred items' epilogues
+                r = nldsc::launch_band_f4_deferred_epi(dom, n_full * (nc2 ? 2 : 1), e->cst.p, e->rep_items.p,
+                                                       e->rep_count.p, e->rep_gram.p, e->pos.p, e->Lw.p, e->Rw.p,
+                                                       e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin,
+                                                       own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, blk_rep, st);
             if (two) {
                 hipError_t rj = hipEventRecord(e->ev_join, e->band_stream2);
                 if (rj == hipSuccess) rj = hipStreamWaitEvent(st, e->ev_join, 0);

@@ -97,7 +97,17 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
                           int which, hipStream_t st, const uint8_t* blk_miss = nullptr, int round_items = 0,
-                          int route_shift = 1, hipStream_t st2 = nullptr);  // st2: odd round launches
+                          int route_shift = 1, hipStream_t st2 = nullptr,  // st2: odd round launches
+                          float* rep_gram = nullptr, int4* rep_items = nullptr, int* rep_count = nullptr);
+// rep_gram (unsegmented rows): the items holding a replayed rare variant run their K loops in the main launch and store
+// each block pair's exact Gram tiles (rep_gram slot = atomicAdd(rep_count), 8192 floats; rep_items[slot] = the block
+// pair); after the replay, launch_band_f4_deferred_epi runs their epilogues (max_items >= the slots used) in place of
+// the KC launch
+hipError_t launch_band_f4_deferred_epi(bool dom, int max_items, const SnpConst* cst, const int4* rep_items,
+                                      const int* rep_count, const float* rep_gram, const double* pos, const int* Lw,
+                                      const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind, double n_org,
+                                      double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
+                                      int* ws_acc, const uint8_t* blk_rep, hipStream_t st);
 // the same with the K loop split in P pieces (small launches: better filled wave slots): partial Gram tiles to
 // `gram` (n_items * P * 8192 floats), then an epilogue kernel (unsegmented rows, n_it <= F4_SEG_CHUNKS)
 hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* geno, int pitch_words, int n_it,

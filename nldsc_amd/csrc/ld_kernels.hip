@@ -1304,7 +1304,7 @@ __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpCons
 template <bool KC>
 __device__ __forceinline__ bool skip_item(const uint8_t* blk_rep, int4 it) {
     if (!KC && blk_rep == nullptr) return false;
-    const bool rep = blk_rep[it.x] | blk_rep[it.y];
+    const bool rep = blk_rep[it.x] | blk_rep[it.y] | (it.z == 2 && blk_rep[it.y + 1]);  // (it.z: column blocks)
     return KC ? !rep : rep;
 }
 
@@ -1756,11 +1756,41 @@ __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __rest
                                                         int own_lo, int own_hi, double* __restrict__ l2_acc,
                                                         double* __restrict__ l2d_acc, int* __restrict__ ws_acc, int xcd,
                                                         const uint8_t* __restrict__ blk_rep,
-                                                        const uint8_t* __restrict__ blk_miss, int route_shift) {
+                                                        const uint8_t* __restrict__ blk_miss, int route_shift,
+                                                        float* __restrict__ rep_gram, int4* __restrict__ rep_items,
+                                                        int* __restrict__ rep_count) {
     __shared__ BandI8Lds sh;
     __shared__ float tr[32 * 33];
     const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
-    if (skip_item<KC>(blk_rep, it)) return;
+    if (skip_item<KC>(blk_rep, it)) {
+        // rep_gram (unsegmented rows): an item holding a replayed rare variant runs its K loop here anyway, storing the
+        // exact Gram tiles of each of its block pairs in a slot of rep_gram; band_f4_epi_kernel<DOM, true> applies the
+        // epilogue (with the ka / kr terms) after the replay — so these items neither wait for the replay nor form a
+        // launch of their own (one partial round of wave slots, or the whole band when most blocks hold such SNPs)
+        if constexpr (!KC && SEG == 0) {
+            if (rep_gram != nullptr) {
+                const int nblk = (n_snp + 31) >> 5, lane = threadIdx.x & 63;
+                for (int c = 0; c < (NCX == 2 ? it.z : 1); ++c) {
+                    const int4 one = make_int4(it.x, it.y + c, 1, 0);
+                    if (blk_miss != nullptr && routed_item(blk_miss, route_shift, one.x, one.y, nblk)) continue;
+                    int slot = 0;
+                    if (lane == 0) slot = atomicAdd(rep_count, 1);
+                    slot = __shfl(slot, 0, 64);
+                    if (lane == 0) rep_items[slot] = one;
+                    __syncthreads();  // (the body rewrites the slot tables)
+                    if (one.y == one.x)
+                        band_f4_body<DOM, 1, true, 0, false, true>(sh, one, geno, pitch_words, n_it, cst, pos, Lw, Rw,
+                                                                   sflags, n_snp, 0.0, 0.0, 0.0, 0, 0, nullptr, nullptr,
+                                                                   nullptr, tr, 0, n_it, rep_gram + (size_t)slot * 8192);
+                    else
+                        band_f4_body<DOM, 1, false, 0, false, true>(sh, one, geno, pitch_words, n_it, cst, pos, Lw, Rw,
+                                                                    sflags, n_snp, 0.0, 0.0, 0.0, 0, 0, nullptr, nullptr,
+                                                                    nullptr, tr, 0, n_it, rep_gram + (size_t)slot * 8192);
+                }
+            }
+        }
+        return;
+    }
 #define NLDSC_BODY(NC_, DIAG_, IT_)                                                                                   \
     band_f4_body<DOM, NC_, DIAG_, SEG, KC>(sh, IT_, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, \
                                            n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, tr)
@@ -2333,11 +2363,15 @@ __global__ void __launch_bounds__(64, 2) band_f4_epi_kernel(const SnpConst* __re
                                                           double* __restrict__ l2d_acc, int* __restrict__ ws_acc,
                                                           const uint8_t* __restrict__ blk_rep, int P,
                                                           const float* __restrict__ gram,
-                                                          const uint8_t* __restrict__ blk_miss, int route_shift) {
+                                                          const uint8_t* __restrict__ blk_miss, int route_shift,
+                                                          const int* __restrict__ count = nullptr) {
     __shared__ BandI8Lds sh;
     __shared__ float tr[32 * 33];
+    // count: the deferred rare-variant list of the single-block kernel (rep_items, P = 1): its first *count entries,
+    // every one run (a pair item's block without a replayed SNP is listed too)
+    if (count != nullptr && (int)blockIdx.x >= *count) return;
     const int4 it = items[blockIdx.x];
-    if (skip_item<KC>(blk_rep, it)) return;
+    if (count == nullptr && skip_item<KC>(blk_rep, it)) return;
     if (blk_miss != nullptr && routed_item(blk_miss, route_shift, it.x, it.y, (n_snp + 31) >> 5)) return;
     const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
     const int I = it.x, J = it.y;
@@ -2732,11 +2766,28 @@ hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* ge
 #define NLDSC_EPI(DOM_, KC_)                                                                                        \
     hipLaunchKernelGGL((band_f4_epi_kernel<DOM_, KC_>), dim3(n_items), dim3(64), 0, st, cst, items, pos, Lw, Rw,    \
                        sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, blk_rep, P, gram, \
-                       blk_miss, route_shift)
+                       blk_miss, route_shift, nullptr)
     if (dom) NLDSC_EPI(true, false); else NLDSC_EPI(false, false);
 kc:
     if (blk_rep && (which & 2)) { if (dom) NLDSC_EPI(true, true); else NLDSC_EPI(false, true); }
 #undef NLDSC_EPI
+    return hipGetLastError();
+}
+
+hipError_t launch_band_f4_deferred_epi(bool dom, int max_items, const SnpConst* cst, const int4* rep_items,
+                                      const int* rep_count, const float* rep_gram, const double* pos, const int* Lw,
+                                      const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind, double n_org,
+                                      double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
+                                      int* ws_acc, const uint8_t* blk_rep, hipStream_t st) {
+    if (max_items <= 0) return hipSuccess;
+    if (dom)
+        hipLaunchKernelGGL((band_f4_epi_kernel<true, true>), dim3(max_items), dim3(64), 0, st, cst, rep_items, pos, Lw,
+                           Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, blk_rep,
+                           1, rep_gram, nullptr, 1, rep_count);
+    else
+        hipLaunchKernelGGL((band_f4_epi_kernel<false, true>), dim3(max_items), dim3(64), 0, st, cst, rep_items, pos,
+                           Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc,
+                           blk_rep, 1, rep_gram, nullptr, 1, rep_count);
     return hipGetLastError();
 }
 
@@ -2745,7 +2796,7 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
                           int which, hipStream_t st, const uint8_t* blk_miss, int round_items, int route_shift,
-                          hipStream_t st2) {
+                          hipStream_t st2, float* rep_gram, int4* rep_items, int* rep_count) {
     if (n_items <= 0) return hipSuccess;
     // single block-pair items, or (additive-only, unsegmented rows) column-block pairs
     if (max_nc != 1 && !(max_nc == 2 && !dom && n_it <= F4_SEG_CHUNKS)) return hipErrorInvalidValue;
@@ -2758,7 +2809,8 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
     hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_, KC_, NCX_>), dim3(std::min(chunk, n_items - o)), dim3(64), 0, \
                        (st2 != nullptr && (r & 1)) ? st2 : st, geno, pitch_words,                                   \
                        n_it, cst, items + o, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi,       \
-                       l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss, route_shift)
+                       l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss, route_shift, SEG_ ? nullptr : rep_gram, \
+                       rep_items, rep_count)
 #define NLDSC_BAND(DOM_, WPS_, SEG_, KC_) NLDSC_BAND_NC(DOM_, WPS_, SEG_, KC_, 1)
 #define NLDSC_PICK(KC_)                                                                                              \
     if (n_it > F4_SEG_CHUNKS) { if (dom) NLDSC_BAND(true, 1, F4_SEG_CHUNKS, KC_); else NLDSC_BAND(false, 2, F4_SEG_CHUNKS, KC_); } \
@@ -2769,7 +2821,8 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
     if (which & 1) { NLDSC_PICK(false); }
     chunk = n_items;
     st2 = nullptr;
-    if (blk_rep && (which & 2)) { NLDSC_PICK(true); }
+    // (with rep_gram the KC items ran their K loops in the main launch: launch_band_f4_deferred_epi after the replay)
+    if (blk_rep && (which & 2) && (rep_gram == nullptr || n_it > F4_SEG_CHUNKS)) { NLDSC_PICK(true); }
 #undef NLDSC_PICK
 #undef NLDSC_BAND
 #undef NLDSC_BAND_NC

@@ -1074,3 +1074,45 @@ def test_quad_round_launches_bitwise_one_launch(engine):
     for k in got:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
     assert (got["l2_ws"] > 3000).all()  # (a half window at the chromosome ends)
+
+
+@pytest.mark.parametrize("dom", [False, True])
+def test_deferred_rare_variant_items_bitwise_kc_launch(engine, dom):
+    """Items holding a replayed rare variant run their K loops in the main single-block launch and their epilogues
+    after the replay from stored Gram tiles ($NLDSC_DEFER_REP, the default): bitwise the separate KC launch
+    ($NLDSC_DEFER_REP=0).  Additive-only: a rare variant only in the second column block of a column-block pair item
+    (block 1 of item (0, 0, 2)) — that pair must take the ka terms too — and equal to single-block items
+    ($NLDSC_F4_NC2=0)."""
+    from nldsc_amd import synth
+    from nldsc_amd.engine import Engine
+    N, M = 50_000, 320
+    spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=2.0, seed=91, missing=0.01)
+    g = synth.genotypes(spec)
+    rng = np.random.default_rng(3)
+    for j in (40, 41, 200):  # rare: 100 het, 8 hom-A2 calls (<= 16 in a class: replayed), 1 % missing
+        r = np.zeros(N, np.int8)
+        r[rng.choice(N, 108, replace=False)[:100]] = 1
+        r[rng.choice(np.flatnonzero(r == 0), 8, replace=False)] = 2
+        r[rng.random(N) < 0.01] = -1
+        g[j] = r
+    rows = synth.pack_bed_rows(g)
+    pos = synth.positions_cm(spec)
+    flags = MODES["f4"] | (0 if dom else _lib_flag("FLAG_ADDITIVE_ONLY"))
+    args = (1.0, 1e-4, 1e-5, 1.0 / M, pos)
+
+    def fresh():
+        with Engine(0) as e:
+            e.load_bed_bytes(synth.bed_bytes(rows), M, N)
+            return e.run(*args, flags=flags)
+    ksplit_off = lambda fn: _env_run("NLDSC_KSPLIT", "0", fn)  # noqa: E731  (small launch: no whole-band K-split)
+    got = ksplit_off(fresh)
+    refs = {"kc_launch": ksplit_off(lambda: _env_run("NLDSC_DEFER_REP", "0", fresh))}
+    if not dom:
+        refs["single_blocks"] = ksplit_off(lambda: _env_run("NLDSC_F4_NC2", "0", fresh))
+    for name, ref in refs.items():
+        for k in got:
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{name} {k}")
+    exp = O.run_c(synth.bed_bytes(rows), M, N, *args)
+    if not dom:
+        exp = dict(exp, l2d=np.full(M, np.nan), l2d_ws=np.full(M, -1, np.int32), l2d_wse=np.full(M, -1, np.int32))
+    assert_ld_close(got, exp, label=f"deferred rare dom={dom}")
