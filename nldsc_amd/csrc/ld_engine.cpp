@@ -114,8 +114,6 @@ struct nldsc_engine {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t plan_stream = nullptr;  // the GPU schedule runs here, beside the count kernel
-    hipStream_t band_stream2 = nullptr;  // odd round launches when $NLDSC_BAND_STREAMS=2
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t ev_pos = nullptr;        // positions uploaded (the schedule's only input)
     hipEvent_t ev[6] = {};
     hipEvent_t ev_dbg[2] = {};  // $NLDSC_DEBUG_TIMING: after the super-item launch, before the single-block launches
@@ -147,7 +145,6 @@ struct nldsc_engine {
     DevBuf<int> rep_count;
     bool defer_rep = true;
     bool ksplit_ok = true;    // $NLDSC_KSPLIT=0 disables the K-split
-    int tail_ksplit = 0;      // $NLDSC_TAIL_KSPLIT=P > 0 forces the round launches' tail split (study knob; 0: model)
     bool replay_overlap = true;  // $NLDSC_REPLAY_OVERLAP=0 runs the rare-variant replay in line on the main stream
     int last_ksplit = 1;
     int last_round_items = 0;
@@ -162,10 +159,6 @@ struct nldsc_engine {
     bool f4_nc2 = true;
     // single-block fp4 band in launches of one round of wave slots ($NLDSC_BAND_ROUNDS=0: one launch)
     bool band_rounds = true;
-    // round launches alternated over two streams ($NLDSC_BAND_STREAMS=2): round k + 1's workgroups take the wave
-    // slots round k's finished items free (two rounds in flight at most)
-    int band_streams = 1;
-    bool compact = true;  // $NLDSC_COMPACT=0: routed runs list every single-block item (routed ones return at once)
     DevBuf<uint8_t> blk_miss;
     DevBuf<uint8_t> blk_zero;  // additive-only quad runs: the routing array of the other kernels (all super-items routed)
     // $NLDSC_QUAD_ADD=1 (study, off): additive-only runs send every 4 x 4 super-item to the quad kernel, those holding
@@ -222,11 +215,8 @@ struct nldsc_engine {
         if (ev_pos) (void)hipEventDestroy(ev_pos);
         if (ev_stats) (void)hipEventDestroy(ev_stats);
         if (ev_replay) (void)hipEventDestroy(ev_replay);
-        if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_route) (void)hipEventDestroy(ev_route);
         items_u.release(); compact_tmp.release();
-        if (ev_join) (void)hipEventDestroy(ev_join);
-        if (band_stream2) (void)hipStreamDestroy(band_stream2);
     }
 };
 
@@ -324,12 +314,9 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_GPU_PLAN")) e->gpu_plan = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_ORIENT")) e->orient = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_KSPLIT")) e->ksplit_ok = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_TAIL_KSPLIT")) e->tail_ksplit = std::max(0, std::min(8, std::atoi(v)));
     if (const char* v = std::getenv("NLDSC_REPLAY_OVERLAP")) e->replay_overlap = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_T2")) e->t2_mode = std::max(0, std::min(3, std::atoi(v)));
     if (const char* v = std::getenv("NLDSC_BAND_ROUNDS")) e->band_rounds = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_BAND_STREAMS")) e->band_streams = std::atoi(v) == 2 ? 2 : 1;
-    if (const char* v = std::getenv("NLDSC_COMPACT")) e->compact = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_DEBUG_TIMING")) e->debug_timing = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_F4_NC2")) e->f4_nc2 = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_QUAD_ADD")) e->quad_add = std::atoi(v) != 0;
@@ -342,11 +329,6 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     }
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->plan_stream, hipStreamNonBlocking);
-    if (he == hipSuccess && e->band_streams == 2) {
-        he = hipStreamCreateWithFlags(&e->band_stream2, hipStreamNonBlocking);
-        if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
-        if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
-    }
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_pos, hipEventDisableTiming);
     for (auto& ev : e->ev)
         if (he == hipSuccess) he = hipEventCreate(&ev);
@@ -759,7 +741,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
             HIPCHK(e->blk_zero.ensure((size_t)nblk));
             HIPCHK(hipMemsetAsync(e->blk_zero.p, 0, (size_t)nblk, ps));
         }
-        compact = use_t2 && routed && n_items > 0 && e->compact;
+        compact = use_t2 && routed && n_items > 0;
         if (compact) {
             const size_t n_chunks = ((size_t)n_items + 1023) / 1024;
             HIPCHK(e->items_u.ensure((size_t)n_items));
@@ -877,7 +859,6 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                       n_single >= 4 * slots ? slots : 0;
         const int tail = round_items > 0 ? n_single % round_items : 0;
         tail_p = tail > 0 ? choose_ksplit(tail) : 1;
-        if (tail > 0 && e->tail_ksplit > 0 && !nc2 && 2 * e->tail_ksplit <= n_it) tail_p = e->tail_ksplit;
         n_full = tail_p > 1 ? n_single - tail : n_single;
         e->last_round_items = round_items;
         e->last_tail_ksplit = tail_p;
@@ -903,7 +884,6 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
             e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
             e->ws_acc.p, true, blk_rep, routed ? e->blk_miss.p : nullptr, which, st);
     };
-    // (uncompacted routed list, $NLDSC_COMPACT=0: the kernels skip the items a super-item kernel takes)
     // (column-block pair items: the compaction keeps an item while one of its blocks is unrouted, the kernel drops
     // the other)
     const uint8_t* single_miss =
@@ -915,19 +895,12 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                                                p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p,
                                                blk_rep, e->gram.p, which, st);
         if (use_f4) {
-            // (two band streams: the odd rounds go to band_stream2, forked from and joined back into `st`)
-            const bool two = round_items > 0 && e->band_stream2 != nullptr && (which & 1);
-            if (two) {
-                hipError_t r = hipEventRecord(e->ev_fork, st);
-                if (r == hipSuccess) r = hipStreamWaitEvent(e->band_stream2, e->ev_fork, 0);
-                if (r != hipSuccess) return r;
-            }
             const bool dfr = defer && n_full > 0;
             hipError_t r = nldsc::launch_band_f4(dom, nc2 ? 2 : 1, n_full, geno, pitch_words, n_it, e->cst.p, single,
                                                  e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N,
                                                  p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
                                                  e->ws_acc.p, true, blk_rep, which, st, single_miss, round_items,
-                                                 route_shift, two ? e->band_stream2 : nullptr,
+                                                 route_shift,
                                                  dfr ? e->rep_gram.p : nullptr, dfr ? e->rep_items.p : nullptr,
                                                  dfr ? e->rep_count.p : nullptr);
             if (r == hipSuccess && dfr && (which & 2))  // after the replay: the deferred items' epilogues
@@ -935,11 +908,6 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                                                        e->rep_count.p, e->rep_gram.p, e->pos.p, e->Lw.p, e->Rw.p,
                                                        e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin,
                                                        own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, blk_rep, st);
-            if (two) {
-                hipError_t rj = hipEventRecord(e->ev_join, e->band_stream2);
-                if (rj == hipSuccess) rj = hipStreamWaitEvent(st, e->ev_join, 0);
-                if (r == hipSuccess) r = rj;
-            }
             if (r != hipSuccess || n_full == n_single) return r;
             return nldsc::launch_band_f4_split(dom, tail_p, n_single - n_full, geno, pitch_words, n_it, e->cst.p,
                                                single + n_full, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
@@ -967,7 +935,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
             n_single = *cnt;
             single = e->items_u.p;
         } else if (use_t2 && routed) {
-            single = e->items.p;  // $NLDSC_COMPACT=0: every item listed, the routed ones return at once
+            single = e->items.p;  // (no compaction: every item listed, the routed ones return at once)
         }
         HIPCHK(size_single());
         const auto t_wait1 = std::chrono::steady_clock::now();

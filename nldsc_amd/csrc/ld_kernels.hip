@@ -2796,7 +2796,7 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
                           int which, hipStream_t st, const uint8_t* blk_miss, int round_items, int route_shift,
-                          hipStream_t st2, float* rep_gram, int4* rep_items, int* rep_count) {
+                          float* rep_gram, int4* rep_items, int* rep_count) {
     if (n_items <= 0) return hipSuccess;
     // single block-pair items, or (additive-only, unsegmented rows) column-block pairs
     if (max_nc != 1 && !(max_nc == 2 && !dom && n_it <= F4_SEG_CHUNKS)) return hipErrorInvalidValue;
@@ -2805,9 +2805,9 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
     // not the KC launch (items holding a replayed rare variant: few, the others return at once)
     int chunk = round_items > 0 ? round_items : n_items;
 #define NLDSC_BAND_NC(DOM_, WPS_, SEG_, KC_, NCX_)                                                                  \
-    for (int o = 0, r = 0; o < n_items; o += chunk, ++r)                                                          \
+    for (int o = 0; o < n_items; o += chunk)                                                                      \
     hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_, KC_, NCX_>), dim3(std::min(chunk, n_items - o)), dim3(64), 0, \
-                       (st2 != nullptr && (r & 1)) ? st2 : st, geno, pitch_words,                                   \
+                       st, geno, pitch_words,                                                                         \
                        n_it, cst, items + o, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi,       \
                        l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss, route_shift, SEG_ ? nullptr : rep_gram, \
                        rep_items, rep_count)
@@ -2820,7 +2820,6 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
     // segmented kernel: the add+dom variant needs more than 256 registers (2 waves / SIMD would spill)
     if (which & 1) { NLDSC_PICK(false); }
     chunk = n_items;
-    st2 = nullptr;
     // (with rep_gram the KC items ran their K loops in the main launch: launch_band_f4_deferred_epi after the replay)
     if (blk_rep && (which & 2) && (rep_gram == nullptr || n_it > F4_SEG_CHUNKS)) { NLDSC_PICK(true); }
 #undef NLDSC_PICK
