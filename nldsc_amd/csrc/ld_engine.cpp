@@ -132,7 +132,16 @@ struct nldsc_engine {
     int32_t n_snp = 0, n_org = 0;
     // work buffers
 
-    DevBuf<int> counts, Lw, Rw, Aw, ws_acc, ws3;
+    DevBuf<int> counts, Lw, Rw, Aw, ws_acc;
+    // the per-SNP results, one allocation: L2, L2D, MAF, RSTD (fp64) then WSA, WSD, WSDE (int32), each M long, so the
+    // owned slices come back in two strided copies (one when a run owns every SNP)
+    DevBuf<double> res;
+    template <class T>
+    struct View {
+        T* p = nullptr;
+    };
+    View<double> l2, l2d, maf, rstd;
+    View<int> ws3;
     DevBuf<float2> lut;
     DevBuf<nldsc::SnpConst> cst;
     DevBuf<uint8_t> sflags;
@@ -170,7 +179,7 @@ struct nldsc_engine {
     // 351 -> 333 ms, C3 missing-free (6 rounds, below the threshold) 12.34 -> 12.51 ms (profiles/r03_ab_q_rounds.json)
     bool q_rounds = true;
     int last_band_kernel = NLDSC_BAND_F4;
-    DevBuf<double> pos, maf, rstd, l2_acc, l2d_acc, l2, l2d;
+    DevBuf<double> pos, l2_acc, l2d_acc;
     DevBuf<int4> items;
     // host scratch
     std::vector<uint8_t> h_flags, h_all_pass;
@@ -203,8 +212,8 @@ struct nldsc_engine {
     ~nldsc_engine() {
         (void)hipSetDevice(device);
         bed.release(); stage_dev.release(); lastb.release(); flip.release(); row_miss.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
-        ws3.release(); lut.release(); cst.release(); sflags.release(); pos.release(); maf.release(); rstd.release();
-        l2_acc.release(); l2d_acc.release(); l2.release(); l2d.release(); items.release(); gram.release();
+        res.release(); lut.release(); cst.release(); sflags.release(); pos.release();
+        l2_acc.release(); l2d_acc.release(); items.release(); gram.release();
         rep_gram.release(); rep_items.release(); rep_count.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         if (ev_plan) (void)hipEventDestroy(ev_plan);
@@ -597,16 +606,17 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     HIPCHK(e->sflags.ensure((size_t)Mpad));
     HIPCHK(e->blk_rep.ensure((size_t)nblk));
     HIPCHK(e->pos.ensure((size_t)M));
-    HIPCHK(e->maf.ensure((size_t)M));
-    HIPCHK(e->rstd.ensure((size_t)M));
+    HIPCHK(e->res.ensure(4 * (size_t)M + (3 * (size_t)M + 1) / 2));
+    e->l2.p = e->res.p;
+    e->l2d.p = e->l2.p + M;
+    e->maf.p = e->l2d.p + M;
+    e->rstd.p = e->maf.p + M;
+    e->ws3.p = reinterpret_cast<int*>(e->rstd.p + M);
     HIPCHK(e->Lw.ensure((size_t)M));
     HIPCHK(e->Rw.ensure((size_t)M));
     HIPCHK(e->l2_acc.ensure((size_t)M));
     HIPCHK(e->l2d_acc.ensure((size_t)M));
     HIPCHK(e->ws_acc.ensure((size_t)M * 4));  // WSA, WSD, WSDE, non-finite flags
-    HIPCHK(e->l2.ensure((size_t)M));
-    HIPCHK(e->l2d.ensure((size_t)M));
-    HIPCHK(e->ws3.ensure((size_t)M * 3));
 
     // band schedule: on the GPU when every position is >= 0 and sorted (the kernels run ahead of the
     // count and the host only waits for two counters), else the host replay of the reference's pointers
@@ -995,31 +1005,30 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         sw = (double)s[0];
         sd = dom ? (double)s[1] : 0.0;
     } else {
-        // the owned slices land in pinned memory by DMA (pageable copies are staged by the runtime, slower),
-        // then go to the caller's arrays
+        // the owned slices land in pinned memory by DMA (pageable copies are staged by the runtime, slower) in two
+        // strided copies (fp64 rows, int32 rows), then go to the caller's arrays; the pair counts are summed on the GPU
         const size_t o = own_begin, b8 = sizeof(double) * (size_t)std::max(n_own, 0),
                      b4 = sizeof(int) * (size_t)std::max(n_own, 0);
-        double* const dsrc[4] = {e->l2.p + o, e->l2d.p + o, e->maf.p + o, e->rstd.p + o};
         double* const ddst[4] = {r->l2 + o, r->l2d + o, r->maf + o, r->residuals_std + o};
-        int* const isrc[3] = {e->ws3.p + o, e->ws3.p + M + o, e->ws3.p + 2 * (size_t)M + o};
         int32_t* const idst[3] = {r->l2_ws + o, r->l2d_ws + o, r->l2d_wse + o};
-        HIPCHK(hipMemcpyAsync(e->h_sums.p, e->sums.p, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
         if (n_own > 0) {
+            HIPCHK(nldsc::launch_pack_table(e->l2.p, e->l2d.p, e->maf.p, e->rstd.p, e->ws3.p, M, own_begin, own_end,
+                                            n_own, nullptr, e->sums.p, st));
             HIPCHK(e->h_res.ensure(4 * b8 + 3 * b4));
-            for (int k = 0; k < 4; ++k)
-                HIPCHK(hipMemcpyAsync(e->h_res.p + k * b8, dsrc[k], b8, hipMemcpyDeviceToHost, st));
-            for (int k = 0; k < 3; ++k)
-                HIPCHK(hipMemcpyAsync(e->h_res.p + 4 * b8 + k * b4, isrc[k], b4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpy2DAsync(e->h_res.p, b8, e->l2.p + o, sizeof(double) * (size_t)M, b8, 4,
+                                    hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpy2DAsync(e->h_res.p + 4 * b8, b4, e->ws3.p + o, sizeof(int) * (size_t)M, b4, 3,
+                                    hipMemcpyDeviceToHost, st));
         }
+        HIPCHK(hipMemcpyAsync(e->h_sums.p, e->sums.p, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         if (n_own > 0) {
             for (int k = 0; k < 4; ++k) std::memcpy(ddst[k], e->h_res.p + k * b8, b8);
             for (int k = 0; k < 3; ++k) std::memcpy(idst[k], e->h_res.p + 4 * b8 + k * b4, b4);
         }
-        for (int j = own_begin; j < own_end; ++j) {
-            if (r->l2_ws[j] > 0) sw += r->l2_ws[j];
-            if (dom && r->l2d_ws[j] > 0) sd += r->l2d_ws[j];
-        }
+        const unsigned long long* s = reinterpret_cast<const unsigned long long*>(e->h_sums.p);
+        sw = (double)s[0];
+        sd = dom ? (double)s[1] : 0.0;
     }
     auto t_end = std::chrono::steady_clock::now();
 
@@ -1030,6 +1039,14 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     HIPCHK(hipEventElapsedTime(&f, e->ev[3], e->ev[4])); e->ms[3] = f;
     HIPCHK(hipEventElapsedTime(&f, e->ev[4], e->ev[5])); e->ms[4] = f;
     e->ms[5] = std::chrono::duration<double, std::milli>(t_end - t_start).count();
+    if (e->debug_timing) {  // where a run's wall time goes: GPU stages, the gap before the band, host tail
+        float g23 = 0, g05 = 0;
+        HIPCHK(hipEventElapsedTime(&g23, e->ev[2], e->ev[3]));
+        HIPCHK(hipEventElapsedTime(&g05, e->ev[0], e->ev[5]));
+        std::fprintf(stderr, "[nldsc debug] count %.3f stats %.3f gap-to-band %.3f band %.3f finalize %.3f | GPU span %.3f, "
+                     "host total %.3f (host wait for the plan %.3f)\n", e->ms[0], e->ms[1], g23, e->ms[3], e->ms[4], g05,
+                     e->ms[5], e->ms[2]);
+    }
     e->flop_issued = (double)reinterpret_cast<const unsigned long long*>(e->h_sums.p)[2] * 2.0 * BLK * BLK *
                      (double)row_bytes * 4.0;
     e->pairs = sw;

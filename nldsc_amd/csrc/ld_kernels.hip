@@ -2456,6 +2456,9 @@ __global__ void __launch_bounds__(256) pack_table_kernel(const double* __restric
         const double qnan = __builtin_nan("");
         const bool in = g < own_hi;
         const int a = in ? ws3[g] : -1, d = in ? ws3[(size_t)n_snp + g] : -1, x = in ? ws3[2 * (size_t)n_snp + g] : -1;
+        sa = a > 0 ? (unsigned long long)a : 0ull;
+        sd = d > 0 ? (unsigned long long)d : 0ull;
+        if (table == nullptr) goto sum;  // (host-result runs: the pair counts only)
         table[c] = in ? l2[g] : qnan;
         table[(size_t)width + c] = in ? l2d[g] : qnan;
         table[2 * (size_t)width + c] = in ? maf[g] : qnan;
@@ -2463,9 +2466,8 @@ __global__ void __launch_bounds__(256) pack_table_kernel(const double* __restric
         table[4 * (size_t)width + c] = in ? (double)a : qnan;
         table[5 * (size_t)width + c] = in ? (double)d : qnan;
         table[6 * (size_t)width + c] = in ? (double)x : qnan;
-        sa = a > 0 ? (unsigned long long)a : 0ull;
-        sd = d > 0 ? (unsigned long long)d : 0ull;
     }
+sum:
     for (int o = 32; o > 0; o >>= 1) {
         sa += __shfl_down(sa, o, 64);
         sd += __shfl_down(sd, o, 64);
