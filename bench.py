@@ -224,6 +224,9 @@ def main():
     ap.add_argument("--no-file", action="store_true",
                     help="skip the wall clock from a PLINK file (rank 0, N = 1: the synthetic .bed written to "
                          "$TMPDIR, then _ldscore.calculate timed from the file)")
+    ap.add_argument("--duplicate-halo", action="store_true",
+                    help="N > 1: load a two-sided halo and compute the boundary pairs on both ranks (no point-to-point "
+                         "exchange) instead of once, by the rank owning the lower SNP")
     ap.add_argument("--force-dist", action="store_true",
                     help="create the process group and run the sharded path (owned range, device table, collective "
                          "gather) even with one rank: the RCCL code of an N-GPU run rehearsed on one GPU")
@@ -282,6 +285,7 @@ def main():
             raise SystemExit("--rehearse is a single-process mode")
         s_rank, s_world = (int(x) for x in args.rehearse.split("/"))
     split = (s_world > 1 or (args.force_dist and not args.rehearse)) and not args.weak
+    plan = None  # split halo plan (boundary pairs once), when `split`
     buf, pos = synth.device_bed(M, N, seed=7 if split else 7 + rank, length_cm=args.length_cm,
                                 missing=args.missing, device=local)
     eng = Engine(local)
@@ -289,9 +293,19 @@ def main():
     if split:
         # --split: ONE chromosome position-sharded over the ranks (strong scaling): rank g keeps only its
         # owned SNP range plus one window of halo rows resident and computes the owned SNPs
-        from nldsc_amd.distributed import RESULT_KEYS, gather_spans, gather_table, halo_range, shard_ranges, table_width
-        lo, hi = shard_ranges(pos, args.window_cm, s_world)[s_rank]
-        a, b = halo_range(pos, args.window_cm, (lo, hi))
+        from nldsc_amd.distributed import (RESULT_KEYS, exchange_halo, gather_spans, gather_table, halo_range,
+                                           shard_ranges, split_plan, table_width)
+        # boundary pairs once (default): rank g loads its owned range + the right halo, computes the pairs whose lower
+        # SNP it owns and sends the halo's sums to rank g + 1 (one point-to-point block per step); else a two-sided
+        # halo with the boundary pairs computed by both neighbours
+        plan = None if args.duplicate_halo else split_plan(pos, args.window_cm, s_world)
+        if plan is not None:
+            lo, hi, b = plan[s_rank]
+            a = lo
+            n_recv = plan[s_rank - 1][2] - plan[s_rank - 1][1] if s_rank > 0 else 0
+        else:
+            lo, hi = shard_ranges(pos, args.window_cm, s_world)[s_rank]
+            a, b = halo_range(pos, args.window_cm, (lo, hi))
         nb = (N + 3) // 4
         sl = torch.cat([buf[:3], buf[3 + a * nb:3 + b * nb]])
         eng.load_bed_device(sl.data_ptr(), sl.numel(), b - a, N)
@@ -303,6 +317,9 @@ def main():
         table = torch.empty((len(RESULT_KEYS), table_width(spans)), dtype=torch.float64, device=f"cuda:{local}")
         gbuf = torch.empty(world * table.numel(), dtype=torch.float64,
                            device=table.device if coll == "cuda" else "cpu") if use_dist else None
+        if plan is not None:
+            export = torch.empty(6 * max(b - hi, 1), dtype=torch.int64, device=table.device)
+            imported = torch.zeros(6 * max(n_recv, 1), dtype=torch.int64, device=table.device)
     else:
         eng.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
     bed_host = None
@@ -319,7 +336,14 @@ def main():
     def step():
         nonlocal out
         if split:  # owned slice of the one chromosome, then the table assembled on rank 0 (RCCL over xGMI)
-            eng.run_device(w, args.maf, args.std_thr, rsq, pos, table, own=own_rel, flags=flags)
+            if plan is not None:  # (a rehearsal of one rank adds a zero block in place of its neighbour's)
+                n_send = eng.run_device_split(w, args.maf, args.std_thr, rsq, pos, table, export, own=own_rel,
+                                              flags=flags)
+                if use_dist:
+                    exchange_halo(export, n_send, imported, n_recv)
+                eng.run_device_finish(imported, n_recv)
+            else:
+                eng.run_device(w, args.maf, args.std_thr, rsq, pos, table, own=own_rel, flags=flags)
             tim = eng.timings()
             tg = time.perf_counter()
             if use_dist:
@@ -443,8 +467,10 @@ def main():
                 "n_org": N, "n_snp": M, "mean_window": float(ws[ws > 0].mean()),
                 "pairs_per_step_per_gpu": tims[-1]["pairs"],
                 "parallelism": (f"one chromosome position-sharded over {world} GPUs (owned SNP ranges balanced by "
-                                f"pair work, one window of halo rows per rank, score table gathered over "
-                                f"{'RCCL' if coll == 'cuda' else 'gloo'})"
+                                f"pair work, " + ("one window of right-halo rows per rank, boundary pairs computed "
+                                                  "once and the halo's sums sent to the next rank point to point"
+                                                  if plan is not None else "one window of halo rows per rank") +
+                                f", score table gathered over {'RCCL' if coll == 'cuda' else 'gloo'})"
                                 if split else f"position sharding, one chromosome unit per GPU x {world}"),
             },
             "roofline": roof,

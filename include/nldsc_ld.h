@@ -118,6 +118,22 @@ int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begi
 int nldsc_engine_run_device(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32_t own_end,
                             double* table_dev, int32_t width, char* err, size_t errlen);
 
+/* nldsc_engine_run_device in two calls, computing each pair that straddles two ranks' owned ranges once (multi-GPU
+ * strong scaling; no reference counterpart: the reference is single-process, ldscalc.h:34-35).  The loaded slice
+ * holds the owned SNPs [own_begin, own_end) and the right halo [own_end, n_snp) (one window, no left halo).
+ * _split computes the pairs whose lower SNP is owned, accumulates the per-SNP sums of every SNP of the slice, and
+ * writes the right halo's accumulators (exact fixed-point sums and counts) to `export_dev`: device memory of
+ * 6 * export_cap int64 (row-major [6][export_n], export_n = n_snp - own_end <= export_cap), synchronised on return.
+ * The caller sends that block to the rank owning those SNPs (whose slice starts at them) and passes the block
+ * received from the left neighbour to _finish, which adds it to the first import_n owned SNPs (import_n <=
+ * own_end - own_begin; 0 for the first rank), finalizes and writes `table_dev` as nldsc_engine_run_device does.  The
+ * result is bitwise that of nldsc_engine_run_device with the left halo loaded (the sums are integers). */
+int nldsc_engine_run_device_split(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32_t own_end,
+                                  double* table_dev, int32_t width, int64_t* export_dev, int32_t export_cap,
+                                  int32_t* export_n, char* err, size_t errlen);
+int nldsc_engine_run_device_finish(nldsc_engine* e, const int64_t* import_dev, int32_t import_n, char* err,
+                                   size_t errlen);
+
 /* Per-stage device timings (milliseconds, HIP events on the engine stream) of the last run:
  * [0] genotype count, [1] per-SNP statistics, [2] window replay + schedule (host time; overlaps [0]),
  * [3] band correlation kernel (all launches), [4] finalize, [5] total.

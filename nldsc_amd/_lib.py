@@ -31,7 +31,8 @@ EXPORTED = (
     "nldsc_engine_load_bed_device", "nldsc_engine_run", "nldsc_engine_timings",
     "nldsc_synth_bed_device", "nldsc_engine_path", "nldsc_plan_band", "nldsc_engine_load_bed_file_range",
     "nldsc_format_scores", "nldsc_engine_ksplit", "nldsc_engine_band_kernel", "nldsc_engine_band_round_items",
-    "nldsc_engine_band_tail_ksplit", "nldsc_engine_run_device",
+    "nldsc_engine_band_tail_ksplit", "nldsc_engine_run_device", "nldsc_engine_run_device_split",
+    "nldsc_engine_run_device_finish",
 )
 
 
@@ -106,6 +107,11 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         if hasattr(L, "nldsc_engine_run_device"):
             L.nldsc_engine_run_device.argtypes = [vp, ctypes.POINTER(Params), ctypes.c_int32, ctypes.c_int32, vp,
                                                   ctypes.c_int32] + c_err
+        if hasattr(L, "nldsc_engine_run_device_split"):
+            L.nldsc_engine_run_device_split.argtypes = [vp, ctypes.POINTER(Params), ctypes.c_int32, ctypes.c_int32, vp,
+                                                        ctypes.c_int32, vp, ctypes.c_int32,
+                                                        ctypes.POINTER(ctypes.c_int32)] + c_err
+            L.nldsc_engine_run_device_finish.argtypes = [vp, vp, ctypes.c_int32] + c_err
         # entry points newer builds add (an older build loaded for A/B timing may lack them)
         if path == LIB_PATH or hasattr(L, "nldsc_engine_load_bed_file_range"):
             L.nldsc_engine_load_bed_file_range.argtypes = [vp, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32,

@@ -153,6 +153,13 @@ struct nldsc_engine {
     DevBuf<int4> rep_items;
     DevBuf<int> rep_count;
     bool defer_rep = true;
+    // a split run between its two calls (nldsc_engine_run_device_split / _finish)
+    bool split_pending = false;
+    int32_t split_M = 0, split_N = 0, split_row_bytes = 0, split_width = 0;
+    std::pair<int32_t, int32_t> split_own{0, 0};
+    bool split_dom = true;
+    double* split_table = nullptr;
+    double split_ms1 = 0.0;  // the first call's host time
     bool ksplit_ok = true;    // $NLDSC_KSPLIT=0 disables the K-split
     bool replay_overlap = true;  // $NLDSC_REPLAY_OVERLAP=0 runs the rare-variant replay in line on the main stream
     int last_ksplit = 1;
@@ -538,8 +545,14 @@ namespace {
 
 // The hot path of one run.  Results go to the host arrays of `r`, or (table_dev != nullptr) stay in device memory
 // as the owned slice of the score table (nldsc_engine_run_device).
+// Split runs (nldsc_engine_run_device_split, export_n != nullptr): only the pairs whose lower SNP is owned are computed,
+// the per-SNP sums of every SNP of the slice accumulate, the right halo's [own_end, M) go out to export_dev and the run
+// stops before finalize; nldsc_engine_run_device_finish adds the left neighbour's export and finishes.
 int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32_t own_end, nldsc_ld_result* r,
-             double* table_dev, int32_t width, char* err, size_t errlen) {
+             double* table_dev, int32_t width, char* err, size_t errlen, long long* export_dev = nullptr,
+             int32_t export_cap = 0, int32_t* export_n = nullptr) {
+    const bool split = export_n != nullptr;
+    if (split) e->split_pending = false;
     if (!e || !p || (!r && !table_dev)) return set_err(err, errlen, NLDSC_E_ARG, "NULL argument");
     if (!e->bed.p) return set_err(err, errlen, NLDSC_E_ARG, "no BED image loaded");
     if (p->n_snp != e->n_snp || p->n_org != e->n_org)
@@ -554,6 +567,12 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     if (table_dev && (width <= 0 || width < own_end - own_begin))
         return set_err(err, errlen, NLDSC_E_ARG, "table width %d below the owned range's %d SNPs", width,
                        own_end - own_begin);
+    if (split && (!table_dev || (export_cap > 0 && !export_dev)))
+        return set_err(err, errlen, NLDSC_E_ARG, "split runs write a device table and need an export buffer");
+    if (split && own_begin == own_end) return set_err(err, errlen, NLDSC_E_ARG, "split runs need an owned SNP");
+    if (split && export_cap < p->n_snp - own_end)
+        return set_err(err, errlen, NLDSC_E_ARG, "export capacity %d below the %d halo SNPs", export_cap,
+                       p->n_snp - own_end);
     if (own_begin == own_end) {  // nothing owned: no kernel runs and no output is written (an empty GPU plan
         // would leave the left pointers unfilled); a device table is all NaN
         for (int k = 0; k < 6; ++k) e->ms[k] = 0.0;
@@ -699,6 +718,8 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     HIPCHK(hipEventRecord(e->ev[1], st));
     HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->oriented ? e->flip.p : nullptr, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->cst.p,
                                    e->sflags.p, e->maf.p, e->rstd.p, st));
+    // split runs: the pairs whose lower SNP is owned (flag bit 3), before the replay may touch the flags (ev_stats)
+    if (split) HIPCHK(nldsc::launch_pair_range(e->sflags.p, M, own_begin, own_end, st));
     // rare variants: the reference's fp32 residual replayed (its sums assume N < 2^23); the flags per block here,
     // the replay itself after the schedule (below)
     const bool replay = N < (1 << 23) && !(p->flags & NLDSC_FLAG_EXACT_RARE);
@@ -882,16 +903,19 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         }
         return tail_p > 1 ? e->gram.ensure((size_t)tail * tail_p * 8192) : hipSuccess;
     };
+    // per-SNP sums accumulate for the owned SNPs, or (split runs) for every SNP from own_begin on (the right halo's to
+    // be exported)
+    const int flush_hi = split ? M : own_end;
     auto launch_super = [&](int which) -> hipError_t {
         if (quad)
             return nldsc::launch_band_f4_q(dom, n_items2, geno, pitch_words, n_it, e->cst.p, e->items2.p,
                                            e->plan_rows.p, nblk, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
-                                           p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p,
+                                           p->ld_wind, (double)N, p->rsq_thr, own_begin, flush_hi, e->l2_acc.p,
                                            e->l2d_acc.p, e->ws_acc.p, true, blk_rep, e->blk_miss.p, which, st, quad_add,
                                            e->q_rounds && n_items2 >= 16 * e->n_cu ? e->n_cu : 0);
         return nldsc::launch_band_f4_t2(
             dom, n_items2, geno, pitch_words, n_it, e->cst.p, e->items2.p, e->plan_rows.p, nblk, e->pos.p, e->Lw.p,
-            e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
+            e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin, flush_hi, e->l2_acc.p, e->l2d_acc.p,
             e->ws_acc.p, true, blk_rep, routed ? e->blk_miss.p : nullptr, which, st);
     };
     // (column-block pair items: the compaction keeps an item while one of its blocks is unrouted, the kernel drops
@@ -902,13 +926,13 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         if (use_f4 && ksplit > 1)
             return nldsc::launch_band_f4_split(dom, ksplit, n_single, geno, pitch_words, n_it, e->cst.p, single,
                                                e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N,
-                                               p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p,
+                                               p->rsq_thr, own_begin, flush_hi, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p,
                                                blk_rep, e->gram.p, which, st);
         if (use_f4) {
             const bool dfr = defer && n_full > 0;
             hipError_t r = nldsc::launch_band_f4(dom, nc2 ? 2 : 1, n_full, geno, pitch_words, n_it, e->cst.p, single,
                                                  e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N,
-                                                 p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
+                                                 p->rsq_thr, own_begin, flush_hi, e->l2_acc.p, e->l2d_acc.p,
                                                  e->ws_acc.p, true, blk_rep, which, st, single_miss, round_items,
                                                  route_shift,
                                                  dfr ? e->rep_gram.p : nullptr, dfr ? e->rep_items.p : nullptr,
@@ -917,17 +941,17 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                 r = nldsc::launch_band_f4_deferred_epi(dom, n_full * (nc2 ? 2 : 1), e->cst.p, e->rep_items.p,
                                                        e->rep_count.p, e->rep_gram.p, e->pos.p, e->Lw.p, e->Rw.p,
                                                        e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin,
-                                                       own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, blk_rep, st);
+                                                       flush_hi, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, blk_rep, st);
             if (r != hipSuccess || n_full == n_single) return r;
             return nldsc::launch_band_f4_split(dom, tail_p, n_single - n_full, geno, pitch_words, n_it, e->cst.p,
                                                single + n_full, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
-                                               p->ld_wind, (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p,
+                                               p->ld_wind, (double)N, p->rsq_thr, own_begin, flush_hi, e->l2_acc.p,
                                                e->l2d_acc.p, e->ws_acc.p, blk_rep, e->gram.p, which, st, single_miss,
                                                route_shift);
         }
         return nldsc::launch_band_i8(dom, max_nc, n_single, geno, pitch_words, n_it, e->cst.p, single, e->pos.p,
                                      e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin,
-                                     own_end, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true, blk_rep, which, st);
+                                     flush_hi, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true, blk_rep, which, st);
     };
     const bool run_single = !use_t2 || routed;  // ($NLDSC_T2=2: every block pair in the 2 x 2 workgroups)
     if (n_items > 0 && (use_f4 || use_i8)) {
@@ -971,14 +995,11 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     if (n_items > 0 && !use_f4 && !use_i8) {
         HIPCHK(nldsc::launch_band(dom, 2, n_items, geno, pitch_words, n_it,
                                       e->lut.p, e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
-                                      (double)N, p->rsq_thr, own_begin, own_end, e->l2_acc.p, e->l2d_acc.p,
+                                      (double)N, p->rsq_thr, own_begin, flush_hi, e->l2_acc.p, e->l2d_acc.p,
                                       e->ws_acc.p, st));
     }
     e->last_path = path;
     HIPCHK(hipEventRecord(e->ev[4], st));
-    HIPCHK(nldsc::launch_finalize(e->Lw.p, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, own_begin, own_end, dom,
-                                  e->l2.p, e->l2d.p, e->ws3.p, st));
-    HIPCHK(hipEventRecord(e->ev[5], st));
     // matrix-core products the band kernels issued, counted on the GPU per work item as each kernel decides them
     // (missing-free blocks skip the m products, diagonal blocks the transposed ones, routed items run in the 2 x 2
     // kernel): sums[2]; sums[0..1] are the device-table run's pair counts
@@ -992,6 +1013,29 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                                              (use_t2 && quad_add ? 4 : 0),
                                          route_shift,
                                          e->sums.p + 2, st));
+    if (split) {  // the right halo's sums out; finalize waits for the left neighbour's (run_device_finish)
+        HIPCHK(nldsc::launch_export_acc(e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, own_end, M, export_dev, st));
+        HIPCHK(hipStreamSynchronize(st));
+        *export_n = M - own_end;
+        float f = 0;
+        HIPCHK(hipEventElapsedTime(&f, e->ev[0], e->ev[1])); e->ms[0] = f;
+        HIPCHK(hipEventElapsedTime(&f, e->ev[1], e->ev[2])); e->ms[1] = f;
+        e->ms[2] = std::chrono::duration<double, std::milli>(t_host1 - t_host0).count();
+        HIPCHK(hipEventElapsedTime(&f, e->ev[3], e->ev[4])); e->ms[3] = f;
+        e->split_ms1 = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+        e->split_pending = true;
+        e->split_M = M;
+        e->split_N = N;
+        e->split_dom = dom;
+        e->split_own = {own_begin, own_end};
+        e->split_row_bytes = row_bytes;
+        e->split_table = table_dev;
+        e->split_width = width;
+        return NLDSC_OK;
+    }
+    HIPCHK(nldsc::launch_finalize(e->Lw.p, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, own_begin, own_end, dom,
+                                  e->l2.p, e->l2d.p, e->ws3.p, st));
+    HIPCHK(hipEventRecord(e->ev[5], st));
     const int n_own = own_end - own_begin;
     double sw = 0, sd = 0;
     if (table_dev) {
@@ -1072,6 +1116,49 @@ int nldsc_engine_run_device(nldsc_engine* e, const nldsc_ld_params* p, int32_t o
                             double* table_dev, int32_t width, char* err, size_t errlen) {
     if (!table_dev) return set_err(err, errlen, NLDSC_E_ARG, "NULL table");
     return run_impl(e, p, own_begin, own_end, nullptr, table_dev, width, err, errlen);
+}
+
+int nldsc_engine_run_device_split(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32_t own_end,
+                                  double* table_dev, int32_t width, int64_t* export_dev, int32_t export_cap,
+                                  int32_t* export_n, char* err, size_t errlen) {
+    if (!table_dev || !export_n) return set_err(err, errlen, NLDSC_E_ARG, "NULL table or export count");
+    return run_impl(e, p, own_begin, own_end, nullptr, table_dev, width, err, errlen,
+                    reinterpret_cast<long long*>(export_dev), export_cap, export_n);
+}
+
+int nldsc_engine_run_device_finish(nldsc_engine* e, const int64_t* import_dev, int32_t import_n, char* err,
+                                   size_t errlen) {
+    if (!e) return set_err(err, errlen, NLDSC_E_ARG, "NULL engine");
+    if (!e->split_pending) return set_err(err, errlen, NLDSC_E_ARG, "no split run to finish");
+    const int32_t M = e->split_M, lo = e->split_own.first, hi = e->split_own.second;
+    if (import_n < 0 || import_n > hi - lo || (import_n > 0 && !import_dev))
+        return set_err(err, errlen, NLDSC_E_ARG, "import of %d SNPs into an owned range of %d", import_n, hi - lo);
+    e->split_pending = false;
+    HIPCHK(hipSetDevice(e->device));
+    hipStream_t st = e->stream;
+    const auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(nldsc::launch_import_acc(e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, lo, import_n,
+                                    reinterpret_cast<const long long*>(import_dev), st));
+    HIPCHK(hipEventRecord(e->ev[4], st));
+    HIPCHK(nldsc::launch_finalize(e->Lw.p, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, lo, hi, e->split_dom, e->l2.p,
+                                  e->l2d.p, e->ws3.p, st));
+    HIPCHK(hipEventRecord(e->ev[5], st));
+    HIPCHK(nldsc::launch_pack_table(e->l2.p, e->l2d.p, e->maf.p, e->rstd.p, e->ws3.p, M, lo, hi, e->split_width,
+                                    e->split_table, e->sums.p, st));
+    HIPCHK(hipMemcpyAsync(e->h_sums.p, e->sums.p, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const unsigned long long* s = reinterpret_cast<const unsigned long long*>(e->h_sums.p);
+    const double sw = (double)s[0], sd = e->split_dom ? (double)s[1] : 0.0, N = (double)e->split_N;
+    float f = 0;
+    HIPCHK(hipEventElapsedTime(&f, e->ev[4], e->ev[5])); e->ms[4] = f;
+    const auto t1 = std::chrono::steady_clock::now();
+    // (total: both calls' host time, without the exchange between them)
+    e->ms[5] = e->split_ms1 + std::chrono::duration<double, std::milli>(t1 - t0).count();
+    e->flop_issued = (double)s[2] * 2.0 * BLK * BLK * (double)e->split_row_bytes * 4.0;
+    e->pairs = sw;
+    e->flop_alg = 2.0 * N * (0.5 * sw + sd);
+    e->ops_alg_i8 = 2.0 * N * (2.0 * sw + 2.0 * sd);
+    return NLDSC_OK;
 }
 
 int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, double* flop_issued,

@@ -59,6 +59,13 @@ hipError_t launch_reference_residuals(const uint8_t* img, int row_bytes, int n_o
 // reference's / PLINK's sample order (keep masks of the last byte as the count kernel's tail_keep)
 hipError_t launch_row_missing(const uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes,
                               uint32_t keep_compat, uint32_t keep_strict, uint8_t* row_miss, hipStream_t st);
+// halo pairs once across ranks: clear flag bit 3 (the pair's lower SNP: computed here) outside [pair_lo, pair_hi);
+// the accumulator rows of SNPs [lo, hi) out to a [6][hi - lo] int64 block, and such a block added into SNPs [lo, lo + n)
+hipError_t launch_pair_range(uint8_t* sflags, int n_snp, int pair_lo, int pair_hi, hipStream_t st);
+hipError_t launch_export_acc(const double* l2_acc, const double* l2d_acc, const int* ws_acc, int n_snp, int lo, int hi,
+                             long long* out, hipStream_t st);
+hipError_t launch_import_acc(double* l2_acc, double* l2d_acc, int* ws_acc, int n_snp, int lo, int n, const long long* in,
+                             hipStream_t st);
 // per run (fp4): blk_miss[b] from row_miss (order 0 reference, 1 PLINK) — equal to the sflags-bit-2 predicate of the
 // band kernels, known without the count kernel
 hipError_t launch_block_missing_rows(const uint8_t* row_miss, int n_snp, int order, uint8_t* blk_miss,

@@ -211,6 +211,33 @@ __global__ void __launch_bounds__(256) row_missing_kernel(const uint8_t* __restr
     }
 }
 
+// Halo pairs computed once across ranks (nldsc_engine_run_device_split): only pairs whose lower SNP lies in
+// [pair_lo, pair_hi) — the rank's owned range — keep flag bit 3 (snp_stats_kernel sets it on every SNP); the pairs of
+// a rank's owned SNPs with the right halo are computed here for both SNPs, the halo SNPs' sums exported to their
+// owner (export_acc_kernel / import_acc_kernel: the fixed-point accumulators and counts add exactly).
+__global__ void pair_range_kernel(uint8_t* __restrict__ sflags, int n_snp, int pair_lo, int pair_hi) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n_snp && (j < pair_lo || j >= pair_hi)) sflags[j] &= (uint8_t)~8u;
+}
+// rows k of `out` (n = hi - lo columns): l2 / l2d fixed-point accumulators, WSA, WSD, WSDE, non-finite flags
+__global__ void export_acc_kernel(const double* __restrict__ l2_acc, const double* __restrict__ l2d_acc,
+                                  const int* __restrict__ ws_acc, int n_snp, int lo, int hi, long long* __restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x, g = lo + c, n = hi - lo;
+    if (g >= hi) return;
+    out[c] = reinterpret_cast<const long long*>(l2_acc)[g];
+    out[(size_t)n + c] = reinterpret_cast<const long long*>(l2d_acc)[g];
+    for (int k = 0; k < 4; ++k) out[(size_t)(2 + k) * n + c] = ws_acc[(size_t)k * n_snp + g];
+}
+__global__ void import_acc_kernel(double* __restrict__ l2_acc, double* __restrict__ l2d_acc, int* __restrict__ ws_acc,
+                                  int n_snp, int lo, int n, const long long* __restrict__ in) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x, g = lo + c;
+    if (c >= n || g >= n_snp) return;
+    reinterpret_cast<long long*>(l2_acc)[g] += in[c];
+    reinterpret_cast<long long*>(l2d_acc)[g] += in[(size_t)n + c];
+    for (int k = 0; k < 3; ++k) ws_acc[(size_t)k * n_snp + g] += (int)in[(size_t)(2 + k) * n + c];
+    ws_acc[3 * (size_t)n_snp + g] |= (int)in[5 * (size_t)n + c];
+}
+
 // per run: blk_miss[b] = block b holds a row with a missing call in this run's sample order (bit `order` of row_miss)
 __global__ void block_missing_rows_kernel(const uint8_t* __restrict__ row_miss, int n_snp, int order,
                                           uint8_t* __restrict__ blk_miss) {
@@ -391,7 +418,7 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const uint8_t* 
     K.isa = K.sa != 0.0 ? 1.0 / K.sa : 0.0;  // (NaN for an all-missing SNP: its windows stay poisoned)
     K.is = K.s != 0.0 ? 1.0 / K.s : 0.0;
     cst[j] = K;
-    sflags[j] = fl;
+    sflags[j] = fl | 8;  // bit 3: the pairs whose lower SNP this is are computed here (pair_range_kernel clears it)
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1112,9 +1139,11 @@ __device__ __forceinline__ void band_body(BandLds& sh, const int4 it, const uint
                 const bool pi = ci.fl & 1, rpi = (ci.fl & 2) != 0;
                 const bool inwin = fabs(cj.pos - ci.pos) <= ld_wind && ci.g != cj.g;
                 // j in N(i): SNP i's window scan (stream.h:142-155) covers j
-                const bool nij = inwin && ci.L >= 0 && cj.g >= ci.L && cj.g <= ci.R && pj;
+                // (flag bit 3 of the pair's lower SNP: this engine computes the pair, see pair_range_kernel)
+                const bool lo_ok = ((ci.g < cj.g ? ci.fl : cj.fl) & 8) != 0;
+                const bool nij = lo_ok && inwin && ci.L >= 0 && cj.g >= ci.L && cj.g <= ci.R && pj;
                 // i in N(j): only for off-diagonal blocks (a diagonal block holds both orders)
-                const bool nji = !diag && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
+                const bool nji = lo_ok && !diag && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
                 if (nij || nji) {
                     // the n_pad non-individual slots hold code 01 (missing): remove their products (non-zero only
                     // for the replayed rare variants, whose missing calls are not centred at 0)
@@ -1242,8 +1271,10 @@ __device__ __forceinline__ void pair_epilogue(const SnpSlot* info, const SnpCons
             const bool pi = ci.fl & 1, rpi = (ci.fl & 2) != 0;
             const bool inwin = fabs(cj.pos - ci.pos) <= ld_wind && ci.g != cj.g;
             // j in N(i): SNP i's window scan (stream.h:142-155) covers j; i in N(j) only off the diagonal
-            const bool nij = inwin && ci.L >= 0 && cj.g >= ci.L && cj.g <= ci.R && pj;
-            const bool nji = !diag && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
+            // the pair's lower SNP carries flag bit 3: this engine computes the pair (pair_range_kernel)
+            const bool lo_ok = ((ci.g < cj.g ? ci.fl : cj.fl) & 8) != 0;
+            const bool nij = lo_ok && inwin && ci.L >= 0 && cj.g >= ci.L && cj.g <= ci.R && pj;
+            const bool nji = lo_ok && !diag && inwin && compj && ci.g >= cj.L && ci.g <= cj.R && pi;
             SlotSum rv = {0.0, 0.0, 0};
             if (nij || nji) {
                 const SnpConst ki = cst[si];
@@ -2605,6 +2636,28 @@ hipError_t launch_row_missing(const uint8_t* img, const uint8_t* last, int n_snp
     if (n_snp <= 0) return hipSuccess;
     hipLaunchKernelGGL(row_missing_kernel, dim3((n_snp + 31) / 32), dim3(256), 0, st, img, last, n_snp, nb, row_bytes, keep_compat,
                        keep_strict, row_miss);
+    return hipGetLastError();
+}
+
+hipError_t launch_pair_range(uint8_t* sflags, int n_snp, int pair_lo, int pair_hi, hipStream_t st) {
+    if (n_snp <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pair_range_kernel, dim3((n_snp + 255) / 256), dim3(256), 0, st, sflags, n_snp, pair_lo, pair_hi);
+    return hipGetLastError();
+}
+
+hipError_t launch_export_acc(const double* l2_acc, const double* l2d_acc, const int* ws_acc, int n_snp, int lo, int hi,
+                             long long* out, hipStream_t st) {
+    if (hi <= lo) return hipSuccess;
+    hipLaunchKernelGGL(export_acc_kernel, dim3((hi - lo + 255) / 256), dim3(256), 0, st, l2_acc, l2d_acc, ws_acc, n_snp,
+                       lo, hi, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_import_acc(double* l2_acc, double* l2d_acc, int* ws_acc, int n_snp, int lo, int n, const long long* in,
+                             hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(import_acc_kernel, dim3((n + 255) / 256), dim3(256), 0, st, l2_acc, l2d_acc, ws_acc, n_snp, lo, n,
+                       in);
     return hipGetLastError();
 }
 

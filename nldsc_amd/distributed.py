@@ -206,6 +206,79 @@ def calculate_sharded_device(bed_path: str, n_snp: int, n_org: int, ld_wind: flo
     return gather_table(tab, spans, n_snp)
 
 
+def split_plan(positions: np.ndarray, ld_wind: float, world: int) -> list[tuple[int, int, int]] | None:
+    """Per rank (lo, hi, b) for split runs — the owned range [lo, hi) and the loaded slice [lo, b), its right halo
+    one window past hi — when each boundary pair can be computed once, by the rank owning its lower SNP: positions
+    non-negative and sorted (so the windows are the reference's neighbour sets) and every right halo inside the next
+    rank's owned range (it then receives the halo's sums).  None otherwise (the ranks then load a two-sided halo and
+    compute boundary pairs twice)."""
+    pos = np.asarray(positions, dtype=np.float64)
+    n = len(pos)
+    if world <= 1 or n == 0 or not (pos >= 0).all() or (np.diff(pos) < 0).any():
+        return None
+    ranges = shard_ranges(pos, ld_wind, world)
+    out = []
+    for g, (lo, hi) in enumerate(ranges):
+        if hi <= lo:
+            return None
+        b = halo_range(pos, ld_wind, (lo, hi))[1]
+        if g + 1 < world and b > ranges[g + 1][1]:
+            return None
+        out.append((lo, hi, b))
+    return out
+
+
+def exchange_halo(export, n_send: int, imported, n_recv: int):
+    """Send this rank's exported halo block ([6][n_send] int64) to the next rank and receive the previous rank's
+    ([6][n_recv]) — point to point (RCCL over xGMI with device tensors; gloo with CPU tensors: a device export is
+    staged through the host)."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    send, recv = export[: 6 * n_send], imported[: 6 * n_recv]
+    host = dist.get_backend() == "gloo"
+    if host:
+        send, recv_h = send.cpu(), torch.empty(recv.shape, dtype=recv.dtype)
+    ops = []
+    if rank + 1 < world and n_send > 0:
+        ops.append(dist.P2POp(dist.isend, send, rank + 1))
+    if rank > 0 and n_recv > 0:
+        ops.append(dist.P2POp(dist.irecv, recv_h if host else recv, rank - 1))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    if host and rank > 0 and n_recv > 0:
+        recv.copy_(recv_h)
+
+
+def calculate_sharded_split(bed_path: str, n_snp: int, n_org: int, ld_wind: float, maf: float, std_thr: float,
+                            rsq_thr: float, positions: np.ndarray, plan: list[tuple[int, int, int]], *, flags: int = 0,
+                            device: int = 0) -> dict | None:
+    """The sharded CLI run with each boundary pair computed once (`split_plan`): this rank loads [lo, b) of the .bed,
+    runs the first half of a split run, sends its right halo's sums to the next rank, adds the previous rank's, and
+    finishes; the score-table blocks are then gathered as in calculate_sharded_device."""
+    import torch
+    import torch.distributed as dist
+    from .engine import Engine
+    world, rank = dist.get_world_size(), dist.get_rank()
+    pos = np.asarray(positions, dtype=np.float64)
+    lo, hi, b = plan[rank]
+    n_recv = plan[rank - 1][2] - plan[rank - 1][1] if rank > 0 else 0
+    dev = torch.device(f"cuda:{device}")
+    coll = dev if dist.get_backend() != "gloo" else None
+    spans = gather_spans((lo, hi), device=coll)
+    tab = torch.full((len(RESULT_KEYS), table_width(spans)), float("nan"), dtype=torch.float64, device=dev)
+    export = torch.empty(6 * max(b - hi, 1), dtype=torch.int64, device=dev)
+    imported = torch.empty(6 * max(n_recv, 1), dtype=torch.int64, device=dev)
+    with Engine(device) as e:
+        e.load_bed_file_range(bed_path, n_snp, n_org, lo, b)
+        n_send = e.run_device_split(ld_wind, maf, std_thr, rsq_thr, pos[lo:b], tab, export, own=(0, hi - lo),
+                                    flags=flags)
+        exchange_halo(export, n_send, imported, n_recv)
+        e.run_device_finish(imported, n_recv)
+    return gather_table(tab if coll is not None else tab.cpu(), spans, n_snp)
+
+
 def engine_runner(bed_path: str, n_snp: int, n_org: int, ld_wind: float, maf: float, std_thr: float,
                   rsq_thr: float, positions: np.ndarray, *, flags: int = 0, device: int = 0):
     """`load_and_run` for calculate_sharded backed by this rank's GPU engine: the rank reads only its

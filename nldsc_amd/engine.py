@@ -107,6 +107,33 @@ class Engine:
                                                       len(err)), err)
         return table
 
+    def run_device_split(self, ld_wind, maf, std_thr, rsq_thr, positions, table, export, *, own, flags=0) -> int:
+        """First half of a split run (C ABI nldsc_engine_run_device_split): the loaded slice is the owned SNPs
+        [own[0], own[1]) and the right halo after them; computes the pairs whose lower SNP is owned and writes the
+        halo's accumulator rows into `export` (contiguous int64 device tensor of >= 6 * halo elements).  Returns the
+        number of halo SNPs exported; finish with run_device_finish."""
+        n = self.n_snp
+        if table.dim() != 2 or table.shape[0] != 7 or not table.is_cuda or str(table.dtype) != "torch.float64" \
+                or not table.is_contiguous():
+            raise ValueError("table must be a contiguous float64 CUDA tensor of shape (7, width)")
+        if not export.is_cuda or str(export.dtype) != "torch.int64" or not export.is_contiguous():
+            raise ValueError("export must be a contiguous int64 CUDA tensor")
+        p, _keep = _lib.make_params(n, self.n_org, ld_wind, maf, std_thr, rsq_thr, positions, flags=flags)
+        cnt = ctypes.c_int32(0)
+        err = _lib.errbuf()
+        _lib.check(self._L.nldsc_engine_run_device_split(
+            self._h, ctypes.byref(p), int(own[0]), int(own[1]), ctypes.c_void_p(table.data_ptr()),
+            int(table.shape[1]), ctypes.c_void_p(export.data_ptr()), int(export.numel() // 6), ctypes.byref(cnt),
+            err, len(err)), err)
+        return int(cnt.value)
+
+    def run_device_finish(self, imported=None, n: int = 0):
+        """Second half: add the left neighbour's exported block (int64 device tensor laid out [6][n]) into the
+        first n owned SNPs, finalize and write the table given to run_device_split."""
+        err = _lib.errbuf()
+        ptr = ctypes.c_void_p(imported.data_ptr()) if (imported is not None and n > 0) else None
+        _lib.check(self._L.nldsc_engine_run_device_finish(self._h, ptr, int(n), err, len(err)), err)
+
     def timings(self) -> dict:
         ms = (ctypes.c_double * 6)()
         flop, issued, pairs = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()

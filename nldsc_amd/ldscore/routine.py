@@ -119,6 +119,12 @@ def _backend() -> str:
     return os.environ.get("NLDSC_DIST_BACKEND", "nccl")
 
 
+def _split_halo() -> bool:
+    """Boundary pairs computed once across ranks ($NLDSC_SPLIT_HALO=0: each rank loads a two-sided halo and computes
+    them itself)."""
+    return os.environ.get("NLDSC_SPLIT_HALO", "1") != "0"
+
+
 def _local_device() -> int:
     import torch
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -145,7 +151,11 @@ def _calculate_sharded(dist, params):
     from .. import distributed as D
     dev = _local_device()
     pos = np.asarray(params.positions, dtype=np.float64)
-    if _backend() == "nccl":  # the owned slices stay in device memory and are gathered over RCCL
+    plan = D.split_plan(pos, params.ld_wind, dist.get_world_size()) if _split_halo() else None
+    if plan is not None:  # boundary pairs once: halo sums sent to the next rank (point to point)
+        full = D.calculate_sharded_split(params.bedfile, params.n_snp, params.n_org, params.ld_wind, params.maf,
+                                         params.std_thr, params.rsq_thr, pos, plan, flags=params.flags, device=dev)
+    elif _backend() == "nccl":  # the owned slices stay in device memory and are gathered over RCCL
         full = D.calculate_sharded_device(params.bedfile, params.n_snp, params.n_org, params.ld_wind, params.maf,
                                           params.std_thr, params.rsq_thr, pos, flags=params.flags, device=dev)
     else:  # gloo: host result arrays, CPU collectives

@@ -119,3 +119,54 @@ def test_halo_slices_reproduce_full_run(world):
         lo, hi = own
         for k in full:
             np.testing.assert_array_equal(part[k][lo - a:hi - a], full[k][lo:hi], err_msg=f"{own} {k}")
+
+
+def _halo_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch
+    import torch.distributed as dist
+    from nldsc_amd import distributed as D
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sizes = [5, 0, 7, 3][:world]  # halo SNPs each rank sends to the next (the last rank sends none)
+        n_send = sizes[rank] if rank + 1 < world else 0
+        n_recv = sizes[rank - 1] if rank > 0 else 0
+        export = torch.arange(6 * max(n_send, 1), dtype=torch.int64) + 1000 * rank
+        imported = torch.full((6 * max(n_recv, 1),), -1, dtype=torch.int64)
+        D.exchange_halo(export, n_send, imported, n_recv)
+        exp = (torch.arange(6 * n_recv, dtype=torch.int64) + 1000 * (rank - 1)) if n_recv else None
+        ok = exp is None or torch.equal(imported[: 6 * n_recv], exp)
+        with open(os.path.join(outdir, f"ok{rank}"), "w") as fh:
+            fh.write("1" if ok else "0")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_halo_exchange_point_to_point(world):
+    """exchange_halo: each rank's exported block reaches the next rank (gloo; an empty send is skipped on both
+    sides)."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_halo_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        assert all(open(os.path.join(d, f"ok{r}")).read() == "1" for r in range(world))
+
+
+def test_split_plan_halo_within_next_owned_range():
+    """split_plan: owned ranges cover every SNP once, each slice is the owned range plus one window on the right,
+    inside the next rank's owned range; unsorted or negative positions (and one-rank runs) give no plan."""
+    from nldsc_amd import distributed as D
+    rng = np.random.default_rng(1)
+    pos = np.cumsum(rng.exponential(0.01, 20_000))
+    for world in (2, 3, 8):
+        plan = D.split_plan(pos, 1.0, world)
+        assert plan is not None and plan[0][0] == 0 and plan[-1][1] == len(pos) == plan[-1][2]
+        for g, (lo, hi, b) in enumerate(plan):
+            assert lo < hi <= b
+            assert b == np.searchsorted(pos, pos[hi - 1] + 1.0 + 1e-9, side="right") or b == hi
+            if g + 1 < world:
+                assert plan[g + 1][0] == hi and b <= plan[g + 1][1]
+    assert D.split_plan(pos, 1.0, 1) is None
+    assert D.split_plan(pos[::-1], 1.0, 2) is None
+    bad = pos.copy(); bad[10] = -1.0
+    assert D.split_plan(bad, 1.0, 2) is None
+    assert D.split_plan(pos, 150.0, 8) is None  # windows longer than a rank's range

@@ -127,3 +127,58 @@ def test_bench_force_dist_rccl_one_rank():
     d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert d["n_gpus"] == 1 and d["value"] > 0 and "RCCL" in d["config"]["parallelism"], d
     assert d["stages_ms"]["gather_ms"] >= 0 and d["per_rank"][0]["owned_snps"] == 6000
+
+
+SPLIT_SCRIPT = r'''
+import json, os, sys
+sys.path.insert(0, {repo!r})
+import numpy as np
+import torch
+import torch.distributed as dist
+torch.cuda.set_device(0)
+dist.init_process_group("gloo")
+from nldsc_amd import distributed as D
+from nldsc_amd.ldscore import _ldscore as lds
+from nldsc_amd.ldscore.common import PLINKFile
+bed, bim, fam = PLINKFile.parse({bfile!r})
+pos = np.asarray(bim.cm, dtype=np.float64)
+M, N, w = bim.n_snp, fam.n_org, 1.0
+args = (bed.data, M, N, w, 1e-4, 1e-5, 1.0 / M)
+plan = D.split_plan(pos, w, dist.get_world_size())
+assert plan is not None
+split = D.calculate_sharded_split(*args, pos, plan, device=0)
+dup = D.calculate_sharded(D.engine_runner(*args, pos, device=0), pos, w, M)
+if dist.get_rank() == 0:
+    p = lds.LDScoreParams(bed.data, n_snp=M, n_org=N, ld_wind=w, maf=1e-4, std_thr=1e-5, rsq_thr=1.0 / M,
+                          positions=pos.tolist())
+    one = lds.calculate(p)
+    out = dict(plan=plan)
+    for k in D.RESULT_KEYS:
+        a = np.asarray(split[k], dtype=np.float64)
+        out[k] = [bool(np.array_equal(a, np.asarray(dup[k], dtype=np.float64), equal_nan=True)),
+                  bool(np.array_equal(a, np.asarray(getattr(one, k), dtype=np.float64), equal_nan=True))]
+    print(json.dumps(out), flush=True)
+dist.destroy_process_group()
+'''
+
+
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_split_halo_bitwise_duplicate_halo_and_one_process(tmp_path, ranks):
+    """Boundary pairs computed once (split runs: each rank loads its owned range + right halo, sends the halo's
+    fixed-point sums to the next rank, point to point) give bitwise the two-sided-halo results and the one-process
+    `calculate` (gloo ranks sharing the one GPU; N = 20 011, 6 000 SNPs over 9 cM, 1 % missing)."""
+    import json
+    from nldsc_amd import synth
+    synth.write_plink(str(tmp_path / "chr1"), synth.SynthSpec(n_org=20_011, n_snp=6000, length_cm=9.0, seed=17,
+                                                                missing=0.01), chrom=1)
+    script = tmp_path / "split.py"
+    script.write_text(SPLIT_SCRIPT.format(repo=REPO, bfile=str(tmp_path / "chr1")))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), str(script)]
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert len(d.pop("plan")) == ranks
+    assert all(a and b for a, b in d.values()), d
