@@ -224,9 +224,10 @@ def main():
     ap.add_argument("--no-file", action="store_true",
                     help="skip the wall clock from a PLINK file (rank 0, N = 1: the synthetic .bed written to "
                          "$TMPDIR, then _ldscore.calculate timed from the file)")
-    ap.add_argument("--duplicate-halo", action="store_true",
-                    help="N > 1: load a two-sided halo and compute the boundary pairs on both ranks (no point-to-point "
-                         "exchange) instead of once, by the rank owning the lower SNP")
+    ap.add_argument("--split-halo", action="store_true",
+                    help="N > 1: compute each boundary pair once, on the rank owning the lower SNP, and send the right "
+                         "halo's sums to the next rank point to point, instead of a two-sided halo on both ranks "
+                         "(measured equal at C3/8, so not the default)")
     ap.add_argument("--force-dist", action="store_true",
                     help="create the process group and run the sharded path (owned range, device table, collective "
                          "gather) even with one rank: the RCCL code of an N-GPU run rehearsed on one GPU")
@@ -295,10 +296,10 @@ def main():
         # owned SNP range plus one window of halo rows resident and computes the owned SNPs
         from nldsc_amd.distributed import (RESULT_KEYS, exchange_halo, gather_spans, gather_table, halo_range,
                                            shard_ranges, split_plan, table_width)
-        # boundary pairs once (default): rank g loads its owned range + the right halo, computes the pairs whose lower
-        # SNP it owns and sends the halo's sums to rank g + 1 (one point-to-point block per step); else a two-sided
-        # halo with the boundary pairs computed by both neighbours
-        plan = None if args.duplicate_halo else split_plan(pos, args.window_cm, s_world)
+        # --split-halo: rank g loads its owned range + the right halo, computes the pairs whose lower SNP it owns and
+        # sends the halo's sums to rank g + 1 (one point-to-point block per step); by default a two-sided halo with
+        # the boundary pairs computed by both neighbours (the same band time at C3/8, no exchange)
+        plan = split_plan(pos, args.window_cm, s_world) if args.split_halo else None
         if plan is not None:
             lo, hi, b = plan[s_rank]
             a = lo

@@ -126,8 +126,9 @@ int nldsc_engine_run_device(nldsc_engine* e, const nldsc_ld_params* p, int32_t o
  * 6 * export_cap int64 (row-major [6][export_n], export_n = n_snp - own_end <= export_cap), synchronised on return.
  * The caller sends that block to the rank owning those SNPs (whose slice starts at them) and passes the block
  * received from the left neighbour to _finish, which adds it to the first import_n owned SNPs (import_n <=
- * own_end - own_begin; 0 for the first rank), finalizes and writes `table_dev` as nldsc_engine_run_device does.  The
- * result is bitwise that of nldsc_engine_run_device with the left halo loaded (the sums are integers). */
+ * own_end - own_begin; 0 for the first rank), finalizes and writes `table_dev` as nldsc_engine_run_device does.  Counts,
+ * MAF and residual std equal those of nldsc_engine_run_device with the left halo loaded; L2 / L2D to the last bits
+ * (the exchanged sums are exact integers; each work item's fp64 partial sums follow the slice's block grid). */
 int nldsc_engine_run_device_split(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32_t own_end,
                                   double* table_dev, int32_t width, int64_t* export_dev, int32_t export_cap,
                                   int32_t* export_n, char* err, size_t errlen);

@@ -120,9 +120,9 @@ def _backend() -> str:
 
 
 def _split_halo() -> bool:
-    """Boundary pairs computed once across ranks ($NLDSC_SPLIT_HALO=0: each rank loads a two-sided halo and computes
-    them itself)."""
-    return os.environ.get("NLDSC_SPLIT_HALO", "1") != "0"
+    """$NLDSC_SPLIT_HALO=1: boundary pairs computed once across ranks (right halo's sums sent point to point); by
+    default each rank loads a two-sided halo and computes them itself (the same band time at C3/8, no exchange)."""
+    return os.environ.get("NLDSC_SPLIT_HALO", "0") != "0"
 
 
 def _local_device() -> int:

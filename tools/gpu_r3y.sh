@@ -6,10 +6,10 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_torchrun.py -m gpu -x -v --
   || { echo "tests failed"; tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 for k in 1 2; do
-timeout -k 10 200 python bench.py --no-cpu --no-file --steps 20 --rehearse 0/8 > $O/reh_split_$k.json 2> $O/reh.err || { tail $O/reh.err; exit 1; }
-timeout -k 10 200 python bench.py --no-cpu --no-file --steps 20 --rehearse 0/8 --duplicate-halo > $O/reh_dup_$k.json 2> $O/reh.err || { tail $O/reh.err; exit 1; }
-timeout -k 10 200 python bench.py --no-cpu --no-file --steps 20 --rehearse 3/8 > $O/reh3_split_$k.json 2> $O/reh.err || { tail $O/reh.err; exit 1; }
-timeout -k 10 200 python bench.py --no-cpu --no-file --steps 20 --rehearse 3/8 --duplicate-halo > $O/reh3_dup_$k.json 2> $O/reh.err || { tail $O/reh.err; exit 1; }
+timeout -k 10 200 python bench.py --no-cpu --no-file --steps 20 --rehearse 0/8 > $O/reh_dup_$k.json 2> $O/reh.err || { tail $O/reh.err; exit 1; }
+timeout -k 10 200 python bench.py --no-cpu --no-file --steps 20 --rehearse 0/8 --split-halo > $O/reh_split_$k.json 2> $O/reh.err || { tail $O/reh.err; exit 1; }
+timeout -k 10 200 python bench.py --no-cpu --no-file --steps 20 --rehearse 3/8 > $O/reh3_dup_$k.json 2> $O/reh.err || { tail $O/reh.err; exit 1; }
+timeout -k 10 200 python bench.py --no-cpu --no-file --steps 20 --rehearse 3/8 --split-halo > $O/reh3_split_$k.json 2> $O/reh.err || { tail $O/reh.err; exit 1; }
 done
 python3 - <<'PY'
 import json, glob
