@@ -161,6 +161,7 @@ struct nldsc_engine {
     double* split_table = nullptr;
     double split_ms1 = 0.0;  // the first call's host time
     bool ksplit_ok = true;    // $NLDSC_KSPLIT=0 disables the K-split
+    int ksplit_force = 0;     // ($NLDSC_KSPLIT_P=P, study) the K-split factor of every K-split launch
     bool replay_overlap = true;  // $NLDSC_REPLAY_OVERLAP=0 runs the rare-variant replay in line on the main stream
     int last_ksplit = 1;
     int last_round_items = 0;
@@ -330,6 +331,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_GPU_PLAN")) e->gpu_plan = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_ORIENT")) e->orient = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_KSPLIT")) e->ksplit_ok = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_KSPLIT_P")) e->ksplit_force = std::max(0, std::min(8, std::atoi(v)));
     if (const char* v = std::getenv("NLDSC_REPLAY_OVERLAP")) e->replay_overlap = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_T2")) e->t2_mode = std::max(0, std::min(3, std::atoi(v)));
     if (const char* v = std::getenv("NLDSC_BAND_ROUNDS")) e->band_rounds = std::atoi(v) != 0;
@@ -672,6 +674,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                     best = cost(P);
                     ksplit = P;
                 }
+            if (e->ksplit_force > 0 && 2 * e->ksplit_force <= n_it) ksplit = e->ksplit_force;
         }
         return ksplit;
     };
