@@ -162,6 +162,7 @@ struct nldsc_engine {
     double split_ms1 = 0.0;  // the first call's host time
     bool ksplit_ok = true;    // $NLDSC_KSPLIT=0 disables the K-split
     int ksplit_force = 0;     // ($NLDSC_KSPLIT_P=P, study) the K-split factor of every K-split launch
+    int round_min = 4;        // ($NLDSC_ROUND_MIN) round launches from this many rounds of single-block items on
     bool replay_overlap = true;  // $NLDSC_REPLAY_OVERLAP=0 runs the rare-variant replay in line on the main stream
     int last_ksplit = 1;
     int last_round_items = 0;
@@ -331,6 +332,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_GPU_PLAN")) e->gpu_plan = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_ORIENT")) e->orient = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_KSPLIT")) e->ksplit_ok = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_ROUND_MIN")) e->round_min = std::max(1, std::atoi(v));
     if (const char* v = std::getenv("NLDSC_KSPLIT_P")) e->ksplit_force = std::max(0, std::min(8, std::atoi(v)));
     if (const char* v = std::getenv("NLDSC_REPLAY_OVERLAP")) e->replay_overlap = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_T2")) e->t2_mode = std::max(0, std::min(3, std::atoi(v)));
@@ -749,6 +751,10 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         const int* meta = reinterpret_cast<const int*>(e->h_meta.p);
         n_items = meta[1];
         ksplit = choose_ksplit(n_items);
+        // bands of at least round_min rounds go in round launches (the last, partial round K-split), not K-split whole
+        if (e->round_min < 4 && e->band_rounds && use_f4 && n_it >= 1024 && n_it <= nldsc::F4_SEG_CHUNKS &&
+            n_items >= e->round_min * 8 * e->n_cu)
+            ksplit = 1;
         use_t2 = t2_cand && ksplit == 1 && n_items > 0;
         // The work lists go out on the plan stream, beside the count kernel: the items, the super-items, the routing
         // (blk_miss, from the load-time row_miss: it needs no count) and, with super-item routing, the list of the
@@ -890,7 +896,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     const bool defer = replay && e->defer_rep && use_f4 && ksplit == 1 && n_it <= nldsc::F4_SEG_CHUNKS;
     auto size_single = [&]() -> hipError_t {
         round_items = use_f4 && ksplit == 1 && e->band_rounds && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 1024 &&
-                      n_single >= 4 * slots ? slots : 0;
+                      n_single >= e->round_min * slots ? slots : 0;
         const int tail = round_items > 0 ? n_single % round_items : 0;
         tail_p = tail > 0 ? choose_ksplit(tail) : 1;
         n_full = tail_p > 1 ? n_single - tail : n_single;
