@@ -162,7 +162,7 @@ struct nldsc_engine {
     double split_ms1 = 0.0;  // the first call's host time
     bool ksplit_ok = true;    // $NLDSC_KSPLIT=0 disables the K-split
     int ksplit_force = 0;     // ($NLDSC_KSPLIT_P=P, study) the K-split factor of every K-split launch
-    int round_min = 4;        // ($NLDSC_ROUND_MIN) round launches from this many rounds of single-block items on
+    int round_min = 1;        // ($NLDSC_ROUND_MIN) round launches from this many rounds of single-block items on
     bool replay_overlap = true;  // $NLDSC_REPLAY_OVERLAP=0 runs the rare-variant replay in line on the main stream
     int last_ksplit = 1;
     int last_round_items = 0;
@@ -751,8 +751,10 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         const int* meta = reinterpret_cast<const int*>(e->h_meta.p);
         n_items = meta[1];
         ksplit = choose_ksplit(n_items);
-        // bands of at least round_min rounds go in round launches (the last, partial round K-split), not K-split whole
-        if (e->round_min < 4 && e->band_rounds && use_f4 && n_it >= 1024 && n_it <= nldsc::F4_SEG_CHUNKS &&
+        // long rows: bands of at least round_min rounds of wave slots go in round launches (the last, partial round
+        // K-split), not K-split whole — a 1/8 shard of C3 (1.6 rounds) band 2.70-2.76 -> 2.61-2.64 ms, a 1/4 shard
+        // (3.2 rounds) 5.21-5.26 -> 4.87-4.89 ms (profiles/r03_ab_round_min.txt; was from 4 rounds on)
+        if (e->band_rounds && use_f4 && n_it >= 1024 && n_it <= nldsc::F4_SEG_CHUNKS &&
             n_items >= e->round_min * 8 * e->n_cu)
             ksplit = 1;
         use_t2 = t2_cand && ksplit == 1 && n_items > 0;

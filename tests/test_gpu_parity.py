@@ -955,7 +955,7 @@ ROUND_CASES = {
 @pytest.mark.parametrize("case", sorted(ROUND_CASES))
 def test_band_round_launches_bitwise_one_launch(engine, case):
     """The single-block fp4 band in launches of one round of the wave slots each (the default for long rows,
-    N >= 2^17, when the band has at least four rounds of items), with the partial last round K-split when the cost
+    N >= 2^17, when the band has at least one round of items), with the partial last round K-split when the cost
     model prefers it, gives bitwise the results of one launch of all items ($NLDSC_BAND_ROUNDS=0): the per-SNP sums
     are order-independent fixed point, the K-split partial Gram tiles are exact integers, and every item runs once.
     12 000 SNPs at 800 per cM, 1 % missing; a few SNPs against the exact truth.  The additive-only case runs
@@ -980,7 +980,7 @@ def _round_launch_case(case):
             t = e.timings()
             assert (t["band_round_items"] > 0) == rounds, t
             if rounds:
-                assert t["band_items"] >= 4 * t["band_round_items"], t
+                assert t["band_items"] >= t["band_round_items"], t
                 assert t["band_tail_ksplit"] > 1 or not tail, t
             return r
     got = fresh(True)
