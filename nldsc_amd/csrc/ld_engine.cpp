@@ -886,7 +886,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // of a launch start together and, all of equal length, stay at nearby K offsets, so the waves on one XCD that
     // share a strip (the plan's 16 x 16 tiles) read it from that XCD's L2.  In one launch of all items the waves
     // drift apart and most strip bytes come from beyond L2 again (C3: 68 -> 14 GB per band, the clock 1.90 -> 2.02
-    // GHz; band -2 to -4 % after the launch tails).  Only for bands of several rounds, and only for long rows: the
+    // GHz; band -2 to -4 % after the launch tails).  From one round of items on ($NLDSC_ROUND_MIN), only for long rows: the
     // waves of a round also reach their epilogues together, which then no longer overlap another wave's products —
     // at N = 50 000 (strips of 0.4 MB, L2-resident anyway; epilogue ~1/3 of an item) round launches made the band
     // 2.8 -> 5.1 ms.  The last, partial round leaves wave slots idle for a whole item length (C3: 1 458 items in
