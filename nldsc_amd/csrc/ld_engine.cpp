@@ -754,10 +754,15 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         // long rows: bands of at least round_min rounds of wave slots go in round launches (the last, partial round
         // K-split), not K-split whole — a 1/8 shard of C3 (1.6 rounds) band 2.70-2.76 -> 2.61-2.64 ms, a 1/4 shard
         // (3.2 rounds) 5.21-5.26 -> 4.87-4.89 ms (profiles/r03_ab_round_min.txt; was from 4 rounds on)
+        // — in the single-block kernel, as the K-split it replaces: a shard's few super-items leave most CUs of the
+        // 4 x 4 kernel idle (a missing-free 1/8 shard of C3: 2.88 ms with it, 1.93-1.99 K-split whole)
+        bool rounds_forced = false;
         if (e->band_rounds && use_f4 && n_it >= 1024 && n_it <= nldsc::F4_SEG_CHUNKS &&
-            n_items >= e->round_min * 8 * e->n_cu)
+            n_items >= e->round_min * 8 * e->n_cu) {
+            rounds_forced = ksplit > 1;
             ksplit = 1;
-        use_t2 = t2_cand && ksplit == 1 && n_items > 0;
+        }
+        use_t2 = t2_cand && ksplit == 1 && n_items > 0 && !rounds_forced;
         // The work lists go out on the plan stream, beside the count kernel: the items, the super-items, the routing
         // (blk_miss, from the load-time row_miss: it needs no count) and, with super-item routing, the list of the
         // items the single-block kernel keeps, compacted in order, so its launches (round launches, the K-split tail)
