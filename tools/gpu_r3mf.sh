@@ -1,7 +1,6 @@
 #!/bin/bash
-# round 3 (next-round study): a variant keeping shards forced into round launches in the single-block kernel was
-# not validated on the GPU in time and is not in the tree; this measures the committed default — parity tests of the
-# band launch paths, then 1/8 shards with and without missing calls and a 1/4 shard (round launches from 1 round, default, vs 4)
+# round 3: shards forced into round launches kept in the single-block kernel — parity tests of the band launch
+# paths, then 1/8 shards with and without missing calls and a 1/4 shard (round launches from 1 round, default, vs 4)
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/r3mf; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_torchrun.py -m gpu -x -q --timeout 300 --timeout-method thread -k "round or ksplit or quad or t2 or split or deferred or rccl or torchrun" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
