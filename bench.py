@@ -105,6 +105,32 @@ def pmc_traffic(kernel_key: str, n_org: int, n_snp: int, missing: float):
                   if stale else "no PMC summary for this workload")
 
 
+def table_digest(out: dict) -> dict:
+    """A fingerprint of the gathered score table (outside the timed region): sha256 of the three window-count
+    columns (exact integers) and the fp64 sums of L2 / L2D, so runs at different rank counts can be compared."""
+    import hashlib
+    h = hashlib.sha256()
+    for k in ("l2_ws", "l2d_ws", "l2d_wse"):
+        if k in out:
+            h.update(np.ascontiguousarray(np.asarray(out[k]), dtype=np.int32).tobytes())
+    d = {"counts_sha16": h.hexdigest()[:16], "n_snp": int(len(out["l2_ws"]))}
+    for k in ("l2", "l2d"):
+        if k in out:
+            d[k + "_sum"] = float(np.nansum(np.asarray(out[k], dtype=np.float64)))
+    return d
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -132,7 +158,7 @@ def cpu_baseline(bed_host: bytes, n_snp, n_org, w, maf, std_thr, rsq, pos, targe
         r0, t0 = timed(k)
     ws = r0["l2_ws"][:k]
     pairs = float(ws[ws > 0].sum())
-    return dict(value=pairs / t0, unit="SNP-pairs/s", cores=threads, kind="port",
+    return dict(value=pairs / t0, unit="SNP-pairs/s", cores=threads, kind="port", cpu_model=cpu_model(),
                 sample=f"first {k} SNPs of the same chromosome (full sliding window from SNP 0), "
                        f"{pairs:.0f} pairs in {t0:.2f} s, C port of the reference path (oracle/ldscore_oracle.c: "
                        f"fp32 sdot + per-pair vector copies, OpenMP over neighbours)")
@@ -408,12 +434,14 @@ def main():
                                        "once per unordered pair, dominance cross term per ordered pair)"}
         roof["frac"] = roof["achieved"] / peak
         if path != "f32":
-            ops = tims[-1]["ops_alg_i8"]
-            roof.update(ops_8_product_per_launch=ops, achieved_8_product_basis=ops / t_band / 1e12,
-                        frac_8_product_basis=ops / t_band / 1e12 / peak,
-                        ops_8_product_definition="2N(4*(1/2)sumWSA + 2*sumWSD): the exact formulation's 8 integer "
-                                                 "Gram entries per pair (vv, vm, mv, mm additive; vh, mh, hv, hm "
-                                                 "dominance), skipped products of missing-free blocks included")
+            # the exact formulation's floor: 8 integer Gram entries per unordered pair for add+dom (vv, vm, mv, mm;
+            # vh, mh, hv, hm) against the 3 dots FLOP_alg counts (one additive, two dominance cross terms) = 8/3; 4
+            # per 1 additive-only.  Above the floor: products of 32x32 blocks that fall outside the windows
+            roof.update(issued_over_alg=tims[-1]["flop_issued"] / flop if flop > 0 else None,
+                        issued_over_alg_floor=(4.0 if args.additive_only else 8.0 / 3.0),
+                        issued_over_alg_note="a ratio of FLOP counts, not a fraction of peak: the MFMA products the "
+                                             "band kernels issued (counted per item on the GPU, skipped products "
+                                             "of missing-free blocks excluded) over FLOP_alg")
         traffic, traffic_src = pmc_traffic(
             ("band_f4_t2_kernel", "band_f4_q_kernel", "band_f4_kernel", "band_f4_part_kernel",
              "band_f4_epi_kernel")  # (the super-item kernel + the single-block rest + the K-split tail)
@@ -428,9 +456,7 @@ def main():
                                  if tims[-1].get("band_round_items") else
                                  "one band launch per run, timed with HIP events on the engine stream"),
                     issued_per_launch=tims[-1]["flop_issued"], work_items=tims[-1]["band_items"],
-                    mfma_pipe_frac=tims[-1]["flop_issued"] / t_band / 1e12 / peak,
-                    fp32_equivalent_tflops=flop / t_band / 1e12,
-                    fp32_equivalent_frac_of_fp32_peak=flop / t_band / 1e12 / FP32_MFMA_PEAK_TFLOPS)
+                    mfma_pipe_frac=tims[-1]["flop_issued"] / t_band / 1e12 / peak)
         stages = {k: round(float(np.mean([x[k] for x in tims])), 3)
                   for k in ("count_ms", "stats_ms", "schedule_ms", "band_ms", "finalize_ms", "total_ms")}
         if split:
@@ -480,6 +506,7 @@ def main():
                               engine_ms=round(float(v[2]), 3), pairs=int(v[3]), owned_snps=int(v[4]))
                          for g, v in enumerate(x.cpu() for x in per_rank)],
             "cpu_baseline": None,
+            "table_digest": table_digest(out),
         }
     if want_file:
         log("[rank 0] wall clock from a PLINK file ...")

@@ -139,8 +139,9 @@ int nldsc_engine_run_device_finish(nldsc_engine* e, const int64_t* import_dev, i
  * [0] genotype count, [1] per-SNP statistics, [2] window replay + schedule (host time; overlaps [0]),
  * [3] band correlation kernel (all launches), [4] finalize, [5] total.
  * Also: algorithmic FLOPs (2N(1/2 sum WSA + sum WSD)), FLOPs issued to the matrix cores by the
- * band kernel (all 32x32 blocks of the schedule, padded sample slots included), SNP pairs
- * (sum WSA) of the last run, and the band kernel's work-item count. */
+ * band kernels (counted on the GPU per work item as each kernel decides them: the products of missing-free blocks
+ * and the transposed products of diagonal blocks that are skipped are not counted; padded sample slots are), SNP
+ * pairs (sum WSA) of the last run, and the band kernel's work-item count. */
 int nldsc_engine_timings(const nldsc_engine* e, double* ms6, double* flop_alg, double* flop_issued,
                          double* pairs, int32_t* n_band_items);
 /* Path of the last run: 2 = exact Gram on fp4 MFMAs, 1 = exact Gram on int8 MFMAs, 0 = fp32;
@@ -157,9 +158,10 @@ int nldsc_engine_band_round_items(const nldsc_engine* e);
 int nldsc_engine_band_tail_ksplit(const nldsc_engine* e);
 /* Band kernel of the last run: NLDSC_BAND_F32 (fp32 MFMA GEMM), NLDSC_BAND_I8, NLDSC_BAND_F4 (one wave per
  * 32x32 block pair), NLDSC_BAND_F4_SEG (rows above 2^19 samples), NLDSC_BAND_F4_KSPLIT, NLDSC_BAND_F4_2X2
- * (4-wave workgroups over 2x2 block pairs sharing their strips through LDS), NLDSC_BAND_F4_ROUTED (the default
- * for sorted non-negative positions: missing-free 2x2 super-items in the 2x2 workgroups, the rest in the
- * single-block kernel).  All exact paths give bitwise the same results. */
+ * (4-wave workgroups over 2x2 block pairs sharing their strips through LDS), NLDSC_BAND_F4_ROUTED (missing-free
+ * 2x2 super-items in the 2x2 workgroups, the rest in the single-block kernel), NLDSC_BAND_F4_QUAD (the default for
+ * sorted non-negative positions: missing-free 4x4 super-items in the quad workgroups, the rest in the single-block
+ * kernel).  All exact paths give bitwise the same results. */
 #define NLDSC_BAND_F32 0
 #define NLDSC_BAND_I8 1
 #define NLDSC_BAND_F4 2

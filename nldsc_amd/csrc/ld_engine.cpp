@@ -161,8 +161,9 @@ struct nldsc_engine {
     double* split_table = nullptr;
     double split_ms1 = 0.0;  // the first call's host time
     bool ksplit_ok = true;    // $NLDSC_KSPLIT=0 disables the K-split
-    int ksplit_force = 0;     // ($NLDSC_KSPLIT_P=P, study) the K-split factor of every K-split launch
-    int round_min = 1;        // ($NLDSC_ROUND_MIN) round launches from this many rounds of single-block items on
+    static constexpr int round_min = 1;  // round launches from this many rounds of single-block items on
+    // deferred rare-variant Gram tiles: at most this many block-pair slots (32 KiB each: 2 GiB)
+    size_t rep_gram_max_slots = (size_t)1 << 16;
     bool replay_overlap = true;  // $NLDSC_REPLAY_OVERLAP=0 runs the rare-variant replay in line on the main stream
     int last_ksplit = 1;
     int last_round_items = 0;
@@ -332,8 +333,6 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_GPU_PLAN")) e->gpu_plan = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_ORIENT")) e->orient = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_KSPLIT")) e->ksplit_ok = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_ROUND_MIN")) e->round_min = std::max(1, std::atoi(v));
-    if (const char* v = std::getenv("NLDSC_KSPLIT_P")) e->ksplit_force = std::max(0, std::min(8, std::atoi(v)));
     if (const char* v = std::getenv("NLDSC_REPLAY_OVERLAP")) e->replay_overlap = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_T2")) e->t2_mode = std::max(0, std::min(3, std::atoi(v)));
     if (const char* v = std::getenv("NLDSC_BAND_ROUNDS")) e->band_rounds = std::atoi(v) != 0;
@@ -556,8 +555,9 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
              double* table_dev, int32_t width, char* err, size_t errlen, long long* export_dev = nullptr,
              int32_t export_cap = 0, int32_t* export_n = nullptr) {
     const bool split = export_n != nullptr;
-    if (split) e->split_pending = false;
     if (!e || !p || (!r && !table_dev)) return set_err(err, errlen, NLDSC_E_ARG, "NULL argument");
+    // any run overwrites the accumulators a pending split run left for run_device_finish
+    e->split_pending = false;
     if (!e->bed.p) return set_err(err, errlen, NLDSC_E_ARG, "no BED image loaded");
     if (p->n_snp != e->n_snp || p->n_org != e->n_org)
         return set_err(err, errlen, NLDSC_E_ARG, "params (%d SNPs x %d) do not match the loaded BED (%d x %d)",
@@ -676,7 +676,6 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                     best = cost(P);
                     ksplit = P;
                 }
-            if (e->ksplit_force > 0 && 2 * e->ksplit_force <= n_it) ksplit = e->ksplit_force;
         }
         return ksplit;
     };
@@ -891,7 +890,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // of a launch start together and, all of equal length, stay at nearby K offsets, so the waves on one XCD that
     // share a strip (the plan's 16 x 16 tiles) read it from that XCD's L2.  In one launch of all items the waves
     // drift apart and most strip bytes come from beyond L2 again (C3: 68 -> 14 GB per band, the clock 1.90 -> 2.02
-    // GHz; band -2 to -4 % after the launch tails).  From one round of items on ($NLDSC_ROUND_MIN), only for long rows: the
+    // GHz; band -2 to -4 % after the launch tails).  From one round of items on (round_min), only for long rows: the
     // waves of a round also reach their epilogues together, which then no longer overlap another wave's products —
     // at N = 50 000 (strips of 0.4 MB, L2-resident anyway; epilogue ~1/3 of an item) round launches made the band
     // 2.8 -> 5.1 ms.  The last, partial round leaves wave slots idle for a whole item length (C3: 1 458 items in
@@ -900,7 +899,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // rare-variant items of the single-block fp4 kernel run their K loops in the main launch (Gram tiles kept), their
     // epilogues after the replay (launch_band_f4 rep_gram): unsegmented rows, no K-split of the whole band (whose
     // partial kernel already runs every item)
-    const bool defer = replay && e->defer_rep && use_f4 && ksplit == 1 && n_it <= nldsc::F4_SEG_CHUNKS;
+    bool defer = replay && e->defer_rep && use_f4 && ksplit == 1 && n_it <= nldsc::F4_SEG_CHUNKS;
     auto size_single = [&]() -> hipError_t {
         round_items = use_f4 && ksplit == 1 && e->band_rounds && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 1024 &&
                       n_single >= e->round_min * slots ? slots : 0;
@@ -909,7 +908,11 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         n_full = tail_p > 1 ? n_single - tail : n_single;
         e->last_round_items = round_items;
         e->last_tail_ksplit = tail_p;
-        if (defer && n_full > 0) {  // slots for every block pair of the main launch (an upper bound)
+        // slots for every block pair of the main launch (an upper bound: which items hold a replayed SNP is known on
+        // the device only); past REP_GRAM_MAX_SLOTS (32 KiB each) the KC launch after the replay runs those items
+        // instead (a wide band of data with missing calls, where nearly every item stays in this kernel: ADVICE r03)
+        if (defer && (size_t)n_full * (nc2 ? 2 : 1) > e->rep_gram_max_slots) defer = false;
+        if (defer && n_full > 0) {
             const size_t slots = (size_t)n_full * (nc2 ? 2 : 1);
             hipError_t r = e->rep_gram.ensure(slots * 8192);
             if (r == hipSuccess) r = e->rep_items.ensure(slots);

@@ -135,14 +135,15 @@ def _assemble_device(blocks, spans: list[tuple[int, int]], n_snp: int) -> dict:
     host.copy_(full, non_blocking=True)
     torch.cuda.current_stream(full.device).synchronize()
     h = host.numpy()
-    return {k: (h[i] if i < 4 else h[i].astype(np.int32)) for i, k in enumerate(RESULT_KEYS)}
+    # copies: the pinned buffer is reused by the next gather (a caller keeping this dict must not see it change)
+    return {k: (h[i].copy() if i < 4 else h[i].astype(np.int32)) for i, k in enumerate(RESULT_KEYS)}
 
 
 def gather_table(table, spans: list[tuple[int, int]], n_snp: int, *, out=None) -> dict | None:
     """One all_gather of every rank's [7, width] fp64 table block (torch tensor; with RCCL it stays in device
     memory and rank 0 assembles the table there before one copy to pinned host memory); the full result dict on
     rank 0, None elsewhere.  `out`: a reusable flat buffer of world * 7 * width elements on the table's device.
-    (Rank 0's float arrays are views of a pinned buffer reused by the next call.)"""
+    (Rank 0's arrays are its own: the pinned staging buffer reused by the next call is copied out.)"""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(), dist.get_rank()
@@ -249,6 +250,10 @@ def exchange_halo(export, n_send: int, imported, n_recv: int):
             req.wait()
     if host and rank > 0 and n_recv > 0:
         recv.copy_(recv_h)
+    if recv.is_cuda:
+        # with RCCL, wait() only makes torch's current stream wait for the receive; the engine reads `imported` on
+        # its own stream, so the host waits here (also done by Engine.run_device_finish)
+        torch.cuda.current_stream(recv.device).synchronize()
 
 
 def calculate_sharded_split(bed_path: str, n_snp: int, n_org: int, ld_wind: float, maf: float, std_thr: float,

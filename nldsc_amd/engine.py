@@ -18,6 +18,15 @@ BAND_KERNELS = {0: "f32", 1: "i8", 2: "f4", 3: "f4_seg", 4: "f4_ksplit", 5: "f4_
                 7: "f4_quad"}
 
 
+def _torch_ready(*tensors):
+    """Device tensors handed to the engine were written on torch's current stream (fills, copies, collectives:
+    with RCCL, `req.wait()` only orders torch's stream); the engine runs on its own non-blocking HIP stream, so
+    the host waits for torch's stream first."""
+    import torch
+    for d in {t.device for t in tensors if t is not None and t.is_cuda}:
+        torch.cuda.current_stream(d).synchronize()
+
+
 class Engine:
     def __init__(self, device: int = -1, lib_path: str | None = None):
         self._L = L = _lib.lib(lib_path)
@@ -101,6 +110,7 @@ class Engine:
                 or not table.is_contiguous():
             raise ValueError("table must be a contiguous float64 CUDA tensor of shape (7, width)")
         p, _keep = _lib.make_params(n, self.n_org, ld_wind, maf, std_thr, rsq_thr, positions, flags=flags)
+        _torch_ready(table)
         err = _lib.errbuf()
         _lib.check(self._L.nldsc_engine_run_device(self._h, ctypes.byref(p), int(own[0]), int(own[1]),
                                                       ctypes.c_void_p(table.data_ptr()), int(table.shape[1]), err,
@@ -120,6 +130,7 @@ class Engine:
             raise ValueError("export must be a contiguous int64 CUDA tensor")
         p, _keep = _lib.make_params(n, self.n_org, ld_wind, maf, std_thr, rsq_thr, positions, flags=flags)
         cnt = ctypes.c_int32(0)
+        _torch_ready(table, export)
         err = _lib.errbuf()
         _lib.check(self._L.nldsc_engine_run_device_split(
             self._h, ctypes.byref(p), int(own[0]), int(own[1]), ctypes.c_void_p(table.data_ptr()),
@@ -132,6 +143,8 @@ class Engine:
         first n owned SNPs, finalize and write the table given to run_device_split."""
         err = _lib.errbuf()
         ptr = ctypes.c_void_p(imported.data_ptr()) if (imported is not None and n > 0) else None
+        if ptr is not None:
+            _torch_ready(imported)
         _lib.check(self._L.nldsc_engine_run_device_finish(self._h, ptr, int(n), err, len(err)), err)
 
     def timings(self) -> dict:

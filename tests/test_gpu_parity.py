@@ -1116,3 +1116,32 @@ def test_deferred_rare_variant_items_bitwise_kc_launch(engine, dom):
     if not dom:
         exp = dict(exp, l2d=np.full(M, np.nan), l2d_ws=np.full(M, -1, np.int32), l2d_wse=np.full(M, -1, np.int32))
     assert_ld_close(got, exp, label=f"deferred rare dom={dom}")
+
+
+def test_deferred_rare_items_capped_on_wide_bands_with_missing_calls(engine):
+    """A wide band (1000 kb windows at 288 bp per SNP: ~3 500 neighbours) of data with missing calls keeps nearly every
+    item in the single-block kernel; the deferred rare-variant Gram tiles would need 32 KiB per item (~140
+    GB at the C5 slice with 1 % missing).  Past 2^16 items the engine runs the rare-variant items in the KC launch
+    instead: bitwise the KC launch ($NLDSC_DEFER_REP=0), and the exact integer outputs of a few SNPs equal the oracle's."""
+    from nldsc_amd import synth
+    from nldsc_amd.engine import Engine
+    N, M = 2053, 90_000
+    buf, pos = synth.device_bed(M, N, seed=41, length_cm=288.0 * M, missing=0.01)
+    args = (1.0e6, 1e-4, 1e-5, 1.0 / M, pos)
+
+    def fresh():
+        with Engine(0) as e:
+            e.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
+            r = e.run(*args)
+            t = e.timings()
+            assert t["band_items"] > (1 << 16) and t["band_kernel"] in ("f4", "f4_quad"), t
+            return r
+    got = fresh()
+    ref = _env_run("NLDSC_DEFER_REP", "0", fresh)
+    for k in got:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    t = np.array([0, 31, 32, 45_000, M - 1], np.int32)
+    bed = buf.cpu().numpy().tobytes()
+    exp = O.run_c(bed, M, N, *args, targets=t, flags=O.NO_COPIES)
+    sub = {k: v[t] for k, v in got.items()}
+    assert_ld_close(sub, exp, label="wide band, missing calls, replayed rare variants vs oracle")

@@ -187,3 +187,91 @@ def test_split_halo_equals_duplicate_halo_and_one_process(tmp_path, ranks):
     d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert len(d.pop("plan")) == ranks
     assert all(a and b for a, b in d.values()), d
+
+
+EIGHT_SCRIPT = r'''
+import json, os, sys
+sys.path.insert(0, {repo!r})
+import numpy as np
+import torch
+import torch.distributed as dist
+torch.cuda.set_device(0)
+dist.init_process_group("gloo")
+from nldsc_amd import distributed as D
+from nldsc_amd.ldscore import _ldscore as lds
+from nldsc_amd.ldscore.common import PLINKFile
+bed, bim, fam = PLINKFile.parse({bfile!r})
+pos = np.asarray(bim.cm, dtype=np.float64)
+M, N, w = bim.n_snp, fam.n_org, 1.0
+args = (bed.data, M, N, w, 1e-4, 1e-5, 1.0 / M)
+own = D.shard_ranges(pos, w, dist.get_world_size())[dist.get_rank()]
+full = D.calculate_sharded(D.engine_runner(*args, pos, device=0), pos, w, M)
+owned = [torch.zeros(2, dtype=torch.int64) for _ in range(dist.get_world_size())]
+dist.all_gather(owned, torch.tensor(own, dtype=torch.int64))
+if dist.get_rank() == 0:
+    p = lds.LDScoreParams(bed.data, n_snp=M, n_org=N, ld_wind=w, maf=1e-4, std_thr=1e-5, rsq_thr=1.0 / M,
+                          positions=pos.tolist())
+    one = lds.calculate(p)
+    out = dict(spans=[t.tolist() for t in owned])
+    for k in D.RESULT_KEYS:
+        a, r = np.asarray(full[k], dtype=np.float64), np.asarray(getattr(one, k), dtype=np.float64)
+        if k in ("l2", "l2d"):  # each rank's 32-SNP block grid starts at its halo slice: fp64 sums regrouped
+            out[k] = bool(np.allclose(a, r, rtol=1e-12, atol=1e-12, equal_nan=True))
+        else:
+            out[k] = bool(np.array_equal(a, r, equal_nan=True))
+    print(json.dumps(out), flush=True)
+dist.destroy_process_group()
+'''
+
+
+def test_eight_gloo_ranks_gathered_table_equals_one_process(tmp_path):
+    """The metric's largest rank count (8) through the sharded path on one GPU (gloo ranks sharing it): each rank
+    loads its owned range + halo from the .bed, computes its owned SNPs, the table is gathered on rank 0 and equals
+    the one-process `calculate` (window counts, MAF, residual std bitwise; L2 / L2D to 1e-12); the 8 owned ranges
+    tile [0, M).  N = 20 011, 6 000 SNPs over 9 cM, 1 % missing."""
+    import json
+    from nldsc_amd import synth
+    synth.write_plink(str(tmp_path / "chr1"), synth.SynthSpec(n_org=20_011, n_snp=6000, length_cm=9.0, seed=23,
+                                                                missing=0.01), chrom=1)
+    script = tmp_path / "eight.py"
+    script.write_text(EIGHT_SCRIPT.format(repo=REPO, bfile=str(tmp_path / "chr1")))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), str(script)]
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    spans = d.pop("spans")
+    assert len(spans) == 8 and spans[0][0] == 0 and spans[-1][1] == 6000
+    assert all(spans[g][1] == spans[g + 1][0] for g in range(7)) and all(b > a for a, b in spans), spans
+    assert all(d.values()), d
+
+
+def _bench(args, timeout=600):
+    import json
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+def test_bench_eight_gloo_ranks_equals_one_gpu():
+    """`bench.py --gpus 8` (the metric's 8-GPU command, its ranks started by bench.py itself) rehearsed with 8 gloo
+    ranks on the one GPU: n_gpus 8, one per_rank entry per rank, owned SNPs tiling the chromosome, and the gathered
+    score table equal to the 1-GPU run of the same synthetic chromosome (window counts bitwise, L2 / L2D sums to
+    1e-9 relative)."""
+    small = ["--no-cpu", "--no-file", "--steps", "2", "--warmup", "1", "--n-snp", "6000", "--n-org", "20000",
+             "--length-cm", "21"]
+    one = _bench(["--gpus", "1"] + small)
+    eight = _bench(["--gpus", "8", "--backend", "gloo"] + small)
+    assert eight["n_gpus"] == 8 and eight["scaling"] == "strong" and eight["value"] > 0, eight
+    pr = eight["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(8)) and sum(r["owned_snps"] for r in pr) == 6000, pr
+    a, b = one["table_digest"], eight["table_digest"]
+    assert a["counts_sha16"] == b["counts_sha16"] and a["n_snp"] == b["n_snp"] == 6000, (a, b)
+    for k in ("l2_sum", "l2d_sum"):
+        assert abs(a[k] - b[k]) <= 1e-9 * abs(a[k]), (k, a[k], b[k])

@@ -4,7 +4,7 @@
 # which reads its traffic from those summaries.   gpurun --timeout 1200 -- bash tools/gpu_bench_final.sh <tag>
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 T=${1:-r3b}
-bash tools/gpu_round3.sh $T skip-tests bench || exit 1
+bash tools/gpu_round.sh $T skip-tests bench || exit 1
 O=gpurun_out/$T
 timeout -k 10 300 python bench.py --no-cpu --no-file --steps 10 --n-org 50000 --additive-only > $O/bench_c2.json 2> $O/bench_c2.err || { tail $O/bench_c2.err; exit 1; }
 timeout -k 10 400 python bench.py --no-cpu --no-file --steps 2 --workload c5 > $O/bench_c5.json 2> $O/bench_c5.err || { tail $O/bench_c5.err; exit 1; }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU parity tests + smoke on the GPU box (first half of a round checkpoint; tools/gpu_round3.sh <tag> skip-tests
+# GPU parity tests + smoke on the GPU box (first half of a round checkpoint; tools/gpu_round.sh <tag> skip-tests
 # is the second).  Usage: gpurun --timeout 1200 -- bash tools/gpu_tests.sh <tag>
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/${1:-run}
