@@ -317,6 +317,70 @@ __global__ void __launch_bounds__(256) count_rows_kernel(uint8_t* __restrict__ i
     }
 }
 
+// The count-free pipeline (fp4 path, GPU plan; ld_engine.cpp): no per-run count pass over the rows.  Per run only the
+// tail chunks are rebuilt for this run's sample order (what count_rows_kernel does besides counting): the last byte
+// keeps the bit pairs that are individuals, the rest and the pitch padding take the pad code.  One thread per
+// (row, 16-byte half of its 32-byte piece of a chunk).
+__global__ void __launch_bounds__(256) tail_rows_kernel(uint8_t* __restrict__ img, const uint8_t* __restrict__ last,
+                                                        int n_snp, int nb, int row_bytes, uint32_t tail_keep,
+                                                        uint32_t pad) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x, j = g >> 1, h = g & 1;
+    if (j >= n_snp) return;
+    const int n_ch = row_bytes >> 5, tc0 = (nb - 1) >> 5;
+    uint8_t* bbase = img + (size_t)(j >> 5) * 32 * (size_t)row_bytes;
+    const uint32_t lb = ((uint32_t)last[j] & tail_keep) | (pad & ~tail_keep & 0xFFu);
+    for (int tt = tc0; tt < n_ch; ++tt) {
+        uint4* unit = reinterpret_cast<uint4*>(bbase + (size_t)tt * 1024 + (size_t)(j & 31) * 32 + 16 * h);
+        const uint4 v = *unit;
+        uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t o = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int p = 32 * tt + 16 * h + 4 * q + k;
+                const uint32_t byte = p < nb - 1 ? (wd[q] >> (8 * k)) & 0xFFu : p == nb - 1 ? lb : (pad & 0xFFu);
+                o |= byte << (8 * k);
+            }
+            wd[q] = o;
+        }
+        *unit = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    }
+}
+
+// the diagonal block pairs (I, I) of every block, the head of the count-free pipeline's first list
+__global__ void diag_items_kernel(int nblk, int4* __restrict__ out) {
+    const int I = blockIdx.x * blockDim.x + threadIdx.x;
+    if (I < nblk) out[I] = make_int4(I, I, 1, 0);
+}
+
+// Genotype counts from the diagonal Gram tiles (band_f4_part_kernel, P pieces per item, the diagonal items first in
+// the list): with v = m + 2x (the e2m1 operand of the raw code: 0, 1 missing, 2 het, 4 hom A2 of the stored coding)
+// and h = [x >= 1], SNP j's own entries are v.v = n_miss + 4 c1 + 16 c2, v.m = n_miss and v.h = 2 c1 + 4 c2 (exact
+// integers; m = 0 on the non-individual slots, which hold code 00), so c2 = ((v.v - v.m) / 4 - v.h / 2) / 2,
+// c1 = v.h / 2 - 2 c2, c0 = n_org - n_miss - c1 - c2 — what count_rows_kernel counts, in the stored coding.  Lane
+// (i, h) register r of a tile holds (row (r & 3) + 8 (r >> 2) + 4 h, column i): entry (j, j) is lane j + 32 ((j >> 2)
+// & 1), register (j & 3) + 4 (j >> 3).
+__global__ void diag_counts_kernel(const float* __restrict__ gram, int P, int n_snp, int n_org,
+                                   int* __restrict__ counts) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_snp) return;
+    const int I = j >> 5, i = j & 31, lane = i + 32 * ((i >> 2) & 1), r = (i & 3) + 4 * (i >> 3);
+    long long vv = 0, vm = 0, vh = 0;
+    for (int p = 0; p < P; ++p) {
+        const float* t = gram + ((size_t)I * P + p) * 8192 + lane * 16 + r;
+        vv += (long long)t[0];
+        vm += (long long)t[1024];
+        vh += (long long)t[4 * 1024];
+    }
+    const long long a = (vv - vm) / 4, b = vh / 2;  // c1 + 4 c2, c1 + 2 c2
+    const long long c2 = (a - b) / 2, c1 = b - 2 * c2;
+    counts[4 * (size_t)j] = (int)((long long)n_org - vm - c1 - c2);
+    counts[4 * (size_t)j + 1] = (int)c1;
+    counts[4 * (size_t)j + 2] = (int)c2;
+    counts[4 * (size_t)j + 3] = 0;
+}
+
 // ------------------------------------------------------------------------------------------
 // 2. per-SNP statistics -> lookup tables
 // ------------------------------------------------------------------------------------------
@@ -782,8 +846,9 @@ __global__ void __launch_bounds__(1024) plan_right_kernel(const int* __restrict_
 
 // per row block I: useful column offsets d = J - I, [d0, d1] (empty: d0 > d1); meta[0] = max d1 + 1,
 // meta[2] = diagonal items
+// skip_diag (the count-free pipeline, which runs every diagonal block pair in its own list): offsets from 1
 __global__ void plan_rows_kernel(const int* __restrict__ E, const int* __restrict__ A, int n, int nblk, int own_lo,
-                                 int own_hi, int2* __restrict__ rows, int* __restrict__ meta) {
+                                 int own_hi, int2* __restrict__ rows, int* __restrict__ meta, int skip_diag) {
     const int I = blockIdx.x * blockDim.x + threadIdx.x;
     if (I >= nblk) return;
     int2 r = make_int2(1, 0);
@@ -793,7 +858,7 @@ __global__ void plan_rows_kernel(const int* __restrict__ E, const int* __restric
         const int ob0 = own_lo / 32, ob1 = (own_hi - 1) / 32;
         const bool own_row = I >= ob0 && I <= ob1;
         const int J0 = own_row ? I : max(I, ob0), J1 = own_row ? Jmax : min(Jmax, ob1);
-        r = make_int2(J0 - I, J1 - I);
+        r = make_int2(max(J0 - I, skip_diag), J1 - I);
     }
     rows[I] = r;
     if (r.x <= r.y) {
@@ -1554,7 +1619,8 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
                                              int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                                              int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
                                              int* __restrict__ ws_acc, float* tr, int t_lo = 0, int t_hi = 0,
-                                             float* __restrict__ part = nullptr) {
+                                             float* __restrict__ part = nullptr,
+                                             const uint8_t* __restrict__ blk_flags = nullptr) {
     constexpr int NS = 32 * (1 + NC);
     const int lane = threadIdx.x & 63;
     const int i = lane & 31, h = lane >> 5;
@@ -1658,8 +1724,10 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     // wave-uniform: does the row block / do the column blocks hold a missing call (flag bit 2)?  With PART this
     // is the only SNP state used (sh.cst and the other flag bits may be rewritten by a concurrent replay:
     // launch_reference_residuals in ld_kernels.h)
-    const bool rm = __any(lane < 32 && (sh.info[lane].fl & 4));
-    const bool cm = __any(32 + lane < NS && (sh.info[32 + lane].fl & 4));
+    // (blk_flags: the per-block missing flags of this run's sample order, blk_miss — the count-free pipeline's
+    // partial K loops run before the statistics that set flag bit 2)
+    const bool rm = blk_flags != nullptr ? blk_flags[I] != 0 : __any(lane < 32 && (sh.info[lane].fl & 4));
+    const bool cm = blk_flags != nullptr ? blk_flags[J0] != 0 : __any(32 + lane < NS && (sh.info[32 + lane].fl & 4));
     auto run = [&](const int t_lo, const int t_hi) {
         if (rm && cm) kloop(std::true_type{}, std::true_type{}, t_lo, t_hi);
         else if (rm) kloop(std::true_type{}, std::false_type{}, t_lo, t_hi);
@@ -2366,7 +2434,8 @@ __global__ void __launch_bounds__(64, 2) band_f4_part_kernel(const uint32_t* __r
                                                            const int* __restrict__ Rw,
                                                            const uint8_t* __restrict__ sflags, int n_snp, int P,
                                                            float* __restrict__ gram,
-                                                           const uint8_t* __restrict__ blk_miss, int route_shift) {
+                                                           const uint8_t* __restrict__ blk_miss, int route_shift,
+                                                           const uint8_t* __restrict__ blk_flags) {
     __shared__ BandI8Lds sh;
     __shared__ float tr[32 * 33];
     const int u = xcd_slot(blockIdx.x, gridDim.x), item = u / P, piece = u % P;
@@ -2378,8 +2447,16 @@ __global__ void __launch_bounds__(64, 2) band_f4_part_kernel(const uint32_t* __r
     float* part = gram + (size_t)u * 8192;
 #define NLDSC_BODY(DIAG_)                                                                                             \
     band_f4_body<DOM, 1, DIAG_, 0, false, true>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp,     \
-                                                0.0, 0.0, 0.0, 0, 0, nullptr, nullptr, nullptr, tr, t_lo, t_hi, part)
-    if (it.y == it.x) NLDSC_BODY(true); else NLDSC_BODY(false);
+                                                0.0, 0.0, 0.0, 0, 0, nullptr, nullptr, nullptr, tr, t_lo, t_hi, part, \
+                                                blk_flags)
+    // (count-free pipeline, blk_flags set: a diagonal item computes v.h even in additive-only runs, for the counts)
+    if (it.y == it.x) {
+        if (!DOM && blk_flags != nullptr)
+            band_f4_body<true, 1, true, 0, false, true>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp,
+                                                        0.0, 0.0, 0.0, 0, 0, nullptr, nullptr, nullptr, tr, t_lo, t_hi,
+                                                        part, blk_flags);
+        else NLDSC_BODY(true);
+    } else NLDSC_BODY(false);
 #undef NLDSC_BODY
 }
 
@@ -2683,14 +2760,14 @@ hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const doubl
 }
 
 hipError_t launch_plan(const double* pos, int n, double w, int own_lo, int own_hi, int* A, int* E, int* R,
-                       int2* rows, int* counts, int* meta, hipStream_t st, bool pair) {
+                       int2* rows, int* counts, int* meta, hipStream_t st, bool pair, bool skip_diag) {
     const int nblk = (n + 31) / 32;
     hipError_t e = hipMemsetAsync(meta, 0, 4 * sizeof(int), st);
     if (e != hipSuccess || n <= 0 || own_hi <= own_lo) return e;
     hipLaunchKernelGGL(plan_edges_kernel, dim3((n + 255) / 256), dim3(256), 0, st, pos, n, w, A, E);
     hipLaunchKernelGGL(plan_right_kernel, dim3(1), dim3(1024), 0, st, E, n, R);
     hipLaunchKernelGGL(plan_rows_kernel, dim3((nblk + 255) / 256), dim3(256), 0, st, E, A, n, nblk, own_lo, own_hi,
-                       rows, meta);
+                       rows, meta, skip_diag ? 1 : 0);
     hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, counts, pair ? 1 : 0);
     hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts, nblk, meta);
     return hipGetLastError();
@@ -2815,15 +2892,68 @@ hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* ge
     const dim3 grid_p((unsigned)n_items * (unsigned)P);
     if (!(which & 1)) goto kc;  // the partial tiles of every item come from the main launch
     if (dom) hipLaunchKernelGGL((band_f4_part_kernel<true>), grid_p, dim3(64), 0, st, geno, pitch_words, n_it, cst,
-                                items, pos, Lw, Rw, sflags, n_snp, P, gram, blk_miss, route_shift);
+                                items, pos, Lw, Rw, sflags, n_snp, P, gram, blk_miss, route_shift, nullptr);
     else hipLaunchKernelGGL((band_f4_part_kernel<false>), grid_p, dim3(64), 0, st, geno, pitch_words, n_it, cst,
-                            items, pos, Lw, Rw, sflags, n_snp, P, gram, blk_miss, route_shift);
+                            items, pos, Lw, Rw, sflags, n_snp, P, gram, blk_miss, route_shift, nullptr);
 #define NLDSC_EPI(DOM_, KC_)                                                                                        \
     hipLaunchKernelGGL((band_f4_epi_kernel<DOM_, KC_>), dim3(n_items), dim3(64), 0, st, cst, items, pos, Lw, Rw,    \
                        sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, blk_rep, P, gram, \
                        blk_miss, route_shift, nullptr)
     if (dom) NLDSC_EPI(true, false); else NLDSC_EPI(false, false);
 kc:
+    if (blk_rep && (which & 2)) { if (dom) NLDSC_EPI(true, true); else NLDSC_EPI(false, true); }
+#undef NLDSC_EPI
+    return hipGetLastError();
+}
+
+hipError_t launch_tail_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
+                            uint32_t pad, hipStream_t st) {
+    if (n_snp <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tail_rows_kernel, dim3((2 * n_snp + 255) / 256), dim3(256), 0, st, img, last, n_snp, nb, row_bytes,
+                       tail_keep, pad);
+    return hipGetLastError();
+}
+
+hipError_t launch_diag_items(int nblk, int4* out, hipStream_t st) {
+    if (nblk <= 0) return hipSuccess;
+    hipLaunchKernelGGL(diag_items_kernel, dim3((nblk + 255) / 256), dim3(256), 0, st, nblk, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_diag_counts(const float* gram, int P, int n_snp, int n_org, int* counts, hipStream_t st) {
+    if (n_snp <= 0) return hipSuccess;
+    hipLaunchKernelGGL(diag_counts_kernel, dim3((n_snp + 255) / 256), dim3(256), 0, st, gram, P, n_snp, n_org, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_band_f4_parts(bool dom, int P, int n_items, const uint32_t* geno, int pitch_words, int n_it,
+                                const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
+                                const uint8_t* sflags, int n_snp, float* gram, const uint8_t* blk_flags,
+                                int round_items, hipStream_t st) {
+    if (n_items <= 0) return hipSuccess;
+    if (n_it > F4_SEG_CHUNKS || P < 1 || 2 * P > n_it || blk_flags == nullptr) return hipErrorInvalidValue;
+    const int chunk = round_items > 0 ? round_items : n_items;
+    for (int o = 0; o < n_items; o += chunk) {
+        const dim3 grid((unsigned)std::min(chunk, n_items - o) * (unsigned)P);
+        float* g = gram + (size_t)o * P * 8192;
+        if (dom) hipLaunchKernelGGL((band_f4_part_kernel<true>), grid, dim3(64), 0, st, geno, pitch_words, n_it, cst,
+                                    items + o, pos, Lw, Rw, sflags, n_snp, P, g, nullptr, 1, blk_flags);
+        else hipLaunchKernelGGL((band_f4_part_kernel<false>), grid, dim3(64), 0, st, geno, pitch_words, n_it, cst,
+                                items + o, pos, Lw, Rw, sflags, n_snp, P, g, nullptr, 1, blk_flags);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_band_f4_epis(bool dom, int P, int n_items, const SnpConst* cst, const int4* items, const double* pos,
+                               const int* Lw, const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind,
+                               double n_org, double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
+                               int* ws_acc, const uint8_t* blk_rep, const float* gram, int which, hipStream_t st) {
+    if (n_items <= 0) return hipSuccess;
+#define NLDSC_EPI(DOM_, KC_)                                                                                        \
+    hipLaunchKernelGGL((band_f4_epi_kernel<DOM_, KC_>), dim3(n_items), dim3(64), 0, st, cst, items, pos, Lw, Rw,    \
+                       sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, blk_rep, P, gram, \
+                       nullptr, 1, nullptr)
+    if (which & 1) { if (dom) NLDSC_EPI(true, false); else NLDSC_EPI(false, false); }
     if (blk_rep && (which & 2)) { if (dom) NLDSC_EPI(true, true); else NLDSC_EPI(false, true); }
 #undef NLDSC_EPI
     return hipGetLastError();
