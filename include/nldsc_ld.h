@@ -172,11 +172,10 @@ int nldsc_engine_band_tail_ksplit(const nldsc_engine* e);
 #define NLDSC_BAND_F4_QUAD 7 /* $NLDSC_T2=3: missing-free 4x4 super-items in the quad workgroups (64x64 tiles per
                                 wave), the rest in the single-block kernel */
 int nldsc_engine_band_kernel(const nldsc_engine* e);
-/* 1 when the last run took the count-free pipeline (fp4, rows of >= 2^17 samples, sorted non-negative positions, no
- * missing-free block): no per-run genotype-count pass over the rows; the diagonal block pairs run first and their
- * exact Gram tiles give every SNP's genotype counts (the statistics the reference derives per SNP, encoder.h:91-133);
- * 0 when the count pass ran ($NLDSC_COUNT_FREE=0 forces it). */
-int nldsc_engine_count_free(const nldsc_engine* e);
+/* 1 when the last run overlapped the per-run genotype count with the band's first round (fp4 round launches on the GPU
+ * plan, no missing-free block): that round's K loops ran beside the count pass and its epilogues after the rest of the
+ * band ($NLDSC_COUNT_OVERLAP=0 turns it off); 0 otherwise.  The results are bitwise the same either way. */
+int nldsc_engine_count_overlap(const nldsc_engine* e);
 
 /* Load SNP rows [snp_begin, snp_end) of a .bed file of n_snp_file SNPs as the engine's image
  * (snp_end - snp_begin SNPs; the run then takes the positions of that slice).  Position sharding

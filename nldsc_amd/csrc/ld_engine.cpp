@@ -116,8 +116,11 @@ struct nldsc_engine {
     hipStream_t plan_stream = nullptr;  // the GPU schedule runs here, beside the count kernel
     hipEvent_t ev_pos = nullptr;        // positions uploaded (the schedule's only input)
     hipEvent_t ev[6] = {};
-    hipEvent_t ev_dbg[2] = {};
-    hipEvent_t ev_pre[2] = {};  // the count-free pipeline's first list (its K loops belong to the band's time)  // $NLDSC_DEBUG_TIMING: after the super-item launch, before the single-block launches
+    hipEvent_t ev_dbg[2] = {};  // $NLDSC_DEBUG_TIMING: after the super-item launch, before the single-block launches
+    // the count overlap (run_impl): the first round's K loops on aux_stream (start, end); the rows' tails rewritten
+    hipEvent_t ev_pre[2] = {};
+    hipEvent_t ev_tail = nullptr;
+    hipStream_t aux_stream = nullptr;
     bool debug_timing = false;
     hipEvent_t ev_plan = nullptr;  // GPU plan counters landed in h_meta
     hipEvent_t ev_stats = nullptr;   // SNP constants and replay flags written (the replay's inputs)
@@ -190,15 +193,14 @@ struct nldsc_engine {
     // 351 -> 333 ms, C3 missing-free (6 rounds, below the threshold) 12.34 -> 12.51 ms (profiles/r03_ab_q_rounds.json)
     bool q_rounds = true;
     int last_band_kernel = NLDSC_BAND_F4;
-    // Count-free pipeline ($NLDSC_COUNT_FREE=0: the count pass instead): fp4 runs on the GPU plan with no super-item
-    // routing skip the per-run count over the rows; the diagonal block pairs go first, their Gram tiles give the
-    // counts (see run_impl).  free_blocks[order]: 32-SNP blocks without a missing call among the individual slots of
-    // sample order `order` (row_miss, at load) — super-item routing needs such blocks, the pipeline needs none.
-    bool count_free = true;
+    // Count overlap ($NLDSC_COUNT_OVERLAP=0: off): fp4 round launches on the GPU plan with no super-item routing run the
+    // first round's K loops on aux_stream beside the per-run count pass, their Gram tiles stored (see run_impl).
+    // free_blocks[order]: 32-SNP blocks without a missing call among the individual slots of sample order `order`
+    // (row_miss, at load) — super-item routing needs such blocks.
+    bool count_overlap = true;
     int free_blocks[2] = {0, 0};
-    bool last_count_free = false;
-    DevBuf<int4> pre_items;  // the diagonal items, then (round launches) the off-diagonal items filling their last round
-    DevBuf<float> pre_gram;  // their Gram tiles
+    bool last_overlap = false;
+    DevBuf<float> pre_gram;  // the first round's Gram tiles
     DevBuf<double> pos, l2_acc, l2d_acc;
     DevBuf<int4> items;
     // host scratch
@@ -234,10 +236,12 @@ struct nldsc_engine {
         bed.release(); stage_dev.release(); lastb.release(); flip.release(); row_miss.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
         res.release(); lut.release(); cst.release(); sflags.release(); pos.release();
         l2_acc.release(); l2d_acc.release(); items.release(); gram.release();
-        rep_gram.release(); rep_items.release(); rep_count.release(); pre_items.release(); pre_gram.release();
+        rep_gram.release(); rep_items.release(); rep_count.release(); pre_gram.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         for (auto& e : ev_dbg) if (e) (void)hipEventDestroy(e);
         for (auto& e : ev_pre) if (e) (void)hipEventDestroy(e);
+        if (ev_tail) (void)hipEventDestroy(ev_tail);
+        if (aux_stream) (void)hipStreamDestroy(aux_stream);
         if (ev_plan) (void)hipEventDestroy(ev_plan);
         Ew.release(); plan_counts.release(); plan_meta.release(); plan_rows.release();
         plan_counts2.release(); plan_rows2.release(); items2.release(); blk_miss.release(); blk_zero.release(); sums.release();
@@ -363,7 +367,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_QUAD_ADD")) e->quad_add = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_Q_ROUNDS")) e->q_rounds = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_DEFER_REP")) e->defer_rep = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_COUNT_FREE")) e->count_free = std::atoi(v) != 0;
+    if (const char* v = std::getenv("NLDSC_COUNT_OVERLAP")) e->count_overlap = std::atoi(v) != 0;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
@@ -371,6 +375,8 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     }
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->plan_stream, hipStreamNonBlocking);
+    if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->aux_stream, hipStreamNonBlocking);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_tail, hipEventDisableTiming);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_pos, hipEventDisableTiming);
     for (auto& ev : e->ev)
         if (he == hipSuccess) he = hipEventCreate(&ev);
@@ -672,19 +678,16 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     const bool gpu_plan = e->gpu_plan && sorted && max_nc == 1 &&
                           std::all_of(p->positions, p->positions + M, [](double x) { return x >= 0.0; });
     const int order = strict ? 1 : 0;  // bit of row_miss: the individual slots of this run's sample order
-    // Count-free pipeline (fp4, GPU plan, unsegmented rows, no super-item routing — the data has no missing-free block
-    // in this order, or the super-item kernels are off): no per-run count pass over the rows.  The diagonal block pairs
-    // of every block run first as K loops that store their exact Gram tiles (with, in round launches, the first
-    // off-diagonal items filling their last round; small bands: every item, K-split); their own entries give every
-    // SNP's genotype counts (diag_counts_kernel), then the statistics, the rest of the band with its fused epilogues,
-    // and the stored items' epilogues.  C3: the count pass (0.94 ms) is gone, the band's work unchanged.
-    // Long rows only (N >= 2^17, the round-launch regime): for short rows the diagonal items alone fill the GPU badly
-    // and cost more than the count pass they replace (C2: ~0.5 against 0.25 ms by the K-split cost model).
-    const bool cfree = e->count_free && gpu_plan && use_f4 && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 1024 &&
-                       (e->t2_mode == 0 || e->free_blocks[order] == 0) && !(e->t2_mode == 3 && !dom && e->quad_add);
-    e->last_count_free = cfree;
+    // Count overlap (fp4 round launches on the GPU plan, no super-item routing — the data has no missing-free block in
+    // this order, or the super-item kernels are off): the count pass is HBM-bound (C3: 0.96 ms at 6.7 TB/s), the band
+    // MFMA-bound, and only the band's epilogues need the statistics.  So the first round of the band runs its K loops
+    // on aux_stream beside the count, storing its exact Gram tiles (launch_band_f4_parts); its epilogues run after the
+    // rest of the band (launch_band_f4_epis).  Bitwise the serial order's results (exact tiles, fixed-point sums).
+    const bool ovl = e->count_overlap && gpu_plan && use_f4 && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 1024 &&
+                     e->band_rounds && (e->t2_mode == 0 || e->free_blocks[order] == 0) &&
+                     !(e->t2_mode == 3 && !dom && e->quad_add);
     // the 2 x 2 block-pair workgroups: fp4, unsegmented rows, GPU plan, and no K-split (choose_ksplit below)
-    const bool t2_cand = !cfree && e->t2_mode > 0 && gpu_plan && use_f4 && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 2;
+    const bool t2_cand = !ovl && e->t2_mode > 0 && gpu_plan && use_f4 && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 2;
     // additive-only fp4 items of two column blocks (GPU plan, unsegmented rows; no K-split: its partial kernel takes
     // single block pairs)
     const bool nc2 = e->f4_nc2 && gpu_plan && use_f4 && !dom && n_it <= nldsc::F4_SEG_CHUNKS;
@@ -745,7 +748,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         HIPCHK(hipEventRecord(e->ev_pos, st));
         HIPCHK(hipStreamWaitEvent(e->plan_stream, e->ev_pos, 0));
         HIPCHK(nldsc::launch_plan(e->pos.p, M, p->ld_wind, own_begin, own_end, e->Aw.p, e->Ew.p, e->Rw.p,
-                                  e->plan_rows.p, e->plan_counts.p, e->plan_meta.p, e->plan_stream, nc2, cfree));
+                                  e->plan_rows.p, e->plan_counts.p, e->plan_meta.p, e->plan_stream, nc2));
         if (t2_cand)
             HIPCHK(nldsc::launch_plan_super(M, e->plan_rows.p, e->plan_rows2.p, e->plan_counts2.p, e->plan_meta.p + 4,
                                             route_shift,
@@ -757,32 +760,14 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     const uint32_t pad = use_f4 ? 0x00u : 0x55u;
     const int n_pad00 = use_f4 ? 4 * row_bytes - N : 0;
     const int slots = 8 * e->n_cu;  // wave slots: 2 per SIMD
-    // the count-free pipeline's first list: pre_items[0, nblk) the diagonal items, then n_pre - nblk off-diagonal
-    // items; pre_P pieces per item; [0, pre_done) launched
-    int n_pre = 0, pre_P = 1, pre_done = 0, pre_round = 0, n_fill = 0;
-    if (cfree) {
-        HIPCHK(e->blk_miss.ensure((size_t)nblk));
-        HIPCHK(nldsc::launch_block_missing_rows(e->row_miss.p, M, order, e->blk_miss.p, st));
+    // the count overlap's first round: items [0, n_pre) of the plan, their tiles in pre_gram
+    int n_pre = 0;
+    if (ovl) {  // the rows' tails first: the first round reads them while the count pass runs (it rewrites the same bytes)
         HIPCHK(nldsc::launch_tail_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, pad, st));
-        HIPCHK(hipEventRecord(e->ev[1], st));
-        if (e->band_rounds && n_it >= 1024 && nblk >= slots) {
-            // the band goes in round launches whatever the plan holds: the whole rounds of diagonal items start now,
-            // beside the plan (their last, partial round waits for the off-diagonal items that fill it)
-            pre_round = slots;
-            pre_done = nblk / slots * slots;
-            HIPCHK(e->pre_items.ensure((size_t)nblk + slots));
-            HIPCHK(e->pre_gram.ensure(((size_t)nblk + slots) * 8192));
-            HIPCHK(nldsc::launch_diag_items(nblk, e->pre_items.p, st));
-            HIPCHK(hipEventRecord(e->ev_pre[0], st));
-            HIPCHK(nldsc::launch_band_f4_parts(dom, 1, pre_done, geno, pitch_words, n_it, e->cst.p, e->pre_items.p,
-                                               e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, e->pre_gram.p,
-                                               e->blk_miss.p, pre_round, st));
-        }
-    } else {
-        HIPCHK(nldsc::launch_count_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, pad, n_pad00, e->counts.p,
-                                        st));
-        HIPCHK(hipEventRecord(e->ev[1], st));
+        HIPCHK(hipEventRecord(e->ev_tail, st));
     }
+    HIPCHK(nldsc::launch_count_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, pad, n_pad00, e->counts.p, st));
+    HIPCHK(hipEventRecord(e->ev[1], st));
     // rare variants: the reference's fp32 residual replayed (its sums assume N < 2^23); the flags per block in the
     // statistics stage, the replay itself after the schedule (below)
     const bool replay = N < (1 << 23) && !(p->flags & NLDSC_FLAG_EXACT_RARE);
@@ -805,10 +790,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     HIPCHK(hipEventRecord(e->ev[2], st));
     return NLDSC_OK;
     };
-    if (!cfree) {
-        const int rc = stats_stage();
-        if (rc) return rc;
-    }
+    if (const int rc = stats_stage()) return rc;
 
     // ---- window replay + schedule ----
     auto t_host0 = std::chrono::steady_clock::now();
@@ -818,34 +800,17 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         HIPCHK(hipEventSynchronize(e->ev_plan));  // the count kernel is running meanwhile
         const int* meta = reinterpret_cast<const int*>(e->h_meta.p);
         n_items = meta[1];
-        if (cfree) {  // (n_items: the off-diagonal items)
-            const int n_tot = n_items + nblk;
-            if (e->band_rounds && n_tot >= e->round_min * slots) {
-                // round launches: the diagonal items' last round filled with the first off-diagonal single items
-                pre_round = slots;
-                pre_P = 1;
-                n_fill = nc2 ? 0 : std::min(n_items, (slots - nblk % slots) % slots);
-            } else if (!nc2 && choose_ksplit(n_tot) > 1) {
-                pre_P = choose_ksplit(n_tot);  // a small band, K-split whole: every K loop before the statistics
-                n_fill = n_items;
-            } else {
-                pre_P = choose_ksplit(nblk, true);  // the diagonal items alone, K-split by the same cost model
-                n_fill = 0;
-            }
-            n_pre = nblk + n_fill;
-            // the rest: round launches (the last, partial round K-split) when it fills a round, else K-split whole
-            const int n_main = n_items - n_fill;
-            ksplit = e->band_rounds && n_main >= e->round_min * slots ? 1 : choose_ksplit(n_main);
-        } else {
-            ksplit = choose_ksplit(n_items);
-        }
+        // count overlap: one round of items beside the count when the rest still fills round launches
+        // (single block pairs only: additive-only column-block pairs take no partial kernel)
+        if (ovl && !nc2 && n_items >= 2 * e->round_min * slots) n_pre = slots;
+        ksplit = n_pre > 0 ? 1 : choose_ksplit(n_items);
         // long rows: bands of at least round_min rounds of wave slots go in round launches (the last, partial round
         // K-split), not K-split whole — a 1/8 shard of C3 (1.6 rounds) band 2.70-2.76 -> 2.61-2.64 ms, a 1/4 shard
         // (3.2 rounds) 5.21-5.26 -> 4.87-4.89 ms (profiles/r03_ab_round_min.txt; was from 4 rounds on)
         // — in the single-block kernel, as the K-split it replaces: a shard's few super-items leave most CUs of the
         // 4 x 4 kernel idle (a missing-free 1/8 shard of C3: 2.88 ms with it, 1.93-1.99 K-split whole)
         bool rounds_forced = false;
-        if (!cfree && e->band_rounds && use_f4 && n_it >= 1024 && n_it <= nldsc::F4_SEG_CHUNKS &&
+        if (e->band_rounds && use_f4 && n_it >= 1024 && n_it <= nldsc::F4_SEG_CHUNKS &&
             n_items >= e->round_min * 8 * e->n_cu) {
             rounds_forced = ksplit > 1;
             ksplit = 1;
@@ -868,7 +833,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                 HIPCHK(nldsc::launch_plan_emit(M, e->plan_rows.p, e->plan_meta.p, e->plan_counts.p, e->items.p, ps,
                                                nc2));
         }
-        if (use_f4 && !cfree) {  // per 32-SNP block: holds a missing call (the m-product predicate: routing, issued count)
+        if (use_f4) {  // per 32-SNP block: holds a missing call (the m-product predicate: routing, issued count)
             HIPCHK(e->blk_miss.ensure((size_t)nblk));
             HIPCHK(nldsc::launch_block_missing_rows(e->row_miss.p, M, order, e->blk_miss.p, ps));
         }
@@ -888,28 +853,17 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                                                e->compact_tmp.p + n_chunks, e->items_u.p, ps));
             HIPCHK(hipMemcpyAsync(e->h_route.p, e->compact_tmp.p + n_chunks, sizeof(int), hipMemcpyDeviceToHost, ps));
         }
-        if (cfree) {  // the first list: the diagonal items (unless launched already), then the filling items
-            if (pre_done == 0) {
-                HIPCHK(e->pre_items.ensure((size_t)n_pre));
-                HIPCHK(e->pre_gram.ensure((size_t)n_pre * pre_P * 8192));
-                HIPCHK(nldsc::launch_diag_items(nblk, e->pre_items.p, ps));
-            }
-            if (n_fill > 0)
-                HIPCHK(hipMemcpyAsync(e->pre_items.p + nblk, e->items.p, sizeof(int4) * (size_t)n_fill,
-                                      hipMemcpyDeviceToDevice, ps));
-        }
         HIPCHK(hipEventRecord(e->ev_route, ps));
         HIPCHK(hipStreamWaitEvent(st, e->ev_route, 0));  // left pointers / band read the schedule and the lists
-        if (cfree) {  // the rest of the first list's K loops, the counts from its diagonal tiles, the statistics
-            if (pre_done == 0) HIPCHK(hipEventRecord(e->ev_pre[0], st));
-            HIPCHK(nldsc::launch_band_f4_parts(dom, pre_P, n_pre - pre_done, geno, pitch_words, n_it, e->cst.p,
-                                               e->pre_items.p + pre_done, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
-                                               e->pre_gram.p + (size_t)pre_done * pre_P * 8192, e->blk_miss.p,
-                                               pre_round, st));
-            HIPCHK(hipEventRecord(e->ev_pre[1], st));
-            HIPCHK(nldsc::launch_diag_counts(e->pre_gram.p, pre_P, M, N, e->counts.p, st));
-            const int rc = stats_stage();
-            if (rc) return rc;
+        if (n_pre > 0) {  // the first round's K loops beside the count (missing flags from blk_miss: no statistics yet)
+            hipStream_t as = e->aux_stream;
+            HIPCHK(e->pre_gram.ensure((size_t)n_pre * 8192));
+            HIPCHK(hipStreamWaitEvent(as, e->ev_route, 0));
+            HIPCHK(hipStreamWaitEvent(as, e->ev_tail, 0));
+            HIPCHK(hipEventRecord(e->ev_pre[0], as));
+            HIPCHK(nldsc::launch_band_f4_parts(dom, 1, n_pre, geno, pitch_words, n_it, e->cst.p, e->items.p, e->pos.p,
+                                               e->Lw.p, e->Rw.p, e->sflags.p, M, e->pre_gram.p, e->blk_miss.p, slots, as));
+            HIPCHK(hipEventRecord(e->ev_pre[1], as));
         }
         HIPCHK(nldsc::launch_left_pointers(e->Aw.p, e->sflags.p, e->pos.p, M, e->Lw.p, st));
     } else {
@@ -984,19 +938,17 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     auto t_host1 = std::chrono::steady_clock::now();
 
     HIPCHK(hipEventRecord(e->ev[3], st));
-    // (count-free: the whole band K-split in the first list)
-    const bool pre_all = cfree && pre_round == 0 && n_fill > 0 && n_fill == n_items;
-    e->n_band_items = n_items + (cfree ? nblk : 0);
-    e->last_ksplit = pre_all ? pre_P : ksplit;
+    e->n_band_items = n_items;
+    e->last_ksplit = ksplit;
+    e->last_overlap = n_pre > 0;
     e->last_band_kernel = use_t2 ? (quad ? NLDSC_BAND_F4_QUAD : routed ? NLDSC_BAND_F4_ROUTED : NLDSC_BAND_F4_2X2) : !use_f4 ? (use_i8 ? NLDSC_BAND_I8 : NLDSC_BAND_F32)
-                        : ksplit > 1 || (pre_all && pre_P > 1) ? NLDSC_BAND_F4_KSPLIT
-                        : n_it > nldsc::F4_SEG_CHUNKS ? NLDSC_BAND_F4_SEG
+                        : ksplit > 1 ? NLDSC_BAND_F4_KSPLIT : n_it > nldsc::F4_SEG_CHUNKS ? NLDSC_BAND_F4_SEG
                         : NLDSC_BAND_F4;
     if (ksplit > 1) HIPCHK(e->gram.ensure((size_t)n_items * ksplit * 8192));
     // which = 1: the launch for the items without a replayed SNP (beside the replay), 2: the KC launch after it
     const uint8_t* blk_rep = replay ? e->blk_rep.p : nullptr;
-    int n_single = n_items - n_fill;   // single-block items (compacted when routed; count-free: after the filling ones)
-    const int4* single = e->items.p + n_fill;
+    int n_single = n_items - n_pre;    // single-block items (compacted when routed; after the count overlap's round)
+    const int4* single = e->items.p + n_pre;
     int round_items = 0, tail_p = 1, n_full = 0;
     // Unsegmented single-block fp4 items go in launches of one round of the wave slots each (2 per SIMD): the items
     // of a launch start together and, all of equal length, stay at nearby K offsets, so the waves on one XCD that
@@ -1123,11 +1075,13 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         HIPCHK(size_single());
         if (replay) HIPCHK(hipStreamWaitEvent(st, e->ev_replay, 0));  // the fp32 path reads the replayed tables
     }
-    if (cfree && n_pre > 0)  // the first list's epilogues (after the replay when replaying: waited for above)
-        HIPCHK(nldsc::launch_band_f4_epis(dom, pre_P, n_pre, e->cst.p, e->pre_items.p, e->pos.p, e->Lw.p, e->Rw.p,
+    if (n_pre > 0) {  // the count overlap's round: its epilogues (after the replay when replaying: waited for above)
+        HIPCHK(hipStreamWaitEvent(st, e->ev_pre[1], 0));
+        HIPCHK(nldsc::launch_band_f4_epis(dom, 1, n_pre, e->cst.p, e->items.p, e->pos.p, e->Lw.p, e->Rw.p,
                                           e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin, flush_hi,
                                           e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, blk_rep, e->pre_gram.p,
                                           replay ? 3 : 1, st));
+    }
     if (n_items > 0 && !use_f4 && !use_i8) {
         HIPCHK(nldsc::launch_band(dom, 2, n_items, geno, pitch_words, n_it,
                                       e->lut.p, e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
@@ -1149,19 +1103,15 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                                              (use_t2 && quad_add ? 4 : 0),
                                          route_shift,
                                          e->sums.p + 2, st));
-    if (cfree && n_pre > 0) {  // (diagonal items issue the dominance products in every run: the counts need v.h)
-        HIPCHK(nldsc::launch_issued_products(e->pre_items.p, nblk, nullptr, 0, nullptr, e->blk_miss.p, nblk, path, true,
-                                             0, route_shift, e->sums.p + 2, st));
-        HIPCHK(nldsc::launch_issued_products(e->pre_items.p + nblk, n_fill, nullptr, 0, nullptr, e->blk_miss.p, nblk,
-                                             path, dom, 0, route_shift, e->sums.p + 2, st));
-    }
-    // stage times: the count-free pipeline's first list (ev_pre) is band work, run before the statistics
+    if (n_pre > 0)
+        HIPCHK(nldsc::launch_issued_products(e->items.p, n_pre, nullptr, 0, nullptr, e->blk_miss.p, nblk, path, dom, 0,
+                                             route_shift, e->sums.p + 2, st));
+    // stage times: with the count overlap the band runs from its first round's start (during the count) to ev[4]
     auto stage_ms = [&]() -> int {
-        float f = 0, pre = 0;
-        if (cfree && n_pre > 0) HIPCHK(hipEventElapsedTime(&pre, e->ev_pre[0], e->ev_pre[1]));
+        float f = 0;
         HIPCHK(hipEventElapsedTime(&f, e->ev[0], e->ev[1])); e->ms[0] = f;
-        HIPCHK(hipEventElapsedTime(&f, e->ev[1], e->ev[2])); e->ms[1] = f - pre;
-        HIPCHK(hipEventElapsedTime(&f, e->ev[3], e->ev[4])); e->ms[3] = f + pre;
+        HIPCHK(hipEventElapsedTime(&f, e->ev[1], e->ev[2])); e->ms[1] = f;
+        HIPCHK(hipEventElapsedTime(&f, n_pre > 0 ? e->ev_pre[0] : e->ev[3], e->ev[4])); e->ms[3] = f;
         return NLDSC_OK;
     };
     if (split) {  // the right halo's sums out; finalize waits for the left neighbour's (run_device_finish)
@@ -1329,7 +1279,7 @@ int nldsc_engine_ksplit(const nldsc_engine* e) { return e ? e->last_ksplit : NLD
 int nldsc_engine_band_round_items(const nldsc_engine* e) { return e ? e->last_round_items : NLDSC_E_ARG; }
 int nldsc_engine_band_tail_ksplit(const nldsc_engine* e) { return e ? e->last_tail_ksplit : NLDSC_E_ARG; }
 int nldsc_engine_band_kernel(const nldsc_engine* e) { return e ? e->last_band_kernel : NLDSC_E_ARG; }
-int nldsc_engine_count_free(const nldsc_engine* e) { return e ? (e->last_count_free ? 1 : 0) : NLDSC_E_ARG; }
+int nldsc_engine_count_overlap(const nldsc_engine* e) { return e ? (e->last_overlap ? 1 : 0) : NLDSC_E_ARG; }
 
 int nldsc_ld_calculate(const nldsc_ld_params* p, nldsc_ld_result* r, char* err, size_t errlen) {
     if (!p || !r || !p->bedfile) return set_err(err, errlen, NLDSC_E_ARG, "NULL argument");

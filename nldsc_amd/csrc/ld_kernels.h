@@ -80,7 +80,7 @@ hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const doubl
 // reaches it), then plan_emit writes the items (16 row blocks x 16 offsets tile order).  pair: items of two
 // neighbouring column blocks (I, J, 2) (the additive-only fp4 kernel's 32 x 64 tiles; a row's odd last one (I, J, 1))
 hipError_t launch_plan(const double* pos, int n, double w, int own_lo, int own_hi, int* A, int* E, int* R,
-                       int2* rows, int* counts, int* meta, hipStream_t st, bool pair = false, bool skip_diag = false);
+                       int2* rows, int* counts, int* meta, hipStream_t st, bool pair = false);
 hipError_t launch_plan_emit(int n, const int2* rows, const int* meta, const int* offsets, int4* items, hipStream_t st,
                             bool pair = false);
 hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int pitch_words, int n_it,
@@ -116,13 +116,9 @@ hipError_t launch_band_f4_deferred_epi(bool dom, int max_items, const SnpConst* 
                                       int* ws_acc, const uint8_t* blk_rep, hipStream_t st);
 // the same with the K loop split in P pieces (small launches: better filled wave slots): partial Gram tiles to
 // `gram` (n_items * P * 8192 floats), then an epilogue kernel (unsegmented rows, n_it <= F4_SEG_CHUNKS)
-// Count-free pipeline (fp4, GPU plan, see ld_engine.cpp): the tail chunks of every row rebuilt for this run's sample
-// order without counting; the diagonal items (I, I, 1, 0) of every block; the genotype counts of every SNP from the
-// diagonal items' Gram tiles (the first nblk items of a launch_band_f4_parts list, P pieces each).
+// Count overlap (ld_engine.cpp): the tail chunks of every row rebuilt for this run's sample order, without counting.
 hipError_t launch_tail_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
                             uint32_t pad, hipStream_t st);
-hipError_t launch_diag_items(int nblk, int4* out, hipStream_t st);
-hipError_t launch_diag_counts(const float* gram, int P, int n_snp, int n_org, int* counts, hipStream_t st);
 // The K loops of a list of single block pairs (P pieces each, launches of round_items items, 0: one launch), their
 // exact Gram tiles stored to gram (8192 floats per item and piece) — before the statistics: the missing-call
 // predicate comes from blk_flags (blk_miss of this run's order); later launch_band_f4_epis runs their epilogues

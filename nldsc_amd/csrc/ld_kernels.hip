@@ -317,9 +317,9 @@ __global__ void __launch_bounds__(256) count_rows_kernel(uint8_t* __restrict__ i
     }
 }
 
-// The count-free pipeline (fp4 path, GPU plan; ld_engine.cpp): no per-run count pass over the rows.  Per run only the
-// tail chunks are rebuilt for this run's sample order (what count_rows_kernel does besides counting): the last byte
-// keeps the bit pairs that are individuals, the rest and the pitch padding take the pad code.  One thread per
+// The count overlap (ld_engine.cpp): the band's first round reads the rows while count_rows_kernel runs, so the tail
+// chunks are rebuilt for this run's sample order first (what count_rows_kernel does besides counting, the same bytes):
+// the last byte keeps the bit pairs that are individuals, the rest and the pitch padding take the pad code.  One thread per
 // (row, 16-byte half of its 32-byte piece of a chunk).
 __global__ void __launch_bounds__(256) tail_rows_kernel(uint8_t* __restrict__ img, const uint8_t* __restrict__ last,
                                                         int n_snp, int nb, int row_bytes, uint32_t tail_keep,
@@ -346,39 +346,6 @@ __global__ void __launch_bounds__(256) tail_rows_kernel(uint8_t* __restrict__ im
         }
         *unit = make_uint4(wd[0], wd[1], wd[2], wd[3]);
     }
-}
-
-// the diagonal block pairs (I, I) of every block, the head of the count-free pipeline's first list
-__global__ void diag_items_kernel(int nblk, int4* __restrict__ out) {
-    const int I = blockIdx.x * blockDim.x + threadIdx.x;
-    if (I < nblk) out[I] = make_int4(I, I, 1, 0);
-}
-
-// Genotype counts from the diagonal Gram tiles (band_f4_part_kernel, P pieces per item, the diagonal items first in
-// the list): with v = m + 2x (the e2m1 operand of the raw code: 0, 1 missing, 2 het, 4 hom A2 of the stored coding)
-// and h = [x >= 1], SNP j's own entries are v.v = n_miss + 4 c1 + 16 c2, v.m = n_miss and v.h = 2 c1 + 4 c2 (exact
-// integers; m = 0 on the non-individual slots, which hold code 00), so c2 = ((v.v - v.m) / 4 - v.h / 2) / 2,
-// c1 = v.h / 2 - 2 c2, c0 = n_org - n_miss - c1 - c2 — what count_rows_kernel counts, in the stored coding.  Lane
-// (i, h) register r of a tile holds (row (r & 3) + 8 (r >> 2) + 4 h, column i): entry (j, j) is lane j + 32 ((j >> 2)
-// & 1), register (j & 3) + 4 (j >> 3).
-__global__ void diag_counts_kernel(const float* __restrict__ gram, int P, int n_snp, int n_org,
-                                   int* __restrict__ counts) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n_snp) return;
-    const int I = j >> 5, i = j & 31, lane = i + 32 * ((i >> 2) & 1), r = (i & 3) + 4 * (i >> 3);
-    long long vv = 0, vm = 0, vh = 0;
-    for (int p = 0; p < P; ++p) {
-        const float* t = gram + ((size_t)I * P + p) * 8192 + lane * 16 + r;
-        vv += (long long)t[0];
-        vm += (long long)t[1024];
-        vh += (long long)t[4 * 1024];
-    }
-    const long long a = (vv - vm) / 4, b = vh / 2;  // c1 + 4 c2, c1 + 2 c2
-    const long long c2 = (a - b) / 2, c1 = b - 2 * c2;
-    counts[4 * (size_t)j] = (int)((long long)n_org - vm - c1 - c2);
-    counts[4 * (size_t)j + 1] = (int)c1;
-    counts[4 * (size_t)j + 2] = (int)c2;
-    counts[4 * (size_t)j + 3] = 0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -846,9 +813,8 @@ __global__ void __launch_bounds__(1024) plan_right_kernel(const int* __restrict_
 
 // per row block I: useful column offsets d = J - I, [d0, d1] (empty: d0 > d1); meta[0] = max d1 + 1,
 // meta[2] = diagonal items
-// skip_diag (the count-free pipeline, which runs every diagonal block pair in its own list): offsets from 1
 __global__ void plan_rows_kernel(const int* __restrict__ E, const int* __restrict__ A, int n, int nblk, int own_lo,
-                                 int own_hi, int2* __restrict__ rows, int* __restrict__ meta, int skip_diag) {
+                                 int own_hi, int2* __restrict__ rows, int* __restrict__ meta) {
     const int I = blockIdx.x * blockDim.x + threadIdx.x;
     if (I >= nblk) return;
     int2 r = make_int2(1, 0);
@@ -858,7 +824,7 @@ __global__ void plan_rows_kernel(const int* __restrict__ E, const int* __restric
         const int ob0 = own_lo / 32, ob1 = (own_hi - 1) / 32;
         const bool own_row = I >= ob0 && I <= ob1;
         const int J0 = own_row ? I : max(I, ob0), J1 = own_row ? Jmax : min(Jmax, ob1);
-        r = make_int2(max(J0 - I, skip_diag), J1 - I);
+        r = make_int2(J0 - I, J1 - I);
     }
     rows[I] = r;
     if (r.x <= r.y) {
@@ -1724,8 +1690,8 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     // wave-uniform: does the row block / do the column blocks hold a missing call (flag bit 2)?  With PART this
     // is the only SNP state used (sh.cst and the other flag bits may be rewritten by a concurrent replay:
     // launch_reference_residuals in ld_kernels.h)
-    // (blk_flags: the per-block missing flags of this run's sample order, blk_miss — the count-free pipeline's
-    // partial K loops run before the statistics that set flag bit 2)
+    // (blk_flags: the per-block missing flags of this run's sample order, blk_miss — the count overlap's partial K
+    // loops run before the statistics that set flag bit 2)
     const bool rm = blk_flags != nullptr ? blk_flags[I] != 0 : __any(lane < 32 && (sh.info[lane].fl & 4));
     const bool cm = blk_flags != nullptr ? blk_flags[J0] != 0 : __any(32 + lane < NS && (sh.info[32 + lane].fl & 4));
     auto run = [&](const int t_lo, const int t_hi) {
@@ -2449,14 +2415,7 @@ __global__ void __launch_bounds__(64, 2) band_f4_part_kernel(const uint32_t* __r
     band_f4_body<DOM, 1, DIAG_, 0, false, true>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp,     \
                                                 0.0, 0.0, 0.0, 0, 0, nullptr, nullptr, nullptr, tr, t_lo, t_hi, part, \
                                                 blk_flags)
-    // (count-free pipeline, blk_flags set: a diagonal item computes v.h even in additive-only runs, for the counts)
-    if (it.y == it.x) {
-        if (!DOM && blk_flags != nullptr)
-            band_f4_body<true, 1, true, 0, false, true>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp,
-                                                        0.0, 0.0, 0.0, 0, 0, nullptr, nullptr, nullptr, tr, t_lo, t_hi,
-                                                        part, blk_flags);
-        else NLDSC_BODY(true);
-    } else NLDSC_BODY(false);
+    if (it.y == it.x) NLDSC_BODY(true); else NLDSC_BODY(false);
 #undef NLDSC_BODY
 }
 
@@ -2760,14 +2719,14 @@ hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const doubl
 }
 
 hipError_t launch_plan(const double* pos, int n, double w, int own_lo, int own_hi, int* A, int* E, int* R,
-                       int2* rows, int* counts, int* meta, hipStream_t st, bool pair, bool skip_diag) {
+                       int2* rows, int* counts, int* meta, hipStream_t st, bool pair) {
     const int nblk = (n + 31) / 32;
     hipError_t e = hipMemsetAsync(meta, 0, 4 * sizeof(int), st);
     if (e != hipSuccess || n <= 0 || own_hi <= own_lo) return e;
     hipLaunchKernelGGL(plan_edges_kernel, dim3((n + 255) / 256), dim3(256), 0, st, pos, n, w, A, E);
     hipLaunchKernelGGL(plan_right_kernel, dim3(1), dim3(1024), 0, st, E, n, R);
     hipLaunchKernelGGL(plan_rows_kernel, dim3((nblk + 255) / 256), dim3(256), 0, st, E, A, n, nblk, own_lo, own_hi,
-                       rows, meta, skip_diag ? 1 : 0);
+                       rows, meta);
     hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, counts, pair ? 1 : 0);
     hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts, nblk, meta);
     return hipGetLastError();
@@ -2911,18 +2870,6 @@ hipError_t launch_tail_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb
     if (n_snp <= 0) return hipSuccess;
     hipLaunchKernelGGL(tail_rows_kernel, dim3((2 * n_snp + 255) / 256), dim3(256), 0, st, img, last, n_snp, nb, row_bytes,
                        tail_keep, pad);
-    return hipGetLastError();
-}
-
-hipError_t launch_diag_items(int nblk, int4* out, hipStream_t st) {
-    if (nblk <= 0) return hipSuccess;
-    hipLaunchKernelGGL(diag_items_kernel, dim3((nblk + 255) / 256), dim3(256), 0, st, nblk, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_diag_counts(const float* gram, int P, int n_snp, int n_org, int* counts, hipStream_t st) {
-    if (n_snp <= 0) return hipSuccess;
-    hipLaunchKernelGGL(diag_counts_kernel, dim3((n_snp + 255) / 256), dim3(256), 0, st, gram, P, n_snp, n_org, counts);
     return hipGetLastError();
 }
 

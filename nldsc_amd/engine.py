@@ -167,8 +167,8 @@ class Engine:
                                    if hasattr(self._L, "nldsc_engine_band_round_items") else 0),
                  band_tail_ksplit=(self._L.nldsc_engine_band_tail_ksplit(self._h)
                                    if hasattr(self._L, "nldsc_engine_band_tail_ksplit") else 1),
-                count_free=(bool(self._L.nldsc_engine_count_free(self._h))
-                            if hasattr(self._L, "nldsc_engine_count_free") else False))
+                count_overlap=(bool(self._L.nldsc_engine_count_overlap(self._h))
+                               if hasattr(self._L, "nldsc_engine_count_overlap") else False))
         return d
 
 

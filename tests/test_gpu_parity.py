@@ -1147,36 +1147,36 @@ def test_deferred_rare_items_capped_on_wide_bands_with_missing_calls(engine):
     assert_ld_close(sub, exp, label="wide band, missing calls, replayed rare variants vs oracle")
 
 
-COUNT_FREE_CASES = {
-    # (N, M, length cM, dom, flags, own, rare): rows of >= 2^17 samples (the count-free regime)
-    "rounds_fill": (315_599, 12_000, 15.0, True, (), None, False),       # one round: 375 diagonal + filling items
-    "rounds_prelaunch": (131_101, 70_000, 88.0, True, (), None, False),  # 2 188 blocks: a diagonal round before the plan
-    "additive_pairs": (131_101, 12_000, 15.0, False, ("FLAG_ADDITIVE_ONLY",), None, False),
-    "ksplit_whole": (131_101, 1_500, 2.0, True, (), None, False),        # a small band: every K loop before the stats
-    "owned_shard": (315_599, 12_000, 15.0, True, (), (4_000, 5_500), False),
-    "strict_order": (131_101, 12_000, 15.0, True, ("FLAG_STRICT_PLINK_ORDER",), None, False),
-    "rare_replay": (315_599, 12_000, 15.0, True, (), None, True),
+COUNT_OVERLAP_CASES = {
+    # (N, M, length cM, dom, flags, own, rare, env, overlap): rows of >= 2^17 samples, round launches
+    "rounds_c3_rows": (315_599, 12_000, 15.0, True, (), None, False, {}, True),
+    "rounds_n131k": (131_101, 12_000, 15.0, True, (), None, False, {}, True),
+    "strict_order": (131_101, 12_000, 15.0, True, ("FLAG_STRICT_PLINK_ORDER",), None, False, {}, True),
+    "rare_replay": (315_599, 12_000, 15.0, True, (), None, True, {}, True),
+    # additive-only single block pairs overlap; column-block pairs (the default) take no partial kernel
+    "additive_single": (131_101, 12_000, 15.0, False, ("FLAG_ADDITIVE_ONLY",), None, False, {"NLDSC_F4_NC2": "0"}, True),
+    "additive_pairs": (131_101, 12_000, 15.0, False, ("FLAG_ADDITIVE_ONLY",), None, False, {}, False),
+    # an owned sub-range too small for two rounds: no overlap
+    "owned_shard": (315_599, 12_000, 15.0, True, (), (4_000, 5_500), False, {}, False),
 }
 
 
-@pytest.mark.parametrize("case", sorted(COUNT_FREE_CASES))
-def test_count_free_pipeline_bitwise_count_pass(engine, case):
-    """The count-free pipeline (the default for fp4 runs on rows of >= 2^17 samples without missing-free blocks): no
-    per-run count pass; the diagonal block pairs run first, their exact Gram tiles give the genotype counts (v.v, v.m,
-    v.h on the diagonal), then the statistics and the band.  Every output is bitwise the count-pass run
-    ($NLDSC_COUNT_FREE=0) — round launches with the diagonal items' last round filled by off-diagonal items, the first
-    diagonal rounds launched beside the plan, additive-only column-block pairs, a small band K-split whole, an owned
-    sub-range, PLINK's sample order, replayed rare variants — and a few SNPs equal the exact truth."""
+@pytest.mark.parametrize("case", sorted(COUNT_OVERLAP_CASES))
+def test_count_overlap_bitwise_serial(engine, case):
+    """The count overlap (the default for fp4 round launches on rows of >= 2^17 samples without missing-free blocks):
+    the band's first round runs its K loops on a second stream beside the per-run count pass, storing exact Gram tiles,
+    and its epilogues run after the rest of the band.  Every output is bitwise the serial run ($NLDSC_COUNT_OVERLAP=0),
+    including PLINK's sample order and replayed rare variants, and a few SNPs equal the exact truth."""
     import torch
     from nldsc_amd import synth
     from nldsc_amd.engine import Engine
-    N, M, length, dom, fl, own, rare = COUNT_FREE_CASES[case]
+    N, M, length, dom, fl, own, rare, env, overlap = COUNT_OVERLAP_CASES[case]
     buf, pos = synth.device_bed(M, N, seed=M + 7, length_cm=length, missing=0.01)
-    if rare:  # rare variants (<= 16 calls in a genotype class: replayed) mid-band and in the last blocks
+    if rare:  # rare variants (<= 16 calls in a genotype class: replayed) in the first round's blocks and later
         img = buf.cpu().numpy().copy()
         rows = img[3:].reshape(M, (N + 3) // 4)
         rng = np.random.default_rng(5)
-        for j in (300, 6001, M - 40, M - 1):
+        for j in (3, 300, 6001, M - 40, M - 1):
             g = np.zeros(N, np.int8)
             pick = rng.choice(N, 108, replace=False)
             g[pick[:100]], g[pick[100:]] = 1, 2
@@ -1188,18 +1188,23 @@ def test_count_free_pipeline_bitwise_count_pass(engine, case):
         flags |= _lib_flag(f)
     args = (1.0, 1e-4, 1e-5, 1.0 / M, pos)
 
-    def fresh(cfree):
+    def fresh(expect):
         with Engine(0) as e:
             e.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
             r = e.run(*args, flags=flags, own=own)
             t = e.timings()
-            assert t["count_free"] == cfree, t
+            assert t["count_overlap"] == expect, t
             return r, t
-    got, tg = fresh(True)
-    ref, tr = _env_run("NLDSC_COUNT_FREE", "0", lambda: fresh(False))
+
+    def both():
+        return fresh(overlap), _env_run("NLDSC_COUNT_OVERLAP", "0", lambda: fresh(False))
+    run = both
+    for var, value in env.items():
+        run = (lambda f, v, x: (lambda: _env_run(v, x, f)))(run, var, value)
+    (got, tg), (ref, tr) = run()
     for k in got:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{case} {k}")
-    assert tg["pairs"] == tr["pairs"] and tg["flop_alg"] == tr["flop_alg"]
+    assert tg["pairs"] == tr["pairs"] and tg["flop_issued"] == tr["flop_issued"], (tg, tr)
     if rare:
         return
     lo, hi = own or (0, M)
@@ -1213,4 +1218,4 @@ def test_count_free_pipeline_bitwise_count_pass(engine, case):
         exp = dict(exp, l2d=np.full(len(t), np.nan), l2d_ws=np.full(len(t), -1, np.int32),
                    l2d_wse=np.full(len(t), -1, np.int32))
     assert_ld_close(sub, exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
-                                       maf=(0.0, 0.0)), label=f"count-free {case}")
+                                       maf=(0.0, 0.0)), label=f"count overlap {case}")

@@ -84,6 +84,7 @@ def main():
     ap.add_argument("--dir", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "nldsc_genome"))
     ap.add_argument("--out", default=None)
     ap.add_argument("--keep", action="store_true", help="keep the files afterwards")
+    ap.add_argument("--fit", action="store_true", help="run the largest prefix of the chromosomes that fits the disk")
     a = ap.parse_args()
     import torch
     from nldsc_amd.engine import Engine
@@ -99,6 +100,11 @@ def main():
         chroms = [(c, a.n_snp, 70.0) for c in range(1, a.chroms + 1)]
     need = sum(3 + M * nb for _, M, _ in chroms)
     du = shutil.disk_usage(a.dir)
+    full_bytes = need
+    if a.fit:  # the largest prefix of the autosomes that fits the disk (leaving 4 GB), scaled to all of them by bytes
+        while len(chroms) > 1 and need > du.free - (4 << 30):
+            chroms = chroms[:-1]
+            need = sum(3 + M * nb for _, M, _ in chroms)
     doc = dict(workload=("C4 (BASELINE.json configs[3]): %d autosomes, M_c proportional to cM length (sum M=%d), N=%d, "
                          "--ld-wind-cm 1, additive+dominance, %g%% missing" %
                          (len(chroms), sum(m for _, m, _ in chroms), N, 100 * a.missing)),
@@ -176,6 +182,11 @@ def main():
              "share one host disk, so the cold projection is max(LPT, all bytes / the measured cold read rate)")
     doc["projection_8gpu"]["cold_s"] = max(doc["projection_8gpu"]["lpt_max_rank_s"],
                                            doc["projection_8gpu"]["disk_bound_s"])
+    if need < full_bytes:  # a prefix ran: every time scaled by bytes to the whole set
+        f = full_bytes / need
+        doc["scaled_to_all"] = dict(factor=round(f, 4), bed_bytes=full_bytes, cli_cold_s=round(doc["cli_cold_s"] * f, 3),
+                                    cli_warm_s=round(doc["cli_warm_s"] * f, 3),
+                                    projection_8gpu_cold_s=round(doc["projection_8gpu"]["cold_s"] * f, 3))
     print(json.dumps(doc), flush=True)
     if a.out:
         json.dump(doc, open(a.out, "w"), indent=1)
