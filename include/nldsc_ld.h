@@ -172,10 +172,6 @@ int nldsc_engine_band_tail_ksplit(const nldsc_engine* e);
 #define NLDSC_BAND_F4_QUAD 7 /* $NLDSC_T2=3: missing-free 4x4 super-items in the quad workgroups (64x64 tiles per
                                 wave), the rest in the single-block kernel */
 int nldsc_engine_band_kernel(const nldsc_engine* e);
-/* 1 when the last run overlapped the per-run genotype count with the band's first round (fp4 round launches on the GPU
- * plan, no missing-free block): that round's K loops ran beside the count pass and its epilogues after the rest of the
- * band ($NLDSC_COUNT_OVERLAP=0 turns it off); 0 otherwise.  The results are bitwise the same either way. */
-int nldsc_engine_count_overlap(const nldsc_engine* e);
 
 /* Load SNP rows [snp_begin, snp_end) of a .bed file of n_snp_file SNPs as the engine's image
  * (snp_end - snp_begin SNPs; the run then takes the positions of that slice).  Position sharding

@@ -32,7 +32,7 @@ EXPORTED = (
     "nldsc_synth_bed_device", "nldsc_engine_path", "nldsc_plan_band", "nldsc_engine_load_bed_file_range",
     "nldsc_format_scores", "nldsc_engine_ksplit", "nldsc_engine_band_kernel", "nldsc_engine_band_round_items",
     "nldsc_engine_band_tail_ksplit", "nldsc_engine_run_device", "nldsc_engine_run_device_split",
-    "nldsc_engine_run_device_finish", "nldsc_engine_count_overlap",
+    "nldsc_engine_run_device_finish",
 )
 
 
@@ -104,8 +104,6 @@ def lib(path: str | None = None) -> ctypes.CDLL:
             L.nldsc_engine_band_round_items.argtypes = [vp]
         if hasattr(L, "nldsc_engine_band_tail_ksplit"):
             L.nldsc_engine_band_tail_ksplit.argtypes = [vp]
-        if hasattr(L, "nldsc_engine_count_overlap"):
-            L.nldsc_engine_count_overlap.argtypes = [vp]
         if hasattr(L, "nldsc_engine_run_device"):
             L.nldsc_engine_run_device.argtypes = [vp, ctypes.POINTER(Params), ctypes.c_int32, ctypes.c_int32, vp,
                                                   ctypes.c_int32] + c_err

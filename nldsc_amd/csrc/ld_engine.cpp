@@ -117,10 +117,6 @@ struct nldsc_engine {
     hipEvent_t ev_pos = nullptr;        // positions uploaded (the schedule's only input)
     hipEvent_t ev[6] = {};
     hipEvent_t ev_dbg[2] = {};  // $NLDSC_DEBUG_TIMING: after the super-item launch, before the single-block launches
-    // the count overlap (run_impl): the first round's K loops on aux_stream (start, end); the rows' tails rewritten
-    hipEvent_t ev_pre[2] = {};
-    hipEvent_t ev_tail = nullptr;
-    hipStream_t aux_stream = nullptr;
     bool debug_timing = false;
     hipEvent_t ev_plan = nullptr;  // GPU plan counters landed in h_meta
     hipEvent_t ev_stats = nullptr;   // SNP constants and replay flags written (the replay's inputs)
@@ -193,14 +189,6 @@ struct nldsc_engine {
     // 351 -> 333 ms, C3 missing-free (6 rounds, below the threshold) 12.34 -> 12.51 ms (profiles/r03_ab_q_rounds.json)
     bool q_rounds = true;
     int last_band_kernel = NLDSC_BAND_F4;
-    // Count overlap ($NLDSC_COUNT_OVERLAP=0: off): fp4 round launches on the GPU plan with no super-item routing run the
-    // first round's K loops on aux_stream beside the per-run count pass, their Gram tiles stored (see run_impl).
-    // free_blocks[order]: 32-SNP blocks without a missing call among the individual slots of sample order `order`
-    // (row_miss, at load) — super-item routing needs such blocks.
-    bool count_overlap = true;
-    int free_blocks[2] = {0, 0};
-    bool last_overlap = false;
-    DevBuf<float> pre_gram;  // the first round's Gram tiles
     DevBuf<double> pos, l2_acc, l2d_acc;
     DevBuf<int4> items;
     // host scratch
@@ -236,12 +224,8 @@ struct nldsc_engine {
         bed.release(); stage_dev.release(); lastb.release(); flip.release(); row_miss.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
         res.release(); lut.release(); cst.release(); sflags.release(); pos.release();
         l2_acc.release(); l2d_acc.release(); items.release(); gram.release();
-        rep_gram.release(); rep_items.release(); rep_count.release(); pre_gram.release();
+        rep_gram.release(); rep_items.release(); rep_count.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
-        for (auto& e : ev_dbg) if (e) (void)hipEventDestroy(e);
-        for (auto& e : ev_pre) if (e) (void)hipEventDestroy(e);
-        if (ev_tail) (void)hipEventDestroy(ev_tail);
-        if (aux_stream) (void)hipStreamDestroy(aux_stream);
         if (ev_plan) (void)hipEventDestroy(ev_plan);
         Ew.release(); plan_counts.release(); plan_meta.release(); plan_rows.release();
         plan_counts2.release(); plan_rows2.release(); items2.release(); blk_miss.release(); blk_zero.release(); sums.release();
@@ -316,16 +300,6 @@ hipError_t finish_image(nldsc_engine* e, int32_t n_snp, int32_t n_org) {
         he = nldsc::launch_row_missing(e->bed.p, e->lastb.p, n_snp, nb, row_pitch(n_org), keep_compat, keep_strict,
                                        e->row_miss.p, e->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
-    if (he == hipSuccess) {  // missing-free blocks per sample order (the count-free pipeline runs without any)
-        std::vector<uint8_t> rm((size_t)n_snp);
-        he = hipMemcpy(rm.data(), e->row_miss.p, (size_t)n_snp, hipMemcpyDeviceToHost);
-        e->free_blocks[0] = e->free_blocks[1] = 0;
-        for (int32_t b = 0; he == hipSuccess && b < (n_snp + 31) / 32; ++b) {
-            uint8_t m = 0;
-            for (int32_t j = 32 * b; j < std::min(n_snp, 32 * b + 32); ++j) m |= rm[(size_t)j];
-            for (int o = 0; o < 2; ++o) e->free_blocks[o] += ((m >> o) & 1) ? 0 : 1;
-        }
-    }
     if (he == hipSuccess) {
         e->n_snp = n_snp;
         e->n_org = n_org;
@@ -367,7 +341,6 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (const char* v = std::getenv("NLDSC_QUAD_ADD")) e->quad_add = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_Q_ROUNDS")) e->q_rounds = std::atoi(v) != 0;
     if (const char* v = std::getenv("NLDSC_DEFER_REP")) e->defer_rep = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_COUNT_OVERLAP")) e->count_overlap = std::atoi(v) != 0;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
@@ -375,8 +348,6 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     }
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->plan_stream, hipStreamNonBlocking);
-    if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->aux_stream, hipStreamNonBlocking);
-    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_tail, hipEventDisableTiming);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_pos, hipEventDisableTiming);
     for (auto& ev : e->ev)
         if (he == hipSuccess) he = hipEventCreate(&ev);
@@ -385,8 +356,6 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_replay, hipEventDisableTiming);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_route, hipEventDisableTiming);
     for (auto& ev : e->ev_dbg)
-        if (he == hipSuccess) he = hipEventCreate(&ev);
-    for (auto& ev : e->ev_pre)
         if (he == hipSuccess) he = hipEventCreate(&ev);
     if (he != hipSuccess) {
         delete e;
@@ -677,17 +646,8 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     const bool sorted = nldsc::positions_sorted(p->positions, M);
     const bool gpu_plan = e->gpu_plan && sorted && max_nc == 1 &&
                           std::all_of(p->positions, p->positions + M, [](double x) { return x >= 0.0; });
-    const int order = strict ? 1 : 0;  // bit of row_miss: the individual slots of this run's sample order
-    // Count overlap (fp4 round launches on the GPU plan, no super-item routing — the data has no missing-free block in
-    // this order, or the super-item kernels are off): the count pass is HBM-bound (C3: 0.96 ms at 6.7 TB/s), the band
-    // MFMA-bound, and only the band's epilogues need the statistics.  So the first round of the band runs its K loops
-    // on aux_stream beside the count, storing its exact Gram tiles (launch_band_f4_parts); its epilogues run after the
-    // rest of the band (launch_band_f4_epis).  Bitwise the serial order's results (exact tiles, fixed-point sums).
-    const bool ovl = e->count_overlap && gpu_plan && use_f4 && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 1024 &&
-                     e->band_rounds && (e->t2_mode == 0 || e->free_blocks[order] == 0) &&
-                     !(e->t2_mode == 3 && !dom && e->quad_add);
     // the 2 x 2 block-pair workgroups: fp4, unsegmented rows, GPU plan, and no K-split (choose_ksplit below)
-    const bool t2_cand = !ovl && e->t2_mode > 0 && gpu_plan && use_f4 && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 2;
+    const bool t2_cand = e->t2_mode > 0 && gpu_plan && use_f4 && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 2;
     // additive-only fp4 items of two column blocks (GPU plan, unsegmented rows; no K-split: its partial kernel takes
     // single block pairs)
     const bool nc2 = e->f4_nc2 && gpu_plan && use_f4 && !dom && n_it <= nldsc::F4_SEG_CHUNKS;
@@ -702,10 +662,9 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // Model: a round of items takes ~0.67 us per K chunk (C3: 2 466 chunks, 1.65 ms per round, 12.7 rounds in
     // 20.9 ms); the split adds ~64 KiB of partial-tile traffic per piece at ~3 TB/s effective (measured: a 1/8
     // shard of C3, 3 300 items, band 3.35 -> 3.01 ms; a 1/2 shard, 13 000 items, P = 5 made it 7.5 % slower).
-    // (singles: the list holds single block pairs only, e.g. the count-free pipeline's first list)
-    auto choose_ksplit = [&](int n_items, bool singles = false) {
+    auto choose_ksplit = [&](int n_items) {
         int ksplit = 1;
-        if (use_f4 && (!nc2 || singles) && n_items > 0 && n_it <= nldsc::F4_SEG_CHUNKS && e->ksplit_ok) {
+        if (use_f4 && !nc2 && n_items > 0 && n_it <= nldsc::F4_SEG_CHUNKS && e->ksplit_ok) {
             const double slots = 8.0 * (double)e->n_cu, t_round = 0.67e-6 * n_it;
             auto cost = [&](int P) {
                 return std::ceil((double)n_items * P / slots) / P * t_round +
@@ -732,9 +691,9 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         HIPCHK(e->plan_meta.ensure(8));  // [0, 4) single-block plan, [4, 8) super-item plan
         HIPCHK(e->h_meta.ensure(8 * sizeof(int)));
         if (t2_cand) {
-            const size_t nblk2 = (size_t)(nblk + 1) / 2, n_t2 = (nblk2 + 15) / 16;
+            const size_t nblk2 = (size_t)(nblk + 1) / 2;
             HIPCHK(e->plan_rows2.ensure(nblk2));
-            HIPCHK(e->plan_counts2.ensure(n_t2 * n_t2));
+            HIPCHK(e->plan_counts2.ensure(nldsc::plan_super_tiles(nblk, route_shift)));
         }
     }
 
@@ -759,23 +718,15 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // non-individual slots read as missing (0x55) for the int8 / fp32 kernels, as 00 (all fp4 planes zero) for fp4
     const uint32_t pad = use_f4 ? 0x00u : 0x55u;
     const int n_pad00 = use_f4 ? 4 * row_bytes - N : 0;
-    const int slots = 8 * e->n_cu;  // wave slots: 2 per SIMD
-    // the count overlap's first round: items [0, n_pre) of the plan, their tiles in pre_gram
-    int n_pre = 0;
-    if (ovl) {  // the rows' tails first: the first round reads them while the count pass runs (it rewrites the same bytes)
-        HIPCHK(nldsc::launch_tail_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, pad, st));
-        HIPCHK(hipEventRecord(e->ev_tail, st));
-    }
     HIPCHK(nldsc::launch_count_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, pad, n_pad00, e->counts.p, st));
     HIPCHK(hipEventRecord(e->ev[1], st));
-    // rare variants: the reference's fp32 residual replayed (its sums assume N < 2^23); the flags per block in the
-    // statistics stage, the replay itself after the schedule (below)
-    const bool replay = N < (1 << 23) && !(p->flags & NLDSC_FLAG_EXACT_RARE);
-    auto stats_stage = [&]() -> int {
     HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->oriented ? e->flip.p : nullptr, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->cst.p,
                                    e->sflags.p, e->maf.p, e->rstd.p, st));
     // split runs: the pairs whose lower SNP is owned (flag bit 3), before the replay may touch the flags (ev_stats)
     if (split) HIPCHK(nldsc::launch_pair_range(e->sflags.p, M, own_begin, own_end, st));
+    // rare variants: the reference's fp32 residual replayed (its sums assume N < 2^23); the flags per block here,
+    // the replay itself after the schedule (below)
+    const bool replay = N < (1 << 23) && !(p->flags & NLDSC_FLAG_EXACT_RARE);
     // Invariant of the overlap: the replay rewrites, for replayed SNPs only, sflags bit 1 (residual pass; a byte
     // read-modify-write), cst and lut.  What runs beside it on the main stream reads sflags bits 0 (MAF pass:
     // left_pointer_kernel, the host flag copy) and 2 (missing calls: the band kernels' rm / cm), which the
@@ -788,22 +739,17 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         HIPCHK(hipEventRecord(e->ev_stats, st));
     }
     HIPCHK(hipEventRecord(e->ev[2], st));
-    return NLDSC_OK;
-    };
-    if (const int rc = stats_stage()) return rc;
 
     // ---- window replay + schedule ----
     auto t_host0 = std::chrono::steady_clock::now();
     int n_items = 0;
+    const int order = strict ? 1 : 0;  // bit of row_miss: the individual slots of this run's sample order
     bool compact = false;
     if (gpu_plan) {
         HIPCHK(hipEventSynchronize(e->ev_plan));  // the count kernel is running meanwhile
         const int* meta = reinterpret_cast<const int*>(e->h_meta.p);
         n_items = meta[1];
-        // count overlap: one round of items beside the count when the rest still fills round launches
-        // (single block pairs only: additive-only column-block pairs take no partial kernel)
-        if (ovl && !nc2 && n_items >= 2 * e->round_min * slots) n_pre = slots;
-        ksplit = n_pre > 0 ? 1 : choose_ksplit(n_items);
+        ksplit = choose_ksplit(n_items);
         // long rows: bands of at least round_min rounds of wave slots go in round launches (the last, partial round
         // K-split), not K-split whole — a 1/8 shard of C3 (1.6 rounds) band 2.70-2.76 -> 2.61-2.64 ms, a 1/4 shard
         // (3.2 rounds) 5.21-5.26 -> 4.87-4.89 ms (profiles/r03_ab_round_min.txt; was from 4 rounds on)
@@ -833,7 +779,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                 HIPCHK(nldsc::launch_plan_emit(M, e->plan_rows.p, e->plan_meta.p, e->plan_counts.p, e->items.p, ps,
                                                nc2));
         }
-        if (use_f4) {  // per 32-SNP block: holds a missing call (the m-product predicate: routing, issued count)
+        if (use_f4) {  // per 32-SNP block: holds a missing call (the kernels' m-product predicate: routing, issued count)
             HIPCHK(e->blk_miss.ensure((size_t)nblk));
             HIPCHK(nldsc::launch_block_missing_rows(e->row_miss.p, M, order, e->blk_miss.p, ps));
         }
@@ -855,16 +801,6 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         }
         HIPCHK(hipEventRecord(e->ev_route, ps));
         HIPCHK(hipStreamWaitEvent(st, e->ev_route, 0));  // left pointers / band read the schedule and the lists
-        if (n_pre > 0) {  // the first round's K loops beside the count (missing flags from blk_miss: no statistics yet)
-            hipStream_t as = e->aux_stream;
-            HIPCHK(e->pre_gram.ensure((size_t)n_pre * 8192));
-            HIPCHK(hipStreamWaitEvent(as, e->ev_route, 0));
-            HIPCHK(hipStreamWaitEvent(as, e->ev_tail, 0));
-            HIPCHK(hipEventRecord(e->ev_pre[0], as));
-            HIPCHK(nldsc::launch_band_f4_parts(dom, 1, n_pre, geno, pitch_words, n_it, e->cst.p, e->items.p, e->pos.p,
-                                               e->Lw.p, e->Rw.p, e->sflags.p, M, e->pre_gram.p, e->blk_miss.p, slots, as));
-            HIPCHK(hipEventRecord(e->ev_pre[1], as));
-        }
         HIPCHK(nldsc::launch_left_pointers(e->Aw.p, e->sflags.p, e->pos.p, M, e->Lw.p, st));
     } else {
     e->h_L.resize(M);
@@ -940,15 +876,15 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     HIPCHK(hipEventRecord(e->ev[3], st));
     e->n_band_items = n_items;
     e->last_ksplit = ksplit;
-    e->last_overlap = n_pre > 0;
     e->last_band_kernel = use_t2 ? (quad ? NLDSC_BAND_F4_QUAD : routed ? NLDSC_BAND_F4_ROUTED : NLDSC_BAND_F4_2X2) : !use_f4 ? (use_i8 ? NLDSC_BAND_I8 : NLDSC_BAND_F32)
                         : ksplit > 1 ? NLDSC_BAND_F4_KSPLIT : n_it > nldsc::F4_SEG_CHUNKS ? NLDSC_BAND_F4_SEG
                         : NLDSC_BAND_F4;
     if (ksplit > 1) HIPCHK(e->gram.ensure((size_t)n_items * ksplit * 8192));
+    const int slots = 8 * e->n_cu;
     // which = 1: the launch for the items without a replayed SNP (beside the replay), 2: the KC launch after it
     const uint8_t* blk_rep = replay ? e->blk_rep.p : nullptr;
-    int n_single = n_items - n_pre;    // single-block items (compacted when routed; after the count overlap's round)
-    const int4* single = e->items.p + n_pre;
+    int n_single = n_items;            // single-block items (compacted when routed)
+    const int4* single = e->items.p;
     int round_items = 0, tail_p = 1, n_full = 0;
     // Unsegmented single-block fp4 items go in launches of one round of the wave slots each (2 per SIMD): the items
     // of a launch start together and, all of equal length, stay at nearby K offsets, so the waves on one XCD that
@@ -1075,13 +1011,6 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         HIPCHK(size_single());
         if (replay) HIPCHK(hipStreamWaitEvent(st, e->ev_replay, 0));  // the fp32 path reads the replayed tables
     }
-    if (n_pre > 0) {  // the count overlap's round: its epilogues (after the replay when replaying: waited for above)
-        HIPCHK(hipStreamWaitEvent(st, e->ev_pre[1], 0));
-        HIPCHK(nldsc::launch_band_f4_epis(dom, 1, n_pre, e->cst.p, e->items.p, e->pos.p, e->Lw.p, e->Rw.p,
-                                          e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin, flush_hi,
-                                          e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, blk_rep, e->pre_gram.p,
-                                          replay ? 3 : 1, st));
-    }
     if (n_items > 0 && !use_f4 && !use_i8) {
         HIPCHK(nldsc::launch_band(dom, 2, n_items, geno, pitch_words, n_it,
                                       e->lut.p, e->items.p, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind,
@@ -1103,23 +1032,15 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                                              (use_t2 && quad_add ? 4 : 0),
                                          route_shift,
                                          e->sums.p + 2, st));
-    if (n_pre > 0)
-        HIPCHK(nldsc::launch_issued_products(e->items.p, n_pre, nullptr, 0, nullptr, e->blk_miss.p, nblk, path, dom, 0,
-                                             route_shift, e->sums.p + 2, st));
-    // stage times: with the count overlap the band runs from its first round's start (during the count) to ev[4]
-    auto stage_ms = [&]() -> int {
-        float f = 0;
-        HIPCHK(hipEventElapsedTime(&f, e->ev[0], e->ev[1])); e->ms[0] = f;
-        HIPCHK(hipEventElapsedTime(&f, e->ev[1], e->ev[2])); e->ms[1] = f;
-        HIPCHK(hipEventElapsedTime(&f, n_pre > 0 ? e->ev_pre[0] : e->ev[3], e->ev[4])); e->ms[3] = f;
-        return NLDSC_OK;
-    };
     if (split) {  // the right halo's sums out; finalize waits for the left neighbour's (run_device_finish)
         HIPCHK(nldsc::launch_export_acc(e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, own_end, M, export_dev, st));
         HIPCHK(hipStreamSynchronize(st));
         *export_n = M - own_end;
-        if (const int rc = stage_ms()) return rc;
+        float f = 0;
+        HIPCHK(hipEventElapsedTime(&f, e->ev[0], e->ev[1])); e->ms[0] = f;
+        HIPCHK(hipEventElapsedTime(&f, e->ev[1], e->ev[2])); e->ms[1] = f;
         e->ms[2] = std::chrono::duration<double, std::milli>(t_host1 - t_host0).count();
+        HIPCHK(hipEventElapsedTime(&f, e->ev[3], e->ev[4])); e->ms[3] = f;
         e->split_ms1 = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
         e->split_pending = true;
         e->split_M = M;
@@ -1175,8 +1096,10 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     auto t_end = std::chrono::steady_clock::now();
 
     float f = 0;
-    if (const int rc = stage_ms()) return rc;
+    HIPCHK(hipEventElapsedTime(&f, e->ev[0], e->ev[1])); e->ms[0] = f;
+    HIPCHK(hipEventElapsedTime(&f, e->ev[1], e->ev[2])); e->ms[1] = f;
     e->ms[2] = std::chrono::duration<double, std::milli>(t_host1 - t_host0).count();
+    HIPCHK(hipEventElapsedTime(&f, e->ev[3], e->ev[4])); e->ms[3] = f;
     HIPCHK(hipEventElapsedTime(&f, e->ev[4], e->ev[5])); e->ms[4] = f;
     e->ms[5] = std::chrono::duration<double, std::milli>(t_end - t_start).count();
     if (e->debug_timing) {  // where a run's wall time goes: GPU stages, the gap before the band, host tail
@@ -1279,7 +1202,6 @@ int nldsc_engine_ksplit(const nldsc_engine* e) { return e ? e->last_ksplit : NLD
 int nldsc_engine_band_round_items(const nldsc_engine* e) { return e ? e->last_round_items : NLDSC_E_ARG; }
 int nldsc_engine_band_tail_ksplit(const nldsc_engine* e) { return e ? e->last_tail_ksplit : NLDSC_E_ARG; }
 int nldsc_engine_band_kernel(const nldsc_engine* e) { return e ? e->last_band_kernel : NLDSC_E_ARG; }
-int nldsc_engine_count_overlap(const nldsc_engine* e) { return e ? (e->last_overlap ? 1 : 0) : NLDSC_E_ARG; }
 
 int nldsc_ld_calculate(const nldsc_ld_params* p, nldsc_ld_result* r, char* err, size_t errlen) {
     if (!p || !r || !p->bedfile) return set_err(err, errlen, NLDSC_E_ARG, "NULL argument");

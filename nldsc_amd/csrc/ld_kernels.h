@@ -116,21 +116,6 @@ hipError_t launch_band_f4_deferred_epi(bool dom, int max_items, const SnpConst* 
                                       int* ws_acc, const uint8_t* blk_rep, hipStream_t st);
 // the same with the K loop split in P pieces (small launches: better filled wave slots): partial Gram tiles to
 // `gram` (n_items * P * 8192 floats), then an epilogue kernel (unsegmented rows, n_it <= F4_SEG_CHUNKS)
-// Count overlap (ld_engine.cpp): the tail chunks of every row rebuilt for this run's sample order, without counting.
-hipError_t launch_tail_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
-                            uint32_t pad, hipStream_t st);
-// The K loops of a list of single block pairs (P pieces each, launches of round_items items, 0: one launch), their
-// exact Gram tiles stored to gram (8192 floats per item and piece) — before the statistics: the missing-call
-// predicate comes from blk_flags (blk_miss of this run's order); later launch_band_f4_epis runs their epilogues
-// (which: 1 the items without a replayed SNP, 2 the KC epilogues of those with one, after the replay).
-hipError_t launch_band_f4_parts(bool dom, int P, int n_items, const uint32_t* geno, int pitch_words, int n_it,
-                                const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
-                                const uint8_t* sflags, int n_snp, float* gram, const uint8_t* blk_flags,
-                                int round_items, hipStream_t st);
-hipError_t launch_band_f4_epis(bool dom, int P, int n_items, const SnpConst* cst, const int4* items, const double* pos,
-                               const int* Lw, const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind,
-                               double n_org, double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
-                               int* ws_acc, const uint8_t* blk_rep, const float* gram, int which, hipStream_t st);
 hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* geno, int pitch_words, int n_it,
                                 const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
                                 const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr,
@@ -143,6 +128,8 @@ hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* ge
 // block pairs the single-block plan does not hold
 constexpr int T2_STAGES = 4;  // LDS ring stages (2 chunks each) of band_f4_t2_kernel
 // shift 1: 2 x 2 super-items; shift 2: the quad kernel's 4 x 4 super-items
+// capacity of counts2 for launch_plan_super: the super-item plan's tiles (shift 2: 4 x 8 tiles of the (I, J) plane)
+size_t plan_super_tiles(int nblk, int shift);
 hipError_t launch_plan_super(int n, const int2* rows, int2* rows2, int* counts2, int* meta2, int shift, hipStream_t st);
 hipError_t launch_plan_emit_super(int n, const int2* rows2, const int* meta2, const int* offsets2, int4* items2,
                                   int shift, hipStream_t st);

@@ -317,37 +317,6 @@ __global__ void __launch_bounds__(256) count_rows_kernel(uint8_t* __restrict__ i
     }
 }
 
-// The count overlap (ld_engine.cpp): the band's first round reads the rows while count_rows_kernel runs, so the tail
-// chunks are rebuilt for this run's sample order first (what count_rows_kernel does besides counting, the same bytes):
-// the last byte keeps the bit pairs that are individuals, the rest and the pitch padding take the pad code.  One thread per
-// (row, 16-byte half of its 32-byte piece of a chunk).
-__global__ void __launch_bounds__(256) tail_rows_kernel(uint8_t* __restrict__ img, const uint8_t* __restrict__ last,
-                                                        int n_snp, int nb, int row_bytes, uint32_t tail_keep,
-                                                        uint32_t pad) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x, j = g >> 1, h = g & 1;
-    if (j >= n_snp) return;
-    const int n_ch = row_bytes >> 5, tc0 = (nb - 1) >> 5;
-    uint8_t* bbase = img + (size_t)(j >> 5) * 32 * (size_t)row_bytes;
-    const uint32_t lb = ((uint32_t)last[j] & tail_keep) | (pad & ~tail_keep & 0xFFu);
-    for (int tt = tc0; tt < n_ch; ++tt) {
-        uint4* unit = reinterpret_cast<uint4*>(bbase + (size_t)tt * 1024 + (size_t)(j & 31) * 32 + 16 * h);
-        const uint4 v = *unit;
-        uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            uint32_t o = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int p = 32 * tt + 16 * h + 4 * q + k;
-                const uint32_t byte = p < nb - 1 ? (wd[q] >> (8 * k)) & 0xFFu : p == nb - 1 ? lb : (pad & 0xFFu);
-                o |= byte << (8 * k);
-            }
-            wd[q] = o;
-        }
-        *unit = make_uint4(wd[0], wd[1], wd[2], wd[3]);
-    }
-}
-
 // ------------------------------------------------------------------------------------------
 // 2. per-SNP statistics -> lookup tables
 // ------------------------------------------------------------------------------------------
@@ -833,28 +802,48 @@ __global__ void plan_rows_kernel(const int* __restrict__ E, const int* __restric
     }
 }
 
-__device__ __forceinline__ int plan_n_c(const int* meta) { return (meta[0] + PLAN_C - 1) / PLAN_C; }
+// Tile geometry of an item order: tiles of R rows x C columns, the columns either diagonal offsets d = J - I
+// (abs_j 0: the band's rows read as a strip, the single-block plan) or absolute column blocks J (abs_j 1: tiles of the
+// (I, J) plane — the quad kernel's super-items, where one XCD's 32 workgroups of a round then share R row and C
+// column strips, 4 + 8 super-strips instead of 2 + 17 for 2 rows of a 16-offset tile).  Tiles in (T, c) order, items
+// row by row within a tile.
+struct TileGeo {
+    int R, C, abs_j;
+};
+constexpr TileGeo PLAN_GEO = {PLAN_R, PLAN_C, 0};
+constexpr TileGeo QUAD_GEO = {4, 8, 1};  // the quad kernel's 4 x 4 super-items (shift 2)
+inline TileGeo super_geo(int shift) { return shift == 2 ? QUAD_GEO : PLAN_GEO; }
+__device__ __forceinline__ int plan_n_c(const int* meta, TileGeo g) {
+    // abs_j: row group T spans columns [T R, T R + R - 1 + max d], i.e. at most (R - 2 + meta[0]) / C + 2 tiles
+    return g.abs_j ? (g.R + meta[0] + g.C - 2) / g.C + 1 : (meta[0] + g.C - 1) / g.C;
+}
+// the absolute columns of row I inside tile (T, c), intersected with its needed range [I + r.x, I + r.y]
+__device__ __forceinline__ int2 tile_span(int I, int2 r, int T, int c, TileGeo g) {
+    const int j0 = g.abs_j ? (T * g.R / g.C + c) * g.C : I + c * g.C;
+    return make_int2(max(I + r.x, j0), min(I + r.y, j0 + g.C - 1));
+}
 
-// per tile (T, c) of PLAN_R row blocks x PLAN_C offsets, in (T, c) order: its item count (pair: items of two
-// neighbouring column blocks, (I, J, 2), the last of a row's run in a tile possibly (I, J, 1))
+// per tile (T, c), in (T, c) order: its item count (pair: items of two neighbouring column blocks, (I, J, 2), the last
+// of a row's run in a tile possibly (I, J, 1))
 __global__ void plan_count_kernel(const int2* __restrict__ rows, int nblk, const int* __restrict__ meta,
-                                  int* __restrict__ counts, int pair) {
-    const int n_t = (nblk + PLAN_R - 1) / PLAN_R, n_c = plan_n_c(meta);
+                                  int* __restrict__ counts, int pair, TileGeo g) {
+    const int n_t = (nblk + g.R - 1) / g.R, n_c = plan_n_c(meta, g);
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n_t * n_c; k += gridDim.x * blockDim.x) {
         const int T = k / n_c, c = k % n_c;
         int cnt = 0;
-        for (int I = T * PLAN_R; I < min(nblk, T * PLAN_R + PLAN_R); ++I) {
-            const int a = max(rows[I].x, c * PLAN_C), b = min(rows[I].y, c * PLAN_C + PLAN_C - 1);
-            if (a <= b) cnt += pair ? (b - a + 2) / 2 : b - a + 1;
+        for (int I = T * g.R; I < min(nblk, T * g.R + g.R); ++I) {
+            const int2 ab = tile_span(I, rows[I], T, c, g);
+            if (ab.x <= ab.y) cnt += pair ? (ab.y - ab.x + 2) / 2 : ab.y - ab.x + 1;
         }
         counts[k] = cnt;
     }
 }
 
 // one workgroup of 1024: exclusive scan of the tile counts in place; meta[1] = total items
-__global__ void __launch_bounds__(1024) plan_scan_kernel(int* __restrict__ counts, int nblk, int* __restrict__ meta) {
+__global__ void __launch_bounds__(1024) plan_scan_kernel(int* __restrict__ counts, int nblk, int* __restrict__ meta,
+                                                        TileGeo g) {
     __shared__ int part[1024];
-    const int n = (nblk + PLAN_R - 1) / PLAN_R * plan_n_c(meta);
+    const int n = (nblk + g.R - 1) / g.R * plan_n_c(meta, g);
     const int t = threadIdx.x, per = (n + 1023) / 1024;
     const int b = min(n, t * per), e = min(n, b + per);
     int sum = 0;
@@ -901,14 +890,14 @@ __global__ void __launch_bounds__(1024) scan_counts_kernel(int* __restrict__ cou
 }
 
 __global__ void plan_emit_kernel(const int2* __restrict__ rows, int nblk, const int* __restrict__ meta,
-                                 const int* __restrict__ offsets, int4* __restrict__ items, int pair) {
-    const int n_t = (nblk + PLAN_R - 1) / PLAN_R, n_c = plan_n_c(meta);
+                                 const int* __restrict__ offsets, int4* __restrict__ items, int pair, TileGeo g) {
+    const int n_t = (nblk + g.R - 1) / g.R, n_c = plan_n_c(meta, g);
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n_t * n_c; k += gridDim.x * blockDim.x) {
         const int T = k / n_c, c = k % n_c;
         int o = offsets[k];
-        for (int I = T * PLAN_R; I < min(nblk, T * PLAN_R + PLAN_R); ++I) {
-            const int a = max(rows[I].x, c * PLAN_C), b = min(rows[I].y, c * PLAN_C + PLAN_C - 1);
-            for (int d = a; d <= b; d += 1 + pair) items[o++] = make_int4(I, I + d, pair ? min(2, b - d + 1) : 1, 0);
+        for (int I = T * g.R; I < min(nblk, T * g.R + g.R); ++I) {
+            const int2 ab = tile_span(I, rows[I], T, c, g);
+            for (int J = ab.x; J <= ab.y; J += 1 + pair) items[o++] = make_int4(I, J, pair ? min(2, ab.y - J + 1) : 1, 0);
         }
     }
 }
@@ -1585,8 +1574,7 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
                                              int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                                              int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
                                              int* __restrict__ ws_acc, float* tr, int t_lo = 0, int t_hi = 0,
-                                             float* __restrict__ part = nullptr,
-                                             const uint8_t* __restrict__ blk_flags = nullptr) {
+                                             float* __restrict__ part = nullptr) {
     constexpr int NS = 32 * (1 + NC);
     const int lane = threadIdx.x & 63;
     const int i = lane & 31, h = lane >> 5;
@@ -1690,10 +1678,8 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     // wave-uniform: does the row block / do the column blocks hold a missing call (flag bit 2)?  With PART this
     // is the only SNP state used (sh.cst and the other flag bits may be rewritten by a concurrent replay:
     // launch_reference_residuals in ld_kernels.h)
-    // (blk_flags: the per-block missing flags of this run's sample order, blk_miss — the count overlap's partial K
-    // loops run before the statistics that set flag bit 2)
-    const bool rm = blk_flags != nullptr ? blk_flags[I] != 0 : __any(lane < 32 && (sh.info[lane].fl & 4));
-    const bool cm = blk_flags != nullptr ? blk_flags[J0] != 0 : __any(32 + lane < NS && (sh.info[32 + lane].fl & 4));
+    const bool rm = __any(lane < 32 && (sh.info[lane].fl & 4));
+    const bool cm = __any(32 + lane < NS && (sh.info[32 + lane].fl & 4));
     auto run = [&](const int t_lo, const int t_hi) {
         if (rm && cm) kloop(std::true_type{}, std::true_type{}, t_lo, t_hi);
         else if (rm) kloop(std::true_type{}, std::false_type{}, t_lo, t_hi);
@@ -2400,8 +2386,7 @@ __global__ void __launch_bounds__(64, 2) band_f4_part_kernel(const uint32_t* __r
                                                            const int* __restrict__ Rw,
                                                            const uint8_t* __restrict__ sflags, int n_snp, int P,
                                                            float* __restrict__ gram,
-                                                           const uint8_t* __restrict__ blk_miss, int route_shift,
-                                                           const uint8_t* __restrict__ blk_flags) {
+                                                           const uint8_t* __restrict__ blk_miss, int route_shift) {
     __shared__ BandI8Lds sh;
     __shared__ float tr[32 * 33];
     const int u = xcd_slot(blockIdx.x, gridDim.x), item = u / P, piece = u % P;
@@ -2413,8 +2398,7 @@ __global__ void __launch_bounds__(64, 2) band_f4_part_kernel(const uint32_t* __r
     float* part = gram + (size_t)u * 8192;
 #define NLDSC_BODY(DIAG_)                                                                                             \
     band_f4_body<DOM, 1, DIAG_, 0, false, true>(sh, it, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp,     \
-                                                0.0, 0.0, 0.0, 0, 0, nullptr, nullptr, nullptr, tr, t_lo, t_hi, part, \
-                                                blk_flags)
+                                                0.0, 0.0, 0.0, 0, 0, nullptr, nullptr, nullptr, tr, t_lo, t_hi, part)
     if (it.y == it.x) NLDSC_BODY(true); else NLDSC_BODY(false);
 #undef NLDSC_BODY
 }
@@ -2727,8 +2711,8 @@ hipError_t launch_plan(const double* pos, int n, double w, int own_lo, int own_h
     hipLaunchKernelGGL(plan_right_kernel, dim3(1), dim3(1024), 0, st, E, n, R);
     hipLaunchKernelGGL(plan_rows_kernel, dim3((nblk + 255) / 256), dim3(256), 0, st, E, A, n, nblk, own_lo, own_hi,
                        rows, meta);
-    hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, counts, pair ? 1 : 0);
-    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts, nblk, meta);
+    hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, counts, pair ? 1 : 0, PLAN_GEO);
+    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts, nblk, meta, PLAN_GEO);
     return hipGetLastError();
 }
 
@@ -2736,7 +2720,8 @@ hipError_t launch_plan_emit(int n, const int2* rows, const int* meta, const int*
                             bool pair) {
     const int nblk = (n + 31) / 32;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, offsets, items, pair ? 1 : 0);
+    hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, offsets, items, pair ? 1 : 0,
+                       PLAN_GEO);
     return hipGetLastError();
 }
 
@@ -2771,13 +2756,20 @@ hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* gen
     return hipGetLastError();
 }
 
+size_t plan_super_tiles(int nblk, int shift) {
+    const TileGeo g = super_geo(shift);
+    const size_t nblk2 = ((size_t)nblk + (1u << shift) - 1) >> shift, n_t = (nblk2 + g.R - 1) / g.R;
+    const size_t n_c = g.abs_j ? (g.R + nblk2 + g.C - 2) / g.C + 1 : (nblk2 + g.C - 1) / g.C;  // (meta[0] <= nblk2)
+    return n_t * n_c;
+}
+
 hipError_t launch_plan_super(int n, const int2* rows, int2* rows2, int* counts2, int* meta2, int shift, hipStream_t st) {
     const int nblk = (n + 31) / 32, nblk2 = (nblk + (1 << shift) - 1) >> shift;
     hipError_t e = hipMemsetAsync(meta2, 0, 4 * sizeof(int), st);
     if (e != hipSuccess || n <= 0) return e;
     hipLaunchKernelGGL(plan_rows2_kernel, dim3((nblk2 + 255) / 256), dim3(256), 0, st, rows, nblk, shift, rows2, meta2);
-    hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, counts2, 0);
-    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts2, nblk2, meta2);
+    hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, counts2, 0, super_geo(shift));
+    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts2, nblk2, meta2, super_geo(shift));
     return hipGetLastError();
 }
 
@@ -2786,7 +2778,8 @@ hipError_t launch_plan_emit_super(int n, const int2* rows2, const int* meta2, co
                                   int shift, hipStream_t st) {
     const int nblk2 = ((n + 31) / 32 + (1 << shift) - 1) >> shift;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, offsets2, items2, 0);
+    hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, offsets2, items2, 0,
+                       super_geo(shift));
     return hipGetLastError();
 }
 
@@ -2851,56 +2844,15 @@ hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* ge
     const dim3 grid_p((unsigned)n_items * (unsigned)P);
     if (!(which & 1)) goto kc;  // the partial tiles of every item come from the main launch
     if (dom) hipLaunchKernelGGL((band_f4_part_kernel<true>), grid_p, dim3(64), 0, st, geno, pitch_words, n_it, cst,
-                                items, pos, Lw, Rw, sflags, n_snp, P, gram, blk_miss, route_shift, nullptr);
+                                items, pos, Lw, Rw, sflags, n_snp, P, gram, blk_miss, route_shift);
     else hipLaunchKernelGGL((band_f4_part_kernel<false>), grid_p, dim3(64), 0, st, geno, pitch_words, n_it, cst,
-                            items, pos, Lw, Rw, sflags, n_snp, P, gram, blk_miss, route_shift, nullptr);
+                            items, pos, Lw, Rw, sflags, n_snp, P, gram, blk_miss, route_shift);
 #define NLDSC_EPI(DOM_, KC_)                                                                                        \
     hipLaunchKernelGGL((band_f4_epi_kernel<DOM_, KC_>), dim3(n_items), dim3(64), 0, st, cst, items, pos, Lw, Rw,    \
                        sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, blk_rep, P, gram, \
                        blk_miss, route_shift, nullptr)
     if (dom) NLDSC_EPI(true, false); else NLDSC_EPI(false, false);
 kc:
-    if (blk_rep && (which & 2)) { if (dom) NLDSC_EPI(true, true); else NLDSC_EPI(false, true); }
-#undef NLDSC_EPI
-    return hipGetLastError();
-}
-
-hipError_t launch_tail_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
-                            uint32_t pad, hipStream_t st) {
-    if (n_snp <= 0) return hipSuccess;
-    hipLaunchKernelGGL(tail_rows_kernel, dim3((2 * n_snp + 255) / 256), dim3(256), 0, st, img, last, n_snp, nb, row_bytes,
-                       tail_keep, pad);
-    return hipGetLastError();
-}
-
-hipError_t launch_band_f4_parts(bool dom, int P, int n_items, const uint32_t* geno, int pitch_words, int n_it,
-                                const SnpConst* cst, const int4* items, const double* pos, const int* Lw, const int* Rw,
-                                const uint8_t* sflags, int n_snp, float* gram, const uint8_t* blk_flags,
-                                int round_items, hipStream_t st) {
-    if (n_items <= 0) return hipSuccess;
-    if (n_it > F4_SEG_CHUNKS || P < 1 || 2 * P > n_it || blk_flags == nullptr) return hipErrorInvalidValue;
-    const int chunk = round_items > 0 ? round_items : n_items;
-    for (int o = 0; o < n_items; o += chunk) {
-        const dim3 grid((unsigned)std::min(chunk, n_items - o) * (unsigned)P);
-        float* g = gram + (size_t)o * P * 8192;
-        if (dom) hipLaunchKernelGGL((band_f4_part_kernel<true>), grid, dim3(64), 0, st, geno, pitch_words, n_it, cst,
-                                    items + o, pos, Lw, Rw, sflags, n_snp, P, g, nullptr, 1, blk_flags);
-        else hipLaunchKernelGGL((band_f4_part_kernel<false>), grid, dim3(64), 0, st, geno, pitch_words, n_it, cst,
-                                items + o, pos, Lw, Rw, sflags, n_snp, P, g, nullptr, 1, blk_flags);
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_band_f4_epis(bool dom, int P, int n_items, const SnpConst* cst, const int4* items, const double* pos,
-                               const int* Lw, const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind,
-                               double n_org, double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
-                               int* ws_acc, const uint8_t* blk_rep, const float* gram, int which, hipStream_t st) {
-    if (n_items <= 0) return hipSuccess;
-#define NLDSC_EPI(DOM_, KC_)                                                                                        \
-    hipLaunchKernelGGL((band_f4_epi_kernel<DOM_, KC_>), dim3(n_items), dim3(64), 0, st, cst, items, pos, Lw, Rw,    \
-                       sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, blk_rep, P, gram, \
-                       nullptr, 1, nullptr)
-    if (which & 1) { if (dom) NLDSC_EPI(true, false); else NLDSC_EPI(false, false); }
     if (blk_rep && (which & 2)) { if (dom) NLDSC_EPI(true, true); else NLDSC_EPI(false, true); }
 #undef NLDSC_EPI
     return hipGetLastError();

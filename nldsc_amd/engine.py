@@ -166,9 +166,7 @@ class Engine:
                  band_round_items=(self._L.nldsc_engine_band_round_items(self._h)
                                    if hasattr(self._L, "nldsc_engine_band_round_items") else 0),
                  band_tail_ksplit=(self._L.nldsc_engine_band_tail_ksplit(self._h)
-                                   if hasattr(self._L, "nldsc_engine_band_tail_ksplit") else 1),
-                count_overlap=(bool(self._L.nldsc_engine_count_overlap(self._h))
-                               if hasattr(self._L, "nldsc_engine_count_overlap") else False))
+                                   if hasattr(self._L, "nldsc_engine_band_tail_ksplit") else 1))
         return d
 
 

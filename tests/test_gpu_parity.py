@@ -1145,77 +1145,3 @@ def test_deferred_rare_items_capped_on_wide_bands_with_missing_calls(engine):
     exp = O.run_c(bed, M, N, *args, targets=t, flags=O.NO_COPIES)
     sub = {k: v[t] for k, v in got.items()}
     assert_ld_close(sub, exp, label="wide band, missing calls, replayed rare variants vs oracle")
-
-
-COUNT_OVERLAP_CASES = {
-    # (N, M, length cM, dom, flags, own, rare, env, overlap): rows of >= 2^17 samples, round launches
-    "rounds_c3_rows": (315_599, 12_000, 15.0, True, (), None, False, {}, True),
-    "rounds_n131k": (131_101, 12_000, 15.0, True, (), None, False, {}, True),
-    "strict_order": (131_101, 12_000, 15.0, True, ("FLAG_STRICT_PLINK_ORDER",), None, False, {}, True),
-    "rare_replay": (315_599, 12_000, 15.0, True, (), None, True, {}, True),
-    # additive-only single block pairs overlap; column-block pairs (the default) take no partial kernel
-    "additive_single": (131_101, 12_000, 15.0, False, ("FLAG_ADDITIVE_ONLY",), None, False, {"NLDSC_F4_NC2": "0"}, True),
-    "additive_pairs": (131_101, 12_000, 15.0, False, ("FLAG_ADDITIVE_ONLY",), None, False, {}, False),
-    # an owned sub-range too small for two rounds: no overlap
-    "owned_shard": (315_599, 12_000, 15.0, True, (), (4_000, 5_500), False, {}, False),
-}
-
-
-@pytest.mark.parametrize("case", sorted(COUNT_OVERLAP_CASES))
-def test_count_overlap_bitwise_serial(engine, case):
-    """The count overlap (the default for fp4 round launches on rows of >= 2^17 samples without missing-free blocks):
-    the band's first round runs its K loops on a second stream beside the per-run count pass, storing exact Gram tiles,
-    and its epilogues run after the rest of the band.  Every output is bitwise the serial run ($NLDSC_COUNT_OVERLAP=0),
-    including PLINK's sample order and replayed rare variants, and a few SNPs equal the exact truth."""
-    import torch
-    from nldsc_amd import synth
-    from nldsc_amd.engine import Engine
-    N, M, length, dom, fl, own, rare, env, overlap = COUNT_OVERLAP_CASES[case]
-    buf, pos = synth.device_bed(M, N, seed=M + 7, length_cm=length, missing=0.01)
-    if rare:  # rare variants (<= 16 calls in a genotype class: replayed) in the first round's blocks and later
-        img = buf.cpu().numpy().copy()
-        rows = img[3:].reshape(M, (N + 3) // 4)
-        rng = np.random.default_rng(5)
-        for j in (3, 300, 6001, M - 40, M - 1):
-            g = np.zeros(N, np.int8)
-            pick = rng.choice(N, 108, replace=False)
-            g[pick[:100]], g[pick[100:]] = 1, 2
-            g[rng.random(N) < 0.01] = -1
-            rows[j] = synth.pack_bed_rows(g[None])[0]
-        buf = torch.from_numpy(img).to("cuda:0")
-    flags = MODES["f4"] | (0 if rare else _lib_flag("FLAG_EXACT_RARE"))
-    for f in fl:
-        flags |= _lib_flag(f)
-    args = (1.0, 1e-4, 1e-5, 1.0 / M, pos)
-
-    def fresh(expect):
-        with Engine(0) as e:
-            e.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
-            r = e.run(*args, flags=flags, own=own)
-            t = e.timings()
-            assert t["count_overlap"] == expect, t
-            return r, t
-
-    def both():
-        return fresh(overlap), _env_run("NLDSC_COUNT_OVERLAP", "0", lambda: fresh(False))
-    run = both
-    for var, value in env.items():
-        run = (lambda f, v, x: (lambda: _env_run(v, x, f)))(run, var, value)
-    (got, tg), (ref, tr) = run()
-    for k in got:
-        np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{case} {k}")
-    assert tg["pairs"] == tr["pairs"] and tg["flop_issued"] == tr["flop_issued"], (tg, tr)
-    if rare:
-        return
-    lo, hi = own or (0, M)
-    t = np.array(sorted({lo, lo + 31, lo + 32, (lo + hi) // 2, hi - 33, hi - 1}), np.int32)
-    bed = buf.cpu().numpy().tobytes()
-    img_rows = np.frombuffer(bed, np.uint8, offset=3).reshape(M, -1)
-    exp = O.run_f64_targets(img_rows, N, *args, t, bed=bed,
-                            **({"strict": True} if "FLAG_STRICT_PLINK_ORDER" in fl else {}))
-    sub = {k: v[t] for k, v in got.items()}
-    if not dom:
-        exp = dict(exp, l2d=np.full(len(t), np.nan), l2d_ws=np.full(len(t), -1, np.int32),
-                   l2d_wse=np.full(len(t), -1, np.int32))
-    assert_ld_close(sub, exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
-                                       maf=(0.0, 0.0)), label=f"count overlap {case}")
