@@ -691,9 +691,9 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         HIPCHK(e->plan_meta.ensure(8));  // [0, 4) single-block plan, [4, 8) super-item plan
         HIPCHK(e->h_meta.ensure(8 * sizeof(int)));
         if (t2_cand) {
-            const size_t nblk2 = (size_t)(nblk + 1) / 2;
+            const size_t nblk2 = (size_t)(nblk + 1) / 2, n_t2 = (nblk2 + 15) / 16;
             HIPCHK(e->plan_rows2.ensure(nblk2));
-            HIPCHK(e->plan_counts2.ensure(nldsc::plan_super_tiles(nblk, route_shift)));
+            HIPCHK(e->plan_counts2.ensure(n_t2 * n_t2));
         }
     }
 

@@ -128,8 +128,6 @@ hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* ge
 // block pairs the single-block plan does not hold
 constexpr int T2_STAGES = 4;  // LDS ring stages (2 chunks each) of band_f4_t2_kernel
 // shift 1: 2 x 2 super-items; shift 2: the quad kernel's 4 x 4 super-items
-// capacity of counts2 for launch_plan_super: the super-item plan's tiles (shift 2: 4 x 8 tiles of the (I, J) plane)
-size_t plan_super_tiles(int nblk, int shift);
 hipError_t launch_plan_super(int n, const int2* rows, int2* rows2, int* counts2, int* meta2, int shift, hipStream_t st);
 hipError_t launch_plan_emit_super(int n, const int2* rows2, const int* meta2, const int* offsets2, int4* items2,
                                   int shift, hipStream_t st);

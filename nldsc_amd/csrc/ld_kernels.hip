@@ -802,48 +802,28 @@ __global__ void plan_rows_kernel(const int* __restrict__ E, const int* __restric
     }
 }
 
-// Tile geometry of an item order: tiles of R rows x C columns, the columns either diagonal offsets d = J - I
-// (abs_j 0: the band's rows read as a strip, the single-block plan) or absolute column blocks J (abs_j 1: tiles of the
-// (I, J) plane — the quad kernel's super-items, where one XCD's 32 workgroups of a round then share R row and C
-// column strips, 4 + 8 super-strips instead of 2 + 17 for 2 rows of a 16-offset tile).  Tiles in (T, c) order, items
-// row by row within a tile.
-struct TileGeo {
-    int R, C, abs_j;
-};
-constexpr TileGeo PLAN_GEO = {PLAN_R, PLAN_C, 0};
-constexpr TileGeo QUAD_GEO = {4, 8, 1};  // the quad kernel's 4 x 4 super-items (shift 2)
-inline TileGeo super_geo(int shift) { return shift == 2 ? QUAD_GEO : PLAN_GEO; }
-__device__ __forceinline__ int plan_n_c(const int* meta, TileGeo g) {
-    // abs_j: row group T spans columns [T R, T R + R - 1 + max d], i.e. at most (R - 2 + meta[0]) / C + 2 tiles
-    return g.abs_j ? (g.R + meta[0] + g.C - 2) / g.C + 1 : (meta[0] + g.C - 1) / g.C;
-}
-// the absolute columns of row I inside tile (T, c), intersected with its needed range [I + r.x, I + r.y]
-__device__ __forceinline__ int2 tile_span(int I, int2 r, int T, int c, TileGeo g) {
-    const int j0 = g.abs_j ? (T * g.R / g.C + c) * g.C : I + c * g.C;
-    return make_int2(max(I + r.x, j0), min(I + r.y, j0 + g.C - 1));
-}
+__device__ __forceinline__ int plan_n_c(const int* meta) { return (meta[0] + PLAN_C - 1) / PLAN_C; }
 
-// per tile (T, c), in (T, c) order: its item count (pair: items of two neighbouring column blocks, (I, J, 2), the last
-// of a row's run in a tile possibly (I, J, 1))
+// per tile (T, c) of PLAN_R row blocks x PLAN_C offsets, in (T, c) order: its item count (pair: items of two
+// neighbouring column blocks, (I, J, 2), the last of a row's run in a tile possibly (I, J, 1))
 __global__ void plan_count_kernel(const int2* __restrict__ rows, int nblk, const int* __restrict__ meta,
-                                  int* __restrict__ counts, int pair, TileGeo g) {
-    const int n_t = (nblk + g.R - 1) / g.R, n_c = plan_n_c(meta, g);
+                                  int* __restrict__ counts, int pair) {
+    const int n_t = (nblk + PLAN_R - 1) / PLAN_R, n_c = plan_n_c(meta);
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n_t * n_c; k += gridDim.x * blockDim.x) {
         const int T = k / n_c, c = k % n_c;
         int cnt = 0;
-        for (int I = T * g.R; I < min(nblk, T * g.R + g.R); ++I) {
-            const int2 ab = tile_span(I, rows[I], T, c, g);
-            if (ab.x <= ab.y) cnt += pair ? (ab.y - ab.x + 2) / 2 : ab.y - ab.x + 1;
+        for (int I = T * PLAN_R; I < min(nblk, T * PLAN_R + PLAN_R); ++I) {
+            const int a = max(rows[I].x, c * PLAN_C), b = min(rows[I].y, c * PLAN_C + PLAN_C - 1);
+            if (a <= b) cnt += pair ? (b - a + 2) / 2 : b - a + 1;
         }
         counts[k] = cnt;
     }
 }
 
 // one workgroup of 1024: exclusive scan of the tile counts in place; meta[1] = total items
-__global__ void __launch_bounds__(1024) plan_scan_kernel(int* __restrict__ counts, int nblk, int* __restrict__ meta,
-                                                        TileGeo g) {
+__global__ void __launch_bounds__(1024) plan_scan_kernel(int* __restrict__ counts, int nblk, int* __restrict__ meta) {
     __shared__ int part[1024];
-    const int n = (nblk + g.R - 1) / g.R * plan_n_c(meta, g);
+    const int n = (nblk + PLAN_R - 1) / PLAN_R * plan_n_c(meta);
     const int t = threadIdx.x, per = (n + 1023) / 1024;
     const int b = min(n, t * per), e = min(n, b + per);
     int sum = 0;
@@ -890,14 +870,14 @@ __global__ void __launch_bounds__(1024) scan_counts_kernel(int* __restrict__ cou
 }
 
 __global__ void plan_emit_kernel(const int2* __restrict__ rows, int nblk, const int* __restrict__ meta,
-                                 const int* __restrict__ offsets, int4* __restrict__ items, int pair, TileGeo g) {
-    const int n_t = (nblk + g.R - 1) / g.R, n_c = plan_n_c(meta, g);
+                                 const int* __restrict__ offsets, int4* __restrict__ items, int pair) {
+    const int n_t = (nblk + PLAN_R - 1) / PLAN_R, n_c = plan_n_c(meta);
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n_t * n_c; k += gridDim.x * blockDim.x) {
         const int T = k / n_c, c = k % n_c;
         int o = offsets[k];
-        for (int I = T * g.R; I < min(nblk, T * g.R + g.R); ++I) {
-            const int2 ab = tile_span(I, rows[I], T, c, g);
-            for (int J = ab.x; J <= ab.y; J += 1 + pair) items[o++] = make_int4(I, J, pair ? min(2, ab.y - J + 1) : 1, 0);
+        for (int I = T * PLAN_R; I < min(nblk, T * PLAN_R + PLAN_R); ++I) {
+            const int a = max(rows[I].x, c * PLAN_C), b = min(rows[I].y, c * PLAN_C + PLAN_C - 1);
+            for (int d = a; d <= b; d += 1 + pair) items[o++] = make_int4(I, I + d, pair ? min(2, b - d + 1) : 1, 0);
         }
     }
 }
@@ -2711,8 +2691,8 @@ hipError_t launch_plan(const double* pos, int n, double w, int own_lo, int own_h
     hipLaunchKernelGGL(plan_right_kernel, dim3(1), dim3(1024), 0, st, E, n, R);
     hipLaunchKernelGGL(plan_rows_kernel, dim3((nblk + 255) / 256), dim3(256), 0, st, E, A, n, nblk, own_lo, own_hi,
                        rows, meta);
-    hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, counts, pair ? 1 : 0, PLAN_GEO);
-    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts, nblk, meta, PLAN_GEO);
+    hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, counts, pair ? 1 : 0);
+    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts, nblk, meta);
     return hipGetLastError();
 }
 
@@ -2720,8 +2700,7 @@ hipError_t launch_plan_emit(int n, const int2* rows, const int* meta, const int*
                             bool pair) {
     const int nblk = (n + 31) / 32;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, offsets, items, pair ? 1 : 0,
-                       PLAN_GEO);
+    hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, offsets, items, pair ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -2756,20 +2735,13 @@ hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* gen
     return hipGetLastError();
 }
 
-size_t plan_super_tiles(int nblk, int shift) {
-    const TileGeo g = super_geo(shift);
-    const size_t nblk2 = ((size_t)nblk + (1u << shift) - 1) >> shift, n_t = (nblk2 + g.R - 1) / g.R;
-    const size_t n_c = g.abs_j ? (g.R + nblk2 + g.C - 2) / g.C + 1 : (nblk2 + g.C - 1) / g.C;  // (meta[0] <= nblk2)
-    return n_t * n_c;
-}
-
 hipError_t launch_plan_super(int n, const int2* rows, int2* rows2, int* counts2, int* meta2, int shift, hipStream_t st) {
     const int nblk = (n + 31) / 32, nblk2 = (nblk + (1 << shift) - 1) >> shift;
     hipError_t e = hipMemsetAsync(meta2, 0, 4 * sizeof(int), st);
     if (e != hipSuccess || n <= 0) return e;
     hipLaunchKernelGGL(plan_rows2_kernel, dim3((nblk2 + 255) / 256), dim3(256), 0, st, rows, nblk, shift, rows2, meta2);
-    hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, counts2, 0, super_geo(shift));
-    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts2, nblk2, meta2, super_geo(shift));
+    hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, counts2, 0);
+    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts2, nblk2, meta2);
     return hipGetLastError();
 }
 
@@ -2778,8 +2750,7 @@ hipError_t launch_plan_emit_super(int n, const int2* rows2, const int* meta2, co
                                   int shift, hipStream_t st) {
     const int nblk2 = ((n + 31) / 32 + (1 << shift) - 1) >> shift;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, offsets2, items2, 0,
-                       super_geo(shift));
+    hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, offsets2, items2, 0);
     return hipGetLastError();
 }
 

@@ -1,13 +1,15 @@
-"""Input / parameter model of `nldsc ld` (behaviour of nldsc/ldscore/common.py:10-182).
+"""Input / parameter model of `nldsc ld` (the validation contract of nldsc/ldscore/common.py:10-182).
 
-Same classes, validation rules and messages: LDWindow (kb -> bp x 1000; > 0; <= 5 Mbp or
-<= 100 cM), PLINKFile.parse, BIMFile (tab-separated, one chromosome per file), FAMFile
-(N = number of lines), MAF [0, 1), ResidualsSTDThreshold [0, 1), RSQThreshold [0, 0.1).
+The reference's public names, validation rules and messages, written table-driven:
+  LDWindow               kb -> bp x 1000; > 0; <= 5 Mbp or <= 100 cM
+  PLINKFile.parse        prefix or one of the three paths -> (BEDFile, BIMFile, FAMFile)
+  BIMFile / FAMFile      tab-separated tables, one chromosome per .bim; n_snp / n_org = number of lines
+  MAF, ResidualsSTDThreshold, RSQThreshold: [0, 1), [0, 1), [0, 0.1)
+(RSQThreshold's repr says `std_thr=`, as the reference's does.)
 """
 from __future__ import annotations
 
 import os
-from abc import ABC
 from pathlib import Path
 
 import pandas as pd
@@ -17,14 +19,15 @@ from ..core.common import Data, NLDSCParameterError
 __all__ = ["LDWindow", "PLINKFile", "BEDFile", "BIMFile", "FAMFile", "MAF", "ResidualsSTDThreshold",
            "RSQThreshold", "NLDSCParameterError"]
 
+# window metric -> (largest window, how the message names it)
+_WINDOW_LIMITS = {"bp": (5 * 10 ** 6, "5 Mbp"), "cm": (100, "100 cm")}
+
 
 class LDWindow(Data):
     def __init__(self, ld_wind: float, metric: str = "bp"):
-        self._data = float(ld_wind)
-        self._metric = metric
-        if self._metric == "kbp":  # kilobases are carried as base pairs
-            self._data *= 1000
-            self._metric = "bp"
+        scale = 1000 if metric == "kbp" else 1  # kilobases are carried as base pairs
+        self._data = float(ld_wind) * scale
+        self._metric = "bp" if metric == "kbp" else metric
         self._validate()
 
     @property
@@ -35,76 +38,71 @@ class LDWindow(Data):
         return f"LDWindow(ld_wind={self._data}, metric='{self._metric}')"
 
     def _validate(self):
-        if self._metric not in ("bp", "cm"):
+        limit = _WINDOW_LIMITS.get(self._metric)
+        if limit is None:
             raise NLDSCParameterError("Invalid metric")
         if self._data <= 0:
             raise NLDSCParameterError("The ld-window must be greater than 0")
-        if self._metric == "bp" and self._data > 5 * 10 ** 6:
-            raise NLDSCParameterError("The ld-window cannot be larger than 5 Mbp")
-        if self._metric == "cm" and self._data > 100:
-            raise NLDSCParameterError("The ld-window cannot be larger than 100 cm")
+        if self._data > limit[0]:
+            raise NLDSCParameterError(f"The ld-window cannot be larger than {limit[1]}")
 
 
-class PLINKFile(Data, ABC):
+class PLINKFile(Data):
+    """One file of a PLINK 1 binary set; a table file keeps its columns in `_data`."""
+    EXT = ""
+    COLUMNS: tuple = ()
+
     def __init__(self, path: str):
         self._path = str(path)
         if not os.path.exists(self._path):
             raise FileNotFoundError(f'No such file: "{self._path}"')
-
-    @staticmethod
-    def parse(bfile: str):
-        """`bfile` is a prefix or the path of one of the three files."""
-        path = Path(bfile).resolve()
-        if any(path.match(ext) for ext in ("*.bed", "*.bim", "*.fam")):
-            path = path.with_suffix("")
-        elif path.is_dir():
-            raise NotImplementedError("")
-        stem = path.as_posix()
-        return BEDFile(stem + ".bed"), BIMFile(stem + ".bim"), FAMFile(stem + ".fam")
-
-
-class BEDFile(PLINKFile):
-    def __init__(self, path: str):
-        super().__init__(path)
-        self._data = path
-
-    def __repr__(self):
-        return f"BEDFile(path='{self._data}')"
+        if self.COLUMNS:
+            self._data = pd.read_csv(self._path, sep="\t", names=self.COLUMNS)
+        self._validate()
 
     def _validate(self):
         pass
 
+    def __repr__(self):
+        return f"{type(self).__name__}(path='{self._path}')"
+
+    @staticmethod
+    def parse(bfile: str):
+        """`bfile` is a prefix or the path of one of the three files -> (BEDFile, BIMFile, FAMFile)."""
+        path = Path(bfile).resolve()
+        if path.suffix in (".bed", ".bim", ".fam"):
+            path = path.with_suffix("")
+        elif path.is_dir():
+            raise NotImplementedError("")
+        return tuple(kind(path.as_posix() + kind.EXT) for kind in (BEDFile, BIMFile, FAMFile))
+
+
+def _column(name: str):
+    return property(lambda self: self._data[name])
+
+
+class BEDFile(PLINKFile):
+    EXT = ".bed"
+
+    def __init__(self, path: str):
+        super().__init__(path)
+        self._data = path  # the engine reads the file itself
+
 
 class BIMFile(PLINKFile):
+    EXT = ".bim"
     COLUMNS = ("CHR", "SNP", "CM", "BP", "A1", "A2")
+    chr, snp, cm, bp = (_column(c) for c in ("CHR", "SNP", "CM", "BP"))
 
     def __init__(self, path: str, **kwargs):
         super().__init__(path)
-        self._data = pd.read_csv(path, sep="\t", names=self.COLUMNS)
-        self._validate()
-
-    def __repr__(self):
-        return f"BIMFile(n_snp={self.n_snp})"
-
-    @property
-    def chr(self) -> pd.Series:
-        return self._data["CHR"]
-
-    @property
-    def snp(self) -> pd.Series:
-        return self._data["SNP"]
-
-    @property
-    def cm(self) -> pd.Series:
-        return self._data["CM"]
-
-    @property
-    def bp(self) -> pd.Series:
-        return self._data["BP"]
 
     @property
     def n_snp(self) -> int:
         return len(self._data)
+
+    def __repr__(self):
+        return f"BIMFile(n_snp={self.n_snp})"
 
     def _validate(self):
         if self._data["CHR"].nunique(dropna=False) != 1:
@@ -113,53 +111,33 @@ class BIMFile(PLINKFile):
 
 
 class FAMFile(PLINKFile):
+    EXT = ".fam"
     COLUMNS = ("FID", "IID", "FATHER", "MOTHER", "SEX", "TRAIT")
-
-    def __init__(self, path: str):
-        super().__init__(path)
-        self._data = pd.read_csv(path, sep="\t", names=self.COLUMNS)
-
-    def __repr__(self):
-        return f"FAMFile(n_org={self.n_org})"
 
     @property
     def n_org(self) -> int:
         return len(self._data)
 
-    def _validate(self):
-        pass
+    def __repr__(self):
+        return f"FAMFile(n_org={self.n_org})"
 
 
-class _UnitInterval(Data):
-    _what = ""
-    _hi = 1.0
-
+def _threshold(name: str, field: str, hi: float, message: str):
+    """A validated threshold in [0, hi) whose repr is `name(field=value)`."""
     def __init__(self, value: float):
         self._data = float(value)
         self._validate()
 
     def _validate(self):
-        if not (0 <= self._data < self._hi):
-            raise NLDSCParameterError(self._what)
+        if not (0 <= self._data < hi):
+            raise NLDSCParameterError(message)
+
+    return type(name, (Data,), {"__init__": __init__, "_validate": _validate,
+                                "__repr__": lambda self: f"{name}({field}={self._data})",
+                                "__module__": __name__})
 
 
-class MAF(_UnitInterval):
-    _what = "Minor allele frequency must be between 0 and 1!"
-
-    def __repr__(self) -> str:
-        return f"MAF(maf={self._data})"
-
-
-class ResidualsSTDThreshold(_UnitInterval):
-    _what = "standard deviation threshold must be between 0 and 1!"
-
-    def __repr__(self) -> str:
-        return f"ResidualsSTDThreshold(std_thr={self._data})"
-
-
-class RSQThreshold(_UnitInterval):
-    _what = "r-squared threshold must be between 0 and 0.1!"
-    _hi = 0.1
-
-    def __repr__(self) -> str:
-        return f"RSQThreshold(std_thr={self._data})"
+MAF = _threshold("MAF", "maf", 1.0, "Minor allele frequency must be between 0 and 1!")
+ResidualsSTDThreshold = _threshold("ResidualsSTDThreshold", "std_thr", 1.0,
+                                   "standard deviation threshold must be between 0 and 1!")
+RSQThreshold = _threshold("RSQThreshold", "std_thr", 0.1, "r-squared threshold must be between 0 and 0.1!")
