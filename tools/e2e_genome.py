@@ -122,7 +122,7 @@ def main():
     outdir = os.path.join(a.dir, "out")
     os.makedirs(outdir, exist_ok=True)
     cli = [sys.executable, "-m", "nldsc_amd", "ld", "--bfile", os.path.join(a.dir, "chr@"), "--ld-wind-cm", "1",
-           "--out", os.path.join(outdir, "o@.L2"), "--extra", "--quiet"]
+           "-maf", "0.0001", "--out", os.path.join(outdir, "o@.L2"), "--extra", "--quiet"]
 
     def run_cli():
         t0 = time.perf_counter()
