@@ -111,12 +111,29 @@ class BIMFile(PLINKFile):
 
 
 class FAMFile(PLINKFile):
+    """Only the number of individuals is used: it is counted from the lines (the rows pandas would parse: non-blank
+    lines; a whole-genome run reads 22 copies of a 315 599-line file, ~0.15 s each through pandas), and the table is
+    parsed when `data` is first asked for."""
     EXT = ".fam"
     COLUMNS = ("FID", "IID", "FATHER", "MOTHER", "SEX", "TRAIT")
 
+    def __init__(self, path: str):
+        self._path = str(path)
+        if not os.path.exists(self._path):
+            raise FileNotFoundError(f'No such file: "{self._path}"')
+        with open(self._path, "rb") as fh:
+            self._n_org = sum(1 for line in fh.read().split(b"\n") if line.rstrip(b"\r"))
+        self._table = None
+
+    @property
+    def data(self) -> pd.DataFrame:
+        if self._table is None:
+            self._table = pd.read_csv(self._path, sep="\t", names=self.COLUMNS)
+        return self._table
+
     @property
     def n_org(self) -> int:
-        return len(self._data)
+        return self._n_org
 
     def __repr__(self):
         return f"FAMFile(n_org={self.n_org})"
