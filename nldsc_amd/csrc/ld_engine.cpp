@@ -347,7 +347,12 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
             e->n_cu = prop.multiProcessorCount;
     }
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
-    if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->plan_stream, hipStreamNonBlocking);
+    // the schedule's stream at the device's highest priority: its short dependent kernels otherwise wait behind the
+    // count pass's workgroups (C3 trace: the plan took the whole 0.96 ms count to finish, plan_scan 0.57 ms of it),
+    // and the band cannot be launched before the host reads the item count
+    int prio_lo = 0, prio_hi = 0;
+    if (he == hipSuccess && hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = 0;
+    if (he == hipSuccess) he = hipStreamCreateWithPriority(&e->plan_stream, hipStreamNonBlocking, prio_hi);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_pos, hipEventDisableTiming);
     for (auto& ev : e->ev)
         if (he == hipSuccess) he = hipEventCreate(&ev);
@@ -685,7 +690,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     if (gpu_plan) {
         const size_t n_t = (size_t)(nblk + 15) / 16;
         HIPCHK(e->Aw.ensure((size_t)M));
-        HIPCHK(e->Ew.ensure((size_t)M));
+        HIPCHK(e->Ew.ensure((size_t)M + (M + 255) / 256));  // (+ the right-pointer scan's tile maxima)
         HIPCHK(e->plan_rows.ensure((size_t)nblk));
         HIPCHK(e->plan_counts.ensure(n_t * n_t));
         HIPCHK(e->plan_meta.ensure(8));  // [0, 4) single-block plan, [4, 8) super-item plan
@@ -789,7 +794,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         }
         compact = use_t2 && routed && n_items > 0;
         if (compact) {
-            const size_t n_chunks = ((size_t)n_items + 1023) / 1024;
+            const size_t n_chunks = ((size_t)n_items + 255) / 256;  // (ld_kernels.hip COMPACT_CHUNK)
             HIPCHK(e->items_u.ensure((size_t)n_items));
             HIPCHK(e->compact_tmp.ensure(n_chunks + 1));
             HIPCHK(e->h_route.ensure(sizeof(int)));

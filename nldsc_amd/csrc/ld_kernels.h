@@ -74,7 +74,8 @@ hipError_t launch_block_missing_rows(const uint8_t* row_miss, int n_snp, int ord
 hipError_t launch_orient_rows(uint8_t* img, uint8_t* last, int n_snp, int row_bytes, uint8_t* flip, hipStream_t st);
 // exact left pointers L from the all-pass replay's A and the device MAF flags (sorted positions)
 hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const double* pos, int n, int* L, hipStream_t st);
-// band schedule on the GPU for non-negative sorted positions: all-pass left pointers A, window edges E,
+// band schedule on the GPU for non-negative sorted positions: all-pass left pointers A, window edges E (capacity
+// n + ceil(n / 256): the right-pointer scan's tile maxima follow the n edges),
 // right pointers R, per-row-block offset ranges `rows` (nblk), tile item offsets `counts` (capacity
 // ceil(nblk/16) * ceil(nblk/16)); meta[1] = items, meta[2] = diagonal items (read after the stream
 // reaches it), then plan_emit writes the items (16 row blocks x 16 offsets tile order).  pair: items of two
@@ -162,7 +163,7 @@ hipError_t launch_issued_products(const int4* items, int n_items, const int4* it
                                  const uint8_t* blk_miss, int nblk, int kind, bool dom, int routed, int route_shift,
                                  unsigned long long* out, hipStream_t st);
 // the single-block items no super-item kernel takes (routing of 2^route_shift-block super-items), in their order, to
-// `out`; *total = their count (device); chunk_counts: ceil(n_items / 1024) ints of scratch
+// `out`; *total = their count (device); chunk_counts: ceil(n_items / 256) ints of scratch
 hipError_t launch_compact_items(const int4* items, int n_items, const uint8_t* blk_miss, int route_shift, int nblk,
                                 int* chunk_counts, int* total, int4* out, hipStream_t st);
 // the owned slice [own_lo, own_hi) of the finalized results as a [7][width] fp64 table in device memory (columns

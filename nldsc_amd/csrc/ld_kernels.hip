@@ -758,26 +758,69 @@ __global__ void plan_edges_kernel(const double* __restrict__ pos, int n, double 
     A[j] = lo;
 }
 
-// one workgroup of 1024: R_j = min(n - 1, j + running max of (E_k - k))
-__global__ void __launch_bounds__(1024) plan_right_kernel(const int* __restrict__ E, int n, int* __restrict__ R) {
-    __shared__ int part[1024];
-    const int t = threadIdx.x, per = (n + 1023) / 1024;
-    const int b = min(n, t * per), e = min(n, b + per);
-    int m = INT_MIN;
-    for (int k = b; k < e; ++k) m = max(m, E[k] - k);
-    part[t] = m;
+// The plan's single-workgroup scans and its tile kernels run with 256-thread workgroups: they share the GPU with the
+// count pass, whose 256-thread workgroups refill every CU as they finish — a 1024-thread workgroup (16 waves on one
+// CU) waited for a CU to drain (C3 trace: plan_scan 0.57 ms, the old one-workgroup right-pointer walk 0.3 ms).
+constexpr int PLAN_WG = 256;
+
+// exclusive scan of v over the PLAN_WG threads (op: sum or max, identity id); the total on every thread
+template <bool MAX>
+__device__ __forceinline__ int block_scan_excl(int v, int id, int* part, int& total) {
+    const int t = threadIdx.x;
+    part[t] = v;
     __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {  // inclusive max-scan of the chunk maxima
-        const int v = t >= o ? part[t - o] : INT_MIN;
+    for (int o = 1; o < PLAN_WG; o <<= 1) {
+        const int u = t >= o ? part[t - o] : id;
         __syncthreads();
-        part[t] = max(part[t], v);
+        part[t] = MAX ? max(part[t], u) : part[t] + u;
         __syncthreads();
     }
-    int run = t > 0 ? part[t - 1] : INT_MIN;
+    total = part[PLAN_WG - 1];
+    const int ex = t > 0 ? part[t - 1] : id;
+    __syncthreads();
+    return ex;
+}
+
+// one workgroup: exclusive scan in place of n values, chunked per thread (thread t: [t per, (t + 1) per)); returns the
+// total (sum, or max) on every thread
+template <bool MAX>
+__device__ __forceinline__ int chunked_scan_excl(int* __restrict__ v, int n, int id, int* part) {
+    const int t = threadIdx.x, per = (n + PLAN_WG - 1) / PLAN_WG;
+    const int b = min(n, t * per), e = min(n, b + per);
+    int acc = id;
+    for (int k = b; k < e; ++k) acc = MAX ? max(acc, v[k]) : acc + v[k];
+    int total;
+    int run = block_scan_excl<MAX>(acc, id, part, total);
     for (int k = b; k < e; ++k) {
-        run = max(run, E[k] - k);
-        R[k] = min(n - 1, k + run);
+        const int c = v[k];
+        v[k] = run;
+        run = MAX ? max(run, c) : run + c;
     }
+    return total;
+}
+
+// R_j = min(n - 1, j + running max of (E_k - k)): a max-scan in tiles of PLAN_WG SNPs — the tiles' maxima, their
+// exclusive scan (one workgroup), then each tile's inclusive scan from its prefix.
+__global__ void __launch_bounds__(PLAN_WG) plan_tile_max_kernel(const int* __restrict__ E, int n, int* __restrict__ tmax) {
+    __shared__ int part[PLAN_WG];
+    const int k = blockIdx.x * PLAN_WG + threadIdx.x;
+    int total;
+    (void)block_scan_excl<true>(k < n ? E[k] - k : INT_MIN, INT_MIN, part, total);
+    if (threadIdx.x == 0) tmax[blockIdx.x] = total;
+}
+// in place: tmax[b] = max of the tiles before b (INT_MIN for the first)
+__global__ void __launch_bounds__(PLAN_WG) plan_tile_scan_kernel(int* __restrict__ tmax, int ntile) {
+    __shared__ int part[PLAN_WG];
+    (void)chunked_scan_excl<true>(tmax, ntile, INT_MIN, part);
+}
+__global__ void __launch_bounds__(PLAN_WG) plan_right_kernel(const int* __restrict__ E, int n,
+                                                           const int* __restrict__ tpre, int* __restrict__ R) {
+    __shared__ int part[PLAN_WG];
+    const int k = blockIdx.x * PLAN_WG + threadIdx.x;
+    const int v = k < n ? E[k] - k : INT_MIN;
+    int total;
+    const int ex = block_scan_excl<true>(v, INT_MIN, part, total);
+    if (k < n) R[k] = min(n - 1, k + max(max(ex, v), tpre[blockIdx.x]));
 }
 
 // per row block I: useful column offsets d = J - I, [d0, d1] (empty: d0 > d1); meta[0] = max d1 + 1,
@@ -820,53 +863,18 @@ __global__ void plan_count_kernel(const int2* __restrict__ rows, int nblk, const
     }
 }
 
-// one workgroup of 1024: exclusive scan of the tile counts in place; meta[1] = total items
-__global__ void __launch_bounds__(1024) plan_scan_kernel(int* __restrict__ counts, int nblk, int* __restrict__ meta) {
-    __shared__ int part[1024];
-    const int n = (nblk + PLAN_R - 1) / PLAN_R * plan_n_c(meta);
-    const int t = threadIdx.x, per = (n + 1023) / 1024;
-    const int b = min(n, t * per), e = min(n, b + per);
-    int sum = 0;
-    for (int k = b; k < e; ++k) sum += counts[k];
-    part[t] = sum;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        const int v = t >= o ? part[t - o] : 0;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    int run = t > 0 ? part[t - 1] : 0;
-    for (int k = b; k < e; ++k) {
-        const int c = counts[k];
-        counts[k] = run;
-        run += c;
-    }
-    if (t == 1023) meta[1] = part[1023];
+// one workgroup: exclusive scan of the tile counts in place; meta[1] = total items
+__global__ void __launch_bounds__(PLAN_WG) plan_scan_kernel(int* __restrict__ counts, int nblk, int* __restrict__ meta) {
+    __shared__ int part[PLAN_WG];
+    const int total = chunked_scan_excl<false>(counts, (nblk + PLAN_R - 1) / PLAN_R * plan_n_c(meta), 0, part);
+    if (threadIdx.x == 0) meta[1] = total;
 }
 
-// one workgroup of 1024: exclusive scan of n counts in place; *total = their sum
-__global__ void __launch_bounds__(1024) scan_counts_kernel(int* __restrict__ counts, int n, int* __restrict__ total) {
-    __shared__ int part[1024];
-    const int t = threadIdx.x, per = (n + 1023) / 1024;
-    const int b = min(n, t * per), e = min(n, b + per);
-    int sum = 0;
-    for (int k = b; k < e; ++k) sum += counts[k];
-    part[t] = sum;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        const int v = t >= o ? part[t - o] : 0;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    int run = t > 0 ? part[t - 1] : 0;
-    for (int k = b; k < e; ++k) {
-        const int c = counts[k];
-        counts[k] = run;
-        run += c;
-    }
-    if (t == 1023) *total = part[1023];
+// one workgroup: exclusive scan of n counts in place; *total = their sum
+__global__ void __launch_bounds__(PLAN_WG) scan_counts_kernel(int* __restrict__ counts, int n, int* __restrict__ total) {
+    __shared__ int part[PLAN_WG];
+    const int t = chunked_scan_excl<false>(counts, n, 0, part);
+    if (threadIdx.x == 0) *total = t;
 }
 
 __global__ void plan_emit_kernel(const int2* __restrict__ rows, int nblk, const int* __restrict__ meta,
@@ -2232,14 +2240,14 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
 // tail — by the work it really has: missing-free data leaves it none, where round launches of all-routed items were
 // thousands of empty launches.  Three passes over 1024-item chunks: per-chunk counts, their exclusive scan (one
 // workgroup; meta_out = the total), the scatter.
-constexpr int COMPACT_CHUNK = 1024;
+constexpr int COMPACT_CHUNK = 256;  // (256-thread workgroups: see PLAN_WG)
 __device__ __forceinline__ bool keep_item(const int4* items, int t, const uint8_t* blk_miss, int route_shift, int nblk) {
     const int4 it = items[t];
     return !routed_item(blk_miss, route_shift, it.x, it.y, nblk) ||
            (it.z == 2 && !routed_item(blk_miss, route_shift, it.x, it.y + 1, nblk));
 }
 
-__global__ void __launch_bounds__(1024) compact_count_kernel(const int4* __restrict__ items, int n_items,
+__global__ void __launch_bounds__(COMPACT_CHUNK) compact_count_kernel(const int4* __restrict__ items, int n_items,
                                                              const uint8_t* __restrict__ blk_miss, int route_shift,
                                                              int nblk, int* __restrict__ chunk_counts) {
     const int t = blockIdx.x * COMPACT_CHUNK + threadIdx.x;
@@ -2248,7 +2256,7 @@ __global__ void __launch_bounds__(1024) compact_count_kernel(const int4* __restr
     if (threadIdx.x == 0) chunk_counts[blockIdx.x] = n;
 }
 
-__global__ void __launch_bounds__(1024) compact_scatter_kernel(const int4* __restrict__ items, int n_items,
+__global__ void __launch_bounds__(COMPACT_CHUNK) compact_scatter_kernel(const int4* __restrict__ items, int n_items,
                                                                const uint8_t* __restrict__ blk_miss, int route_shift,
                                                                int nblk, const int* __restrict__ chunk_offsets,
                                                                int4* __restrict__ out) {
@@ -2259,7 +2267,7 @@ __global__ void __launch_bounds__(1024) compact_scatter_kernel(const int4* __res
     const int before = __popcll(ballot & ((1ull << lane) - 1ull));
     if (lane == 0) wave_base[wv] = __popcll(ballot);
     __syncthreads();
-    if (threadIdx.x == 0) {  // exclusive scan of the 16 wave counts
+    if (threadIdx.x == 0) {  // exclusive scan of the wave counts
         int run = 0;
         for (int k = 0; k < COMPACT_CHUNK / 64; ++k) {
             const int c = wave_base[k];
@@ -2688,11 +2696,14 @@ hipError_t launch_plan(const double* pos, int n, double w, int own_lo, int own_h
     hipError_t e = hipMemsetAsync(meta, 0, 4 * sizeof(int), st);
     if (e != hipSuccess || n <= 0 || own_hi <= own_lo) return e;
     hipLaunchKernelGGL(plan_edges_kernel, dim3((n + 255) / 256), dim3(256), 0, st, pos, n, w, A, E);
-    hipLaunchKernelGGL(plan_right_kernel, dim3(1), dim3(1024), 0, st, E, n, R);
+    const int ntile = (n + PLAN_WG - 1) / PLAN_WG;  // (E holds n + ntile ints: the tiles' maxima after the n edges)
+    hipLaunchKernelGGL(plan_tile_max_kernel, dim3(ntile), dim3(PLAN_WG), 0, st, E, n, E + n);
+    hipLaunchKernelGGL(plan_tile_scan_kernel, dim3(1), dim3(PLAN_WG), 0, st, E + n, ntile);
+    hipLaunchKernelGGL(plan_right_kernel, dim3(ntile), dim3(PLAN_WG), 0, st, E, n, E + n, R);
     hipLaunchKernelGGL(plan_rows_kernel, dim3((nblk + 255) / 256), dim3(256), 0, st, E, A, n, nblk, own_lo, own_hi,
                        rows, meta);
     hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows, nblk, meta, counts, pair ? 1 : 0);
-    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts, nblk, meta);
+    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(PLAN_WG), 0, st, counts, nblk, meta);
     return hipGetLastError();
 }
 
@@ -2741,7 +2752,7 @@ hipError_t launch_plan_super(int n, const int2* rows, int2* rows2, int* counts2,
     if (e != hipSuccess || n <= 0) return e;
     hipLaunchKernelGGL(plan_rows2_kernel, dim3((nblk2 + 255) / 256), dim3(256), 0, st, rows, nblk, shift, rows2, meta2);
     hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, counts2, 0);
-    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, st, counts2, nblk2, meta2);
+    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(PLAN_WG), 0, st, counts2, nblk2, meta2);
     return hipGetLastError();
 }
 
@@ -2908,7 +2919,7 @@ hipError_t launch_compact_items(const int4* items, int n_items, const uint8_t* b
     if (n_items <= 0) return hipMemsetAsync(total, 0, sizeof(int), st);
     hipLaunchKernelGGL(compact_count_kernel, dim3(n_chunks), dim3(COMPACT_CHUNK), 0, st, items, n_items, blk_miss,
                        route_shift, nblk, chunk_counts);
-    hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(1024), 0, st, chunk_counts, n_chunks, total);
+    hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(PLAN_WG), 0, st, chunk_counts, n_chunks, total);
     hipLaunchKernelGGL(compact_scatter_kernel, dim3(n_chunks), dim3(COMPACT_CHUNK), 0, st, items, n_items, blk_miss,
                        route_shift, nblk, chunk_counts, out);
     return hipGetLastError();
