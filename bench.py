@@ -105,10 +105,14 @@ def pmc_traffic(kernel_key: str, n_org: int, n_snp: int, missing: float):
                   if stale else "no PMC summary for this workload")
 
 
-def table_digest(out: dict) -> dict:
+def table_digest(out) -> dict:
     """A fingerprint of the gathered score table (outside the timed region): sha256 of the three window-count
-    columns (exact integers) and the fp64 sums of L2 / L2D, so runs at different rank counts can be compared."""
+    columns (exact integers) and the fp64 sums of L2 / L2D, so runs at different rank counts can be compared.
+    `out`: the result dict, or the raw [7, M] table of a sharded run (RESULT_KEYS rows)."""
     import hashlib
+    if isinstance(out, np.ndarray):
+        from nldsc_amd.distributed import RESULT_KEYS
+        out = {k: out[i] for i, k in enumerate(RESULT_KEYS)}
     h = hashlib.sha256()
     for k in ("l2_ws", "l2d_ws", "l2d_wse"):
         if k in out:
@@ -373,8 +377,8 @@ def main():
                 eng.run_device(w, args.maf, args.std_thr, rsq, pos, table, own=own_rel, flags=flags)
             tim = eng.timings()
             tg = time.perf_counter()
-            if use_dist:
-                full = gather_table(table if coll == "cuda" else table.cpu(), spans, M, out=gbuf)
+            if use_dist:  # (RCCL: rank 0 gets the assembled table in pinned host memory, no per-step host copies)
+                full = gather_table(table if coll == "cuda" else table.cpu(), spans, M, out=gbuf, raw=True)
                 out = full if full is not None else out
             else:  # rehearsal of one rank: its slice to the host
                 out = {"l2_ws": table[4].cpu().numpy()}
@@ -461,7 +465,10 @@ def main():
                   for k in ("count_ms", "stats_ms", "schedule_ms", "band_ms", "finalize_ms", "total_ms")}
         if split:
             stages["gather_ms"] = round(float(np.mean([x["gather_ms"] for x in tims])), 3)
-        ws = out["l2_ws"]
+        if isinstance(out, np.ndarray):  # a sharded run's raw [7, M] table (RESULT_KEYS rows)
+            from nldsc_amd.distributed import RESULT_KEYS
+            out = {k: out[i] for i, k in enumerate(RESULT_KEYS)}
+        ws = np.asarray(out["l2_ws"])
         res = {
             "metric": METRIC,
             "value": total_pairs / t_max,

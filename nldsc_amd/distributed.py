@@ -109,7 +109,7 @@ def assemble(arr: np.ndarray, spans: list[tuple[int, int]], n_snp: int) -> dict:
 _ASSEMBLY: dict = {}
 
 
-def _assemble_device(blocks, spans: list[tuple[int, int]], n_snp: int) -> dict:
+def _assemble_device(blocks, spans: list[tuple[int, int]], n_snp: int, raw: bool = False):
     """Rank 0 with RCCL: the gathered [world, 7, width] device block -> the [7, n_snp] table in device memory (one
     strided copy per rank), then one copy into a pinned host buffer (both buffers reused across calls), so only
     the table itself crosses PCIe, not every rank's padded block, and no per-key host copies follow."""
@@ -135,15 +135,19 @@ def _assemble_device(blocks, spans: list[tuple[int, int]], n_snp: int) -> dict:
     host.copy_(full, non_blocking=True)
     torch.cuda.current_stream(full.device).synchronize()
     h = host.numpy()
+    if raw:  # the [7, n_snp] table itself (a view of the pinned buffer the next gather reuses)
+        return h
     # copies: the pinned buffer is reused by the next gather (a caller keeping this dict must not see it change)
     return {k: (h[i].copy() if i < 4 else h[i].astype(np.int32)) for i, k in enumerate(RESULT_KEYS)}
 
 
-def gather_table(table, spans: list[tuple[int, int]], n_snp: int, *, out=None) -> dict | None:
+def gather_table(table, spans: list[tuple[int, int]], n_snp: int, *, out=None, raw: bool = False):
     """One all_gather of every rank's [7, width] fp64 table block (torch tensor; with RCCL it stays in device
     memory and rank 0 assembles the table there before one copy to pinned host memory); the full result dict on
     rank 0, None elsewhere.  `out`: a reusable flat buffer of world * 7 * width elements on the table's device.
-    (Rank 0's arrays are its own: the pinned staging buffer reused by the next call is copied out.)"""
+    (Rank 0's arrays are its own: the pinned staging buffer reused by the next call is copied out.)  raw (RCCL, rank 0):
+    the assembled [7, n_snp] fp64 table as a view of that pinned buffer instead — no host copies per call (the
+    strong-scaling bench gathers every step), valid until the next call."""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(), dist.get_rank()
@@ -154,7 +158,7 @@ def gather_table(table, spans: list[tuple[int, int]], n_snp: int, *, out=None) -
         return None
     blocks = out.view((world,) + tuple(table.shape))
     if blocks.is_cuda:
-        return _assemble_device(blocks, spans, n_snp)
+        return _assemble_device(blocks, spans, n_snp, raw=raw)
     return assemble(blocks.numpy(), spans, n_snp)
 
 
