@@ -448,8 +448,8 @@ def main():
                                              "of missing-free blocks excluded) over FLOP_alg")
         traffic, traffic_src = pmc_traffic(
             ("band_f4_t2_kernel", "band_f4_q_kernel", "band_f4_kernel", "band_f4_part_kernel",
-             "band_f4_epi_kernel")  # (the super-item kernel + the single-block rest + the K-split tail)
-            if tims[-1].get("band_kernel") in ("f4_routed", "f4_quad") else kname.split("<")[0],
+             "band_f4_epi_kernel")  # (any super-item kernel + the single-block kernel + the K-split tail)
+            if path == "f4" else kname.split("<")[0],
             N, M, args.missing)
         roof.update(traffic=traffic, traffic_source=traffic_src,
                     algorithmic_bytes_per_launch=eng.n_snp * 4 * ((((N + 3) // 4) + 31) // 32 * 8),

@@ -189,6 +189,9 @@ struct nldsc_engine {
     // 351 -> 333 ms, C3 missing-free (6 rounds, below the threshold) 12.34 -> 12.51 ms (profiles/r03_ab_q_rounds.json)
     bool q_rounds = true;
     int last_band_kernel = NLDSC_BAND_F4;
+    // 32-SNP blocks without a missing call among the individual slots of sample order o (row_miss, at load): the
+    // super-item kernels take only missing-free blocks, so with none the run skips their plan, routing and launches
+    int free_blocks[2] = {0, 0};
     DevBuf<double> pos, l2_acc, l2d_acc;
     DevBuf<int4> items;
     // host scratch
@@ -300,6 +303,16 @@ hipError_t finish_image(nldsc_engine* e, int32_t n_snp, int32_t n_org) {
         he = nldsc::launch_row_missing(e->bed.p, e->lastb.p, n_snp, nb, row_pitch(n_org), keep_compat, keep_strict,
                                        e->row_miss.p, e->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    if (he == hipSuccess) {  // missing-free blocks per sample order
+        std::vector<uint8_t> rm((size_t)n_snp);
+        he = hipMemcpy(rm.data(), e->row_miss.p, (size_t)n_snp, hipMemcpyDeviceToHost);
+        e->free_blocks[0] = e->free_blocks[1] = 0;
+        for (int32_t b = 0; he == hipSuccess && b < (n_snp + 31) / 32; ++b) {
+            uint8_t m = 0;
+            for (int32_t j = 32 * b; j < std::min(n_snp, 32 * b + 32); ++j) m |= rm[(size_t)j];
+            for (int o = 0; o < 2; ++o) e->free_blocks[o] += ((m >> o) & 1) ? 0 : 1;
+        }
+    }
     if (he == hipSuccess) {
         e->n_snp = n_snp;
         e->n_org = n_org;
@@ -347,12 +360,7 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
             e->n_cu = prop.multiProcessorCount;
     }
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
-    // the schedule's stream at the device's highest priority: its short dependent kernels otherwise wait behind the
-    // count pass's workgroups (C3 trace: the plan took the whole 0.96 ms count to finish, plan_scan 0.57 ms of it),
-    // and the band cannot be launched before the host reads the item count
-    int prio_lo = 0, prio_hi = 0;
-    if (he == hipSuccess && hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = 0;
-    if (he == hipSuccess) he = hipStreamCreateWithPriority(&e->plan_stream, hipStreamNonBlocking, prio_hi);
+    if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->plan_stream, hipStreamNonBlocking);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_pos, hipEventDisableTiming);
     for (auto& ev : e->ev)
         if (he == hipSuccess) he = hipEventCreate(&ev);
@@ -651,8 +659,13 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     const bool sorted = nldsc::positions_sorted(p->positions, M);
     const bool gpu_plan = e->gpu_plan && sorted && max_nc == 1 &&
                           std::all_of(p->positions, p->positions + M, [](double x) { return x >= 0.0; });
-    // the 2 x 2 block-pair workgroups: fp4, unsegmented rows, GPU plan, and no K-split (choose_ksplit below)
-    const bool t2_cand = e->t2_mode > 0 && gpu_plan && use_f4 && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 2;
+    // the 2 x 2 block-pair workgroups: fp4, unsegmented rows, GPU plan, and no K-split (choose_ksplit below); with
+    // super-item routing (t2 modes 1 and 3) only when a missing-free block exists in this run's sample order (routing
+    // takes none otherwise: C3 / C2 synthetic data, 1 % missing — the super plan, the compaction and two empty quad
+    // launches cost ~50 us per run)
+    const int order = strict ? 1 : 0;  // bit of row_miss: the individual slots of this run's sample order
+    const bool t2_cand = e->t2_mode > 0 && gpu_plan && use_f4 && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 2 &&
+                         (e->t2_mode == 2 || e->free_blocks[order] > 0 || (e->quad_add && !dom));
     // additive-only fp4 items of two column blocks (GPU plan, unsegmented rows; no K-split: its partial kernel takes
     // single block pairs)
     const bool nc2 = e->f4_nc2 && gpu_plan && use_f4 && !dom && n_it <= nldsc::F4_SEG_CHUNKS;
@@ -748,7 +761,6 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // ---- window replay + schedule ----
     auto t_host0 = std::chrono::steady_clock::now();
     int n_items = 0;
-    const int order = strict ? 1 : 0;  // bit of row_miss: the individual slots of this run's sample order
     bool compact = false;
     if (gpu_plan) {
         HIPCHK(hipEventSynchronize(e->ev_plan));  // the count kernel is running meanwhile

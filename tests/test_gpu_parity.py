@@ -863,7 +863,10 @@ def test_2x2_workgroups_bitwise_single_block(engine, case, t2):
         with Engine(0) as e:
             e.load_bed_bytes(synth.bed_bytes(rows), M, N)
             r = e.run(*args, flags=flags, own=own)
-            assert e.timings()["band_kernel"] == kernel
+            # (with routing, data without a missing-free block skips the super-item kernels: the single-block run)
+            got_kernel = e.timings()["band_kernel"]
+            assert got_kernel == kernel or (t2 in ("1", "3") and got_kernel == "f4" and "missing_free" not in case
+                                            and "mixed" not in case), (got_kernel, kernel)
             return r
     # (additive-only with T2=3: the study mode that sends every super-item to the quad kernel, $NLDSC_QUAD_ADD=1)
     got = _env_run("NLDSC_QUAD_ADD", "1" if not dom and t2 == "3" else "0", lambda: _env_run(
