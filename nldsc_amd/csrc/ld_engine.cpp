@@ -117,6 +117,7 @@ struct nldsc_engine {
     hipEvent_t ev_pos = nullptr;        // positions uploaded (the schedule's only input)
     hipEvent_t ev[6] = {};
     hipEvent_t ev_dbg[2] = {};  // $NLDSC_DEBUG_TIMING: after the super-item launch, before the single-block launches
+    hipEvent_t ev_d2h[7] = {};  // the result columns landed in pinned memory (host results)
     bool debug_timing = false;
     hipEvent_t ev_plan = nullptr;  // GPU plan counters landed in h_meta
     hipEvent_t ev_stats = nullptr;   // SNP constants and replay flags written (the replay's inputs)
@@ -229,6 +230,8 @@ struct nldsc_engine {
         l2_acc.release(); l2d_acc.release(); items.release(); gram.release();
         rep_gram.release(); rep_items.release(); rep_count.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+        for (auto& e : ev_dbg) if (e) (void)hipEventDestroy(e);
+        for (auto& e : ev_d2h) if (e) (void)hipEventDestroy(e);
         if (ev_plan) (void)hipEventDestroy(ev_plan);
         Ew.release(); plan_counts.release(); plan_meta.release(); plan_rows.release();
         plan_counts2.release(); plan_rows2.release(); items2.release(); blk_miss.release(); blk_zero.release(); sums.release();
@@ -370,6 +373,8 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_route, hipEventDisableTiming);
     for (auto& ev : e->ev_dbg)
         if (he == hipSuccess) he = hipEventCreate(&ev);
+    for (auto& ev : e->ev_d2h)
+        if (he == hipSuccess) he = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (he != hipSuccess) {
         delete e;
         return set_err(err, errlen, NLDSC_E_HIP, "HIP error %s creating stream/events", hipGetErrorString(he));
@@ -888,6 +893,11 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     HIPCHK(hipMemsetAsync(e->l2_acc.p, 0, sizeof(double) * M, st));
     HIPCHK(hipMemsetAsync(e->l2d_acc.p, 0, sizeof(double) * M, st));
     HIPCHK(hipMemsetAsync(e->ws_acc.p, 0, sizeof(int) * 4 * (size_t)M, st));
+    // sums[2]: matrix-core products issued, in 16 x 16 tiles (the band kernel takes off the sub-tiles of band-edge items
+    // it skips); sums[0..1] are the device-table run's pair counts
+    HIPCHK(e->sums.ensure(3));
+    HIPCHK(e->h_sums.ensure(3 * sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(e->sums.p, 0, 3 * sizeof(unsigned long long), st));
     auto t_host1 = std::chrono::steady_clock::now();
 
     HIPCHK(hipEventRecord(e->ev[3], st));
@@ -972,7 +982,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                                                  e->ws_acc.p, true, blk_rep, which, st, single_miss, round_items,
                                                  route_shift,
                                                  dfr ? e->rep_gram.p : nullptr, dfr ? e->rep_items.p : nullptr,
-                                                 dfr ? e->rep_count.p : nullptr);
+                                                 dfr ? e->rep_count.p : nullptr, e->sums.p + 2);
             if (r == hipSuccess && dfr && (which & 2))  // after the replay: the deferred items' epilogues
                 r = nldsc::launch_band_f4_deferred_epi(dom, n_full * (nc2 ? 2 : 1), e->cst.p, e->rep_items.p,
                                                        e->rep_count.p, e->rep_gram.p, e->pos.p, e->Lw.p, e->Rw.p,
@@ -1038,10 +1048,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     HIPCHK(hipEventRecord(e->ev[4], st));
     // matrix-core products the band kernels issued, counted on the GPU per work item as each kernel decides them
     // (missing-free blocks skip the m products, diagonal blocks the transposed ones, routed items run in the 2 x 2
-    // kernel): sums[2]; sums[0..1] are the device-table run's pair counts
-    HIPCHK(e->sums.ensure(3));
-    HIPCHK(e->h_sums.ensure(3 * sizeof(unsigned long long)));
-    HIPCHK(hipMemsetAsync(e->sums.p, 0, 3 * sizeof(unsigned long long), st));
+    // kernel, band-edge items skip sub-tiles): sums[2], zeroed before the band
     HIPCHK(nldsc::launch_issued_products(single, run_single ? n_single : 0, use_t2 ? e->items2.p : nullptr,
                                          n_items2, gpu_plan ? e->plan_rows.p : nullptr,
                                          use_f4 ? e->blk_miss.p : nullptr, nblk, path, dom,
@@ -1085,27 +1092,36 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         sw = (double)s[0];
         sd = dom ? (double)s[1] : 0.0;
     } else {
-        // the owned slices land in pinned memory by DMA (pageable copies are staged by the runtime, slower) in two
-        // strided copies (fp64 rows, int32 rows), then go to the caller's arrays; the pair counts are summed on the GPU
+        // the owned slices land in pinned memory by DMA (pageable copies are staged by the runtime, slower), one copy
+        // and event per column, and each goes on to the caller's array as soon as it has landed, while the next column
+        // is still in flight; the pair counts are summed on the GPU
         const size_t o = own_begin, b8 = sizeof(double) * (size_t)std::max(n_own, 0),
                      b4 = sizeof(int) * (size_t)std::max(n_own, 0);
-        double* const ddst[4] = {r->l2 + o, r->l2d + o, r->maf + o, r->residuals_std + o};
-        int32_t* const idst[3] = {r->l2_ws + o, r->l2d_ws + o, r->l2d_wse + o};
+        void* const dst[7] = {r->l2 + o, r->l2d + o, r->maf + o, r->residuals_std + o,
+                              r->l2_ws + o, r->l2d_ws + o, r->l2d_wse + o};
+        const void* const src[7] = {e->l2.p + o, e->l2d.p + o, e->maf.p + o, e->rstd.p + o,
+                                    e->ws3.p + o, e->ws3.p + M + o, e->ws3.p + 2 * (size_t)M + o};
         if (n_own > 0) {
             HIPCHK(nldsc::launch_pack_table(e->l2.p, e->l2d.p, e->maf.p, e->rstd.p, e->ws3.p, M, own_begin, own_end,
                                             n_own, nullptr, e->sums.p, st));
             HIPCHK(e->h_res.ensure(4 * b8 + 3 * b4));
-            HIPCHK(hipMemcpy2DAsync(e->h_res.p, b8, e->l2.p + o, sizeof(double) * (size_t)M, b8, 4,
-                                    hipMemcpyDeviceToHost, st));
-            HIPCHK(hipMemcpy2DAsync(e->h_res.p + 4 * b8, b4, e->ws3.p + o, sizeof(int) * (size_t)M, b4, 3,
-                                    hipMemcpyDeviceToHost, st));
+            for (int k = 0; k < 7; ++k) {
+                HIPCHK(hipMemcpyAsync(e->h_res.p + (k < 4 ? k * b8 : 4 * b8 + (k - 4) * b4), src[k], k < 4 ? b8 : b4,
+                                      hipMemcpyDeviceToHost, st));
+                HIPCHK(hipEventRecord(e->ev_d2h[k], st));
+            }
         }
         HIPCHK(hipMemcpyAsync(e->h_sums.p, e->sums.p, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
         if (n_own > 0) {
-            for (int k = 0; k < 4; ++k) std::memcpy(ddst[k], e->h_res.p + k * b8, b8);
-            for (int k = 0; k < 3; ++k) std::memcpy(idst[k], e->h_res.p + 4 * b8 + k * b4, b4);
+            for (int k = 0; k < 7; ++k) {
+                hipError_t q;
+                while ((q = hipEventQuery(e->ev_d2h[k])) == hipErrorNotReady) {  // (a blocking wait wakes late)
+                }
+                HIPCHK(q);
+                std::memcpy(dst[k], e->h_res.p + (k < 4 ? k * b8 : 4 * b8 + (k - 4) * b4), k < 4 ? b8 : b4);
+            }
         }
+        HIPCHK(hipStreamSynchronize(st));
         const unsigned long long* s = reinterpret_cast<const unsigned long long*>(e->h_sums.p);
         sw = (double)s[0];
         sd = dom ? (double)s[1] : 0.0;
@@ -1127,7 +1143,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                      "host total %.3f (host wait for the plan %.3f)\n", e->ms[0], e->ms[1], g23, e->ms[3], e->ms[4], g05,
                      e->ms[5], e->ms[2]);
     }
-    e->flop_issued = (double)reinterpret_cast<const unsigned long long*>(e->h_sums.p)[2] * 2.0 * BLK * BLK *
+    e->flop_issued = (double)reinterpret_cast<const unsigned long long*>(e->h_sums.p)[2] * 2.0 * 16.0 * 16.0 *
                      (double)row_bytes * 4.0;
     e->pairs = sw;
     // BASELINE.md metric: FLOP_alg = 2N(1/2 sum WSA + sum WSD); additive-only 2N * 1/2 sum WSA
@@ -1190,7 +1206,7 @@ int nldsc_engine_run_device_finish(nldsc_engine* e, const int64_t* import_dev, i
     const auto t1 = std::chrono::steady_clock::now();
     // (total: both calls' host time, without the exchange between them)
     e->ms[5] = e->split_ms1 + std::chrono::duration<double, std::milli>(t1 - t0).count();
-    e->flop_issued = (double)s[2] * 2.0 * BLK * BLK * (double)e->split_row_bytes * 4.0;
+    e->flop_issued = (double)s[2] * 2.0 * 16.0 * 16.0 * (double)e->split_row_bytes * 4.0;
     e->pairs = sw;
     e->flop_alg = 2.0 * N * (0.5 * sw + sd);
     e->ops_alg_i8 = 2.0 * N * (2.0 * sw + 2.0 * sd);
