@@ -893,11 +893,6 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     HIPCHK(hipMemsetAsync(e->l2_acc.p, 0, sizeof(double) * M, st));
     HIPCHK(hipMemsetAsync(e->l2d_acc.p, 0, sizeof(double) * M, st));
     HIPCHK(hipMemsetAsync(e->ws_acc.p, 0, sizeof(int) * 4 * (size_t)M, st));
-    // sums[2]: matrix-core products issued, in 16 x 16 tiles (the band kernel takes off the sub-tiles of band-edge items
-    // it skips); sums[0..1] are the device-table run's pair counts
-    HIPCHK(e->sums.ensure(3));
-    HIPCHK(e->h_sums.ensure(3 * sizeof(unsigned long long)));
-    HIPCHK(hipMemsetAsync(e->sums.p, 0, 3 * sizeof(unsigned long long), st));
     auto t_host1 = std::chrono::steady_clock::now();
 
     HIPCHK(hipEventRecord(e->ev[3], st));
@@ -982,7 +977,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                                                  e->ws_acc.p, true, blk_rep, which, st, single_miss, round_items,
                                                  route_shift,
                                                  dfr ? e->rep_gram.p : nullptr, dfr ? e->rep_items.p : nullptr,
-                                                 dfr ? e->rep_count.p : nullptr, e->sums.p + 2);
+                                                 dfr ? e->rep_count.p : nullptr);
             if (r == hipSuccess && dfr && (which & 2))  // after the replay: the deferred items' epilogues
                 r = nldsc::launch_band_f4_deferred_epi(dom, n_full * (nc2 ? 2 : 1), e->cst.p, e->rep_items.p,
                                                        e->rep_count.p, e->rep_gram.p, e->pos.p, e->Lw.p, e->Rw.p,
@@ -1048,7 +1043,10 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     HIPCHK(hipEventRecord(e->ev[4], st));
     // matrix-core products the band kernels issued, counted on the GPU per work item as each kernel decides them
     // (missing-free blocks skip the m products, diagonal blocks the transposed ones, routed items run in the 2 x 2
-    // kernel, band-edge items skip sub-tiles): sums[2], zeroed before the band
+    // kernel): sums[2]; sums[0..1] are the device-table run's pair counts
+    HIPCHK(e->sums.ensure(3));
+    HIPCHK(e->h_sums.ensure(3 * sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(e->sums.p, 0, 3 * sizeof(unsigned long long), st));
     HIPCHK(nldsc::launch_issued_products(single, run_single ? n_single : 0, use_t2 ? e->items2.p : nullptr,
                                          n_items2, gpu_plan ? e->plan_rows.p : nullptr,
                                          use_f4 ? e->blk_miss.p : nullptr, nblk, path, dom,
@@ -1143,7 +1141,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                      "host total %.3f (host wait for the plan %.3f)\n", e->ms[0], e->ms[1], g23, e->ms[3], e->ms[4], g05,
                      e->ms[5], e->ms[2]);
     }
-    e->flop_issued = (double)reinterpret_cast<const unsigned long long*>(e->h_sums.p)[2] * 2.0 * 16.0 * 16.0 *
+    e->flop_issued = (double)reinterpret_cast<const unsigned long long*>(e->h_sums.p)[2] * 2.0 * BLK * BLK *
                      (double)row_bytes * 4.0;
     e->pairs = sw;
     // BASELINE.md metric: FLOP_alg = 2N(1/2 sum WSA + sum WSD); additive-only 2N * 1/2 sum WSA
@@ -1206,7 +1204,7 @@ int nldsc_engine_run_device_finish(nldsc_engine* e, const int64_t* import_dev, i
     const auto t1 = std::chrono::steady_clock::now();
     // (total: both calls' host time, without the exchange between them)
     e->ms[5] = e->split_ms1 + std::chrono::duration<double, std::milli>(t1 - t0).count();
-    e->flop_issued = (double)s[2] * 2.0 * 16.0 * 16.0 * (double)e->split_row_bytes * 4.0;
+    e->flop_issued = (double)s[2] * 2.0 * BLK * BLK * (double)e->split_row_bytes * 4.0;
     e->pairs = sw;
     e->flop_alg = 2.0 * N * (0.5 * sw + sd);
     e->ops_alg_i8 = 2.0 * N * (2.0 * sw + 2.0 * sd);

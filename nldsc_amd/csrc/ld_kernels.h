@@ -105,10 +105,7 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
                           int which, hipStream_t st, const uint8_t* blk_miss = nullptr, int round_items = 0,
-                          int route_shift = 1, float* rep_gram = nullptr, int4* rep_items = nullptr, int* rep_count = nullptr,
-                          unsigned long long* issued = nullptr);
-// issued (or nullptr): the issued-product count of launch_issued_products (16 x 16 sub-tile units), from which the
-// band-edge items that skip sub-tiles take them off.
+                          int route_shift = 1, float* rep_gram = nullptr, int4* rep_items = nullptr, int* rep_count = nullptr);
 // rep_gram (unsegmented rows): the items holding a replayed rare variant run their K loops in the main launch and store
 // each block pair's exact Gram tiles (rep_gram slot = atomicAdd(rep_count), 8192 floats; rep_items[slot] = the block
 // pair); after the replay, launch_band_f4_deferred_epi runs their epilogues (max_items >= the slots used) in place of
@@ -157,8 +154,7 @@ hipError_t launch_band_f4_q(bool dom, int n_items4, const uint32_t* geno, int pi
 // where sharing the strips pays), the block pairs of the others to the single-block kernel (MFMA bound at 8 products)
 hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2d_acc, const int* ws_acc, int n_snp,
                            int own_lo, int own_hi, bool dom, double* l2, double* l2d, int* ws3, hipStream_t st);
-// the matrix-core products the band kernels issued (four per 32x32 block product over all K: 16 x 16 sub-tile units, the
-// band-edge items of launch_band_f4 take off the sub-tiles they skip), counted per work item
+// the matrix-core products the band kernels issued (one per 32x32 block product over all K), counted per work item
 // as each kernel decides them: kind 2 fp4 single-block items (+ the super-items when items2 != nullptr; `routed`
 // bit 0: skip single items routed to a super-item kernel, bit 1: count only routed super-items), 1 int8, 0 fp32
 // (items of it.z column blocks);

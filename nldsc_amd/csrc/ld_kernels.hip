@@ -1495,7 +1495,6 @@ __global__ void __launch_bounds__(64, 2) band_i8_kernel(const uint32_t* __restri
 // o-products follow exactly from per-SNP sums (pair_epilogue<.., MB = true>).
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int E8M0_ONE = 127;  // block scale 2^0
 constexpr int E8M0_HALF = 126;  // 2^-1
 // VALU instructions interleaved after each MFMA of a full 8-product K step (3, 5, 6 and alternating 4/5
@@ -1556,138 +1555,6 @@ __device__ __forceinline__ f32x16v mfma_f4(const i32x4& a, const i32x4& b, const
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, B, c, 4, 4, 0, SA, 0, SB);
 }
 
-// ---- band-edge items on 16 x 16 sub-tiles (verdict r03 item 4) ----
-// An off-diagonal block pair at the edge of the band often needs only some of its four 16 x 16 sub-tiles (rows
-// 16 a.., columns 16 b..; bit 2 a + b): the window's staircase leaves out the top-right one first, then the top-left
-// or the bottom-right one, then all but the bottom-left one (C3: 2 505 of 26 034 items, 5 % of the products).  Such
-// items run their K loop on the 16 x 16 x 128 MFMA shape (the same rate per product) over the sub-tiles they need
-// only; the accumulators go to the 32 x 32 layout through LDS and the common epilogue runs on them.  The sub-tiles are
-// chosen by the epilogue's own predicate (pair_need), so a skipped entry is never read.
-__device__ __forceinline__ int needed_subtiles(const SnpSlot* info, int i, int h, double ld_wind) {
-    const SnpSlot cj = info[32 + i];
-    bool top = false, bot = false;  // this lane's column against rows 0-15 / 16-31 (its rows k + 8 q + 4 h)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const PairNeed n = pair_need(info[k + 8 * q + 4 * h], cj, false, ld_wind);
-            if (q < 2) top |= n.nij || n.nji; else bot |= n.nij || n.nji;
-        }
-    const bool left = i < 16;
-    return (__any(top && left) ? 1 : 0) | (__any(top && !left) ? 2 : 0) | (__any(bot && left) ? 4 : 0) |
-           (__any(bot && !left) ? 8 : 0);
-}
-
-// One chunk of a strip as loaded (lane (i, h): row i, samples 64 h .. 64 h + 63) -> the 16 x 16 x 128 operands of
-// rows r (f0) and 16 + r (f1) at lane 16 g + r, samples 32 g .. 32 g + 31 of the chunk: two v_permlane16_swap (odd
-// 16-lane rows of the first word <-> even rows of the second) move the words, then the usual decode.
-__device__ __forceinline__ void decode_f4_halves(const uint4 c, F4Frag& f0, F4Frag& f1) {
-    const auto s0 = __builtin_amdgcn_permlane16_swap(c.x, c.z, false, false);
-    const auto s1 = __builtin_amdgcn_permlane16_swap(c.y, c.w, false, false);
-    f0 = decode_f4<true>(s0[0], s1[0]);
-    f1 = decode_f4<true>(s0[1], s1[1]);
-}
-
-__device__ __forceinline__ f32x4 mfma_f4_16(const i32x4& a, const i32x4& b, const f32x4& c) {
-    const i32x8 A = {a[0], a[1], a[2], a[3], 0, 0, 0, 0}, B = {b[0], b[1], b[2], b[3], 0, 0, 0, 0};
-    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(A, B, c, 4, 4, 0, E8M0_ONE, 0, E8M0_ONE);
-}
-
-// K loop of an edge item (row and column blocks both with missing calls: the m products issued) over the sub-tiles of
-// MASK; g[s][p]: sub-tile s, product p in the order xx, xo, ox, oo, xh, oh, hx, ho.  The same two-buffer chunk
-// pipeline as the 32 x 32 loop, one chunk (K = 128) per step.
-template <bool DOM, int MASK>
-__device__ __forceinline__ void edge_kloop(const uint4* __restrict__ rowp, const uint4* __restrict__ colp, int n_it,
-                                           f32x4 (&g)[4][8]) {
-    constexpr int NT = (MASK & 1) + ((MASK >> 1) & 1) + ((MASK >> 2) & 1) + ((MASK >> 3) & 1);
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int p = 0; p < 8; ++p) g[s][p] = f32x4{};
-    auto mf = [&](const F4Frag (&a)[2], const F4Frag (&b)[2]) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            if (!((MASK >> s) & 1)) continue;
-            const F4Frag &A = a[s >> 1], &B = b[s & 1];
-            g[s][0] = mfma_f4_16(A.x, B.x, g[s][0]);
-            g[s][1] = mfma_f4_16(A.x, B.o, g[s][1]);
-            if (DOM) g[s][4] = mfma_f4_16(A.x, B.h, g[s][4]);
-            g[s][2] = mfma_f4_16(A.o, B.x, g[s][2]);
-            if (DOM) g[s][6] = mfma_f4_16(A.h, B.x, g[s][6]);
-            g[s][3] = mfma_f4_16(A.o, B.o, g[s][3]);
-            if (DOM) g[s][5] = mfma_f4_16(A.o, B.h, g[s][5]);
-            if (DOM) g[s][7] = mfma_f4_16(A.h, B.o, g[s][7]);
-        }
-        constexpr int n_mfma = NT * (DOM ? 8 : 4), n_valu = 2 * (4 * 9 + 2);
-#pragma unroll
-        for (int m = 0; m < n_mfma; ++m) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, (n_valu + n_mfma - 1) / n_mfma, 0);
-        }
-    };
-    const int last = n_it - 1;
-    uint4 pr = rowp[0], pc = colp[0], qr = rowp[CHUNK_U4], qc = colp[CHUNK_U4];
-    F4Frag a0[2], b0[2], a1[2], b1[2];
-    decode_f4_halves(pr, a0[0], a0[1]);
-    decode_f4_halves(pc, b0[0], b0[1]);
-    pr = rowp[CHUNK_U4 * min(2, last)];
-    pc = colp[CHUNK_U4 * min(2, last)];
-    for (int t = 0; t < n_it; t += 2) {
-        decode_f4_halves(qr, a1[0], a1[1]);
-        decode_f4_halves(qc, b1[0], b1[1]);
-        qr = rowp[CHUNK_U4 * min(t + 3, last)];
-        qc = colp[CHUNK_U4 * min(t + 3, last)];
-        mf(a0, b0);  // chunk t
-        decode_f4_halves(pr, a0[0], a0[1]);
-        decode_f4_halves(pc, b0[0], b0[1]);
-        pr = rowp[CHUNK_U4 * min(t + 4, last)];
-        pc = colp[CHUNK_U4 * min(t + 4, last)];
-        mf(a1, b1);  // chunk t + 1
-    }
-}
-
-// The sub-tiles' accumulators -> the 32 x 32 layout (lane (i, h), register r: row (r & 3) + 8 (r >> 2) + 4 h, column
-// i) through tr (32 x 33 floats), one product at a time; sub-tiles left out read as 0.
-template <bool DOM, int MASK>
-__device__ __forceinline__ void edge_to_tiles(const f32x4 (&g)[4][8], f32x16v* const (&out)[8], float* tr, int lane) {
-    const int i = lane & 31, h = lane >> 5, n = lane & 15, m0 = 4 * (lane >> 4);
-#pragma unroll
-    for (int p = 0; p < (DOM ? 8 : 4); ++p) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                tr[(16 * (s >> 1) + m0 + k) * 33 + 16 * (s & 1) + n] = ((MASK >> s) & 1) ? g[s][p][k] : 0.0f;
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < 16; ++r) (*out[p])[r] = tr[((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + i];
-        __syncthreads();
-    }
-}
-
-// An edge item's K loop when its sub-tile mask is one of the window staircase's (or 0: no pair needed, no K loop);
-// false: run the 32 x 32 loop.  The issued-product count (16 x 16 units) loses the sub-tiles left out.
-template <bool DOM>
-__device__ __forceinline__ bool band_f4_edge(int mask, const uint4* __restrict__ rowp, const uint4* __restrict__ colp,
-                                             int n_it, float* tr, int lane, f32x16v* const (&out)[8],
-                                             unsigned long long* __restrict__ issued) {
-    f32x4 g[4][8];
-    switch (mask) {
-#define NLDSC_EDGE(M_)                              \
-    case M_:                                        \
-        edge_kloop<DOM, M_>(rowp, colp, n_it, g);   \
-        edge_to_tiles<DOM, M_>(g, out, tr, lane);   \
-        break;
-        NLDSC_EDGE(4) NLDSC_EDGE(5) NLDSC_EDGE(12) NLDSC_EDGE(13)
-#undef NLDSC_EDGE
-        case 0: break;
-        default: return false;
-    }
-    if (issued != nullptr && lane == 0)
-        atomicAdd(issued, (unsigned long long)(-(long long)((4 - __builtin_popcount(mask)) * (DOM ? 8 : 4))));
-    return true;
-}
-
 // NC column blocks J0 .. J0+NC-1 share the row strip's decode; DIAG0: block 0 is the diagonal.
 // tr (32 x 33 floats of LDS): on a diagonal block, m.x is the transpose of x.m, so its MFMAs are skipped and
 // the epilogue reads x.m transposed through tr.
@@ -1705,8 +1572,7 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
                                              int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                                              int own_hi, double* __restrict__ l2_acc, double* __restrict__ l2d_acc,
                                              int* __restrict__ ws_acc, float* tr, int t_lo = 0, int t_hi = 0,
-                                             float* __restrict__ part = nullptr,
-                                             unsigned long long* __restrict__ issued = nullptr) {
+                                             float* __restrict__ part = nullptr) {
     constexpr int NS = 32 * (1 + NC);
     const int lane = threadIdx.x & 63;
     const int i = lane & 31, h = lane >> 5;
@@ -1831,23 +1697,7 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
         }
         return;
     } else if constexpr (SEG == 0) {
-        bool edge = false;
-#if NLDSC_STUDY_EDGE == 2
-        constexpr bool EDGE = false;
-#else
-        constexpr bool EDGE = DOM;
-#endif
-        if constexpr (EDGE && NC == 1 && !DIAG0 && !KC) {  // (a band-edge item: 16 x 16 sub-tiles)
-            if (rm && cm) {
-                f32x16v* const out[8] = {&gxx[0], &gxo[0], &gox[0], &goo[0], &gxh[0], &goh[0], &ghx[0], &gho[0]};
-                int mask = needed_subtiles(sh.info, i, h, ld_wind);
-#if NLDSC_STUDY_EDGE == 1
-                mask |= n_it > 0 ? 15 : 0;
-#endif
-                edge = band_f4_edge<DOM>(mask, rowp, colp[0], n_it, tr, lane, out, issued);
-            }
-        }
-        if (!edge) run(0, n_it);
+        run(0, n_it);
         if constexpr (DIAG0) {  // m.x(a, b) = x.m(b, a): lane (i, h) register r holds (row si(r), column i)
 #pragma unroll
             for (int r = 0; r < 16; ++r) tr[((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + i] = gxo[0][r];
@@ -1957,8 +1807,7 @@ __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __rest
                                                         const uint8_t* __restrict__ blk_rep,
                                                         const uint8_t* __restrict__ blk_miss, int route_shift,
                                                         float* __restrict__ rep_gram, int4* __restrict__ rep_items,
-                                                        int* __restrict__ rep_count,
-                                                        unsigned long long* __restrict__ issued) {
+                                                        int* __restrict__ rep_count) {
     __shared__ BandI8Lds sh;
     __shared__ float tr[32 * 33];
     const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
@@ -1993,8 +1842,7 @@ __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __rest
     }
 #define NLDSC_BODY(NC_, DIAG_, IT_)                                                                                   \
     band_f4_body<DOM, NC_, DIAG_, SEG, KC>(sh, IT_, geno, pitch_words, n_it, cst, pos, Lw, Rw, sflags, n_snp, ld_wind, \
-                                           n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, tr, 0, 0, nullptr,  \
-                                           issued)
+                                           n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, tr)
     if constexpr (NCX == 2) {
         static_assert(!DOM && SEG == 0, "column-block pairs: additive-only, unsegmented rows");
         if (it.z == 2) {
@@ -2496,7 +2344,6 @@ __global__ void issued_products_kernel(const int4* __restrict__ items, int n_ite
             }
         }
     }
-    n *= 4;  // (16 x 16 sub-tile units: band-edge items take off the sub-tiles they skip, band_f4_edge)
     for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o, 64);
     if ((threadIdx.x & 63) == 0 && n) atomicAdd(out, n);
 }
@@ -3025,7 +2872,7 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
                           int which, hipStream_t st, const uint8_t* blk_miss, int round_items, int route_shift,
-                          float* rep_gram, int4* rep_items, int* rep_count, unsigned long long* issued) {
+                          float* rep_gram, int4* rep_items, int* rep_count) {
     if (n_items <= 0) return hipSuccess;
     // single block-pair items, or (additive-only, unsegmented rows) column-block pairs
     if (max_nc != 1 && !(max_nc == 2 && !dom && n_it <= F4_SEG_CHUNKS)) return hipErrorInvalidValue;
@@ -3039,7 +2886,7 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                        st, geno, pitch_words,                                                                         \
                        n_it, cst, items + o, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi,       \
                        l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss, route_shift, SEG_ ? nullptr : rep_gram, \
-                       rep_items, rep_count, issued)
+                       rep_items, rep_count)
 #define NLDSC_BAND(DOM_, WPS_, SEG_, KC_) NLDSC_BAND_NC(DOM_, WPS_, SEG_, KC_, 1)
 #define NLDSC_PICK(KC_)                                                                                              \
     if (n_it > F4_SEG_CHUNKS) { if (dom) NLDSC_BAND(true, 1, F4_SEG_CHUNKS, KC_); else NLDSC_BAND(false, 2, F4_SEG_CHUNKS, KC_); } \

@@ -624,33 +624,6 @@ def test_routing_reads_this_runs_individual_slots(engine, strict, t2):
                                        maf=(0.0, 0.0)), label=f"routing strict={strict}")
 
 
-def _edge_quarters(g, pos, L, R, I, J, miss, routed, w, replay):
-    """16 x 16 sub-tile products the add+dom band-edge path leaves out (band_f4_edge), for items of the single-block
-    kernel: off the diagonal, both blocks with missing calls and (replay: the rare-variant replay runs) neither block
-    holding a replayed SNP (a genotype class of at most 16 calls: those items run the 32 x 32 loop); a sub-tile is
-    needed when one of its pairs is in the window and in a window pointer range (every SNP passes MAF here); the masks
-    of the window staircase only."""
-    M = len(pos)
-    cls = np.stack([(g == k).sum(axis=1) for k in range(3)])
-    rep = (cls.sum(axis=0) > 0) & (cls.min(axis=0) <= 16) & replay
-    blk_rep = np.array([rep[32 * b:32 * b + 32].any() for b in range(len(miss))])
-    out = 0
-    for I_, J_, r_ in zip(I.tolist(), J.tolist(), routed.tolist()):
-        if r_ or I_ == J_ or not (miss[I_] and miss[J_]) or blk_rep[I_] or blk_rep[J_]:
-            continue
-        mask = 0
-        for a in range(32):
-            for b in range(32):
-                i, j = 32 * I_ + a, 32 * J_ + b
-                if i >= M or j >= M or abs(pos[j] - pos[i]) > w:
-                    continue
-                if (L[i] >= 0 and L[i] <= j <= R[i]) or (L[j] >= 0 and L[j] <= i <= R[j]):
-                    mask |= 1 << (2 * (a >= 16) + (b >= 16))
-        if mask in (0, 4, 5, 12, 13):
-            out += (4 - bin(mask).count("1")) * 8
-    return out
-
-
 @pytest.mark.parametrize("t2", ["0", "1", "3"])
 @pytest.mark.parametrize("dom", [True, False])
 def test_issued_products_counted_per_item(engine, t2, dom):
@@ -660,10 +633,8 @@ def test_issued_products_counted_per_item(engine, t2, dom):
     !diag); fp32 1 + dom (2 - diag); with the quad kernel ($NLDSC_T2=3) every wave of a routed 4 x 4 super-item that
     needs one of its four block pairs issues all four (4 (1 + 2 dom)); additive-only runs route every super-item
     there with $NLDSC_QUAD_ADD=1 (the study mode, set here), 4 x 4 products per such wave where the super-item holds
-    missing calls.  Counted in 16 x 16 sub-tiles (four per block product): an add+dom band-edge item of the
-    single-block kernel (off the diagonal, both blocks with missing calls, no replayed SNP) skips the sub-tiles none of
-    whose pairs its epilogue uses when they form one of the window staircase's masks (_edge_quarters).  Groups of four
-    blocks alternate between missing-free, one missing call and 2 % missing."""
+    missing calls.  Groups of four blocks alternate between
+    missing-free, one missing call and 2 % missing."""
     from nldsc_amd import _lib, synth
     from nldsc_amd.engine import Engine
     N, M = 1003, 800
@@ -677,11 +648,10 @@ def test_issued_products_counted_per_item(engine, t2, dom):
     pos = synth.positions_cm(spec)
     nblk = (M + 31) // 32
     miss = np.array([(g[32 * b:32 * b + 32] < 0).any() for b in range(nblk)], int)
-    L, R, items = _lib.plan_band(pos, np.ones(M, np.uint8), 1.0, max_nc=1)
+    _, _, items = _lib.plan_band(pos, np.ones(M, np.uint8), 1.0, max_nc=1)
     I, J = items[:, 0], items[:, 1]
     rm, cm, nd = miss[I], miss[J], (I != J).astype(int)
     f4 = 1 + cm + rm * nd + rm * cm + (1 + nd + rm + cm * nd if dom else 0)
-    routed = np.zeros(len(I), bool)
     mb = lambda b: miss[np.minimum(b, nblk - 1)]  # noqa: E731
     if t2 == "1":  # super-items whose four (clamped) blocks are missing-free run in the 2 x 2 kernel
         routed = ~(mb(I & ~1) | mb((I & ~1) + 1) | mb(J & ~1) | mb((J & ~1) + 1)).astype(bool)
@@ -703,8 +673,7 @@ def test_issued_products_counted_per_item(engine, t2, dom):
         f4 = np.append(np.where(routed, 0, f4), quad)
     i8 = 4 + (2 + 2 * nd if dom else 0 * nd)
     f32 = 1 + (1 + nd if dom else 0 * nd)
-    edge = _edge_quarters(g, pos, L, R, I, J, miss, routed, 1.0, replay=False) if dom else 0  # (FLAG_EXACT_RARE)
-    expect = {"f4": 4 * int(f4.sum()) - edge, "i8": 4 * int(i8.sum()), "f32": 4 * int(f32.sum())}
+    expect = {"f4": int(f4.sum()), "i8": int(i8.sum()), "f32": int(f32.sum())}
     row_bytes = -(-((N + 3) // 4) // 64) * 64
     flags = _lib_flag("FLAG_EXACT_RARE") | (0 if dom else _lib_flag("FLAG_ADDITIVE_ONLY"))
 
@@ -714,7 +683,7 @@ def test_issued_products_counted_per_item(engine, t2, dom):
             e.load_bed_bytes(synth.bed_bytes(rows), M, N)
             for mode in MODES:
                 e.run(1.0, 0.01, 1e-5, 1.0 / M, pos, flags=flags | MODES[mode])
-                out[mode] = e.timings()["flop_issued"] / (2.0 * 16 * 16 * 4 * row_bytes)
+                out[mode] = e.timings()["flop_issued"] / (2.0 * 32 * 32 * 4 * row_bytes)
         return out
     got = _env_run("NLDSC_QUAD_ADD", "1", lambda: _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", t2, run)))
     assert got == {k: float(v) for k, v in expect.items()}, (got, expect)
