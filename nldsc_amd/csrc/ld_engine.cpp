@@ -117,7 +117,6 @@ struct nldsc_engine {
     hipEvent_t ev_pos = nullptr;        // positions uploaded (the schedule's only input)
     hipEvent_t ev[6] = {};
     hipEvent_t ev_dbg[2] = {};  // $NLDSC_DEBUG_TIMING: after the super-item launch, before the single-block launches
-    hipEvent_t ev_d2h[7] = {};  // the result columns landed in pinned memory (host results)
     bool debug_timing = false;
     hipEvent_t ev_plan = nullptr;  // GPU plan counters landed in h_meta
     hipEvent_t ev_stats = nullptr;   // SNP constants and replay flags written (the replay's inputs)
@@ -231,7 +230,6 @@ struct nldsc_engine {
         rep_gram.release(); rep_items.release(); rep_count.release();
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         for (auto& e : ev_dbg) if (e) (void)hipEventDestroy(e);
-        for (auto& e : ev_d2h) if (e) (void)hipEventDestroy(e);
         if (ev_plan) (void)hipEventDestroy(ev_plan);
         Ew.release(); plan_counts.release(); plan_meta.release(); plan_rows.release();
         plan_counts2.release(); plan_rows2.release(); items2.release(); blk_miss.release(); blk_zero.release(); sums.release();
@@ -373,8 +371,6 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_route, hipEventDisableTiming);
     for (auto& ev : e->ev_dbg)
         if (he == hipSuccess) he = hipEventCreate(&ev);
-    for (auto& ev : e->ev_d2h)
-        if (he == hipSuccess) he = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (he != hipSuccess) {
         delete e;
         return set_err(err, errlen, NLDSC_E_HIP, "HIP error %s creating stream/events", hipGetErrorString(he));
@@ -722,13 +718,19 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
 
     auto t_start = std::chrono::steady_clock::now();
     HIPCHK(hipEventRecord(e->ev[0], st));
+    // the count kernel goes first: it reads only the resident rows; the positions go up and the schedule (which
+    // depends only on them) runs on the plan stream beside it, and the statistics wait for the positions (C2: the
+    // count starts ~0.09 ms earlier than behind the positions' host copy, upload and the schedule's launches)
+    // non-individual slots read as missing (0x55) for the int8 / fp32 kernels, as 00 (all fp4 planes zero) for fp4
+    const uint32_t pad = use_f4 ? 0x00u : 0x55u;
+    const int n_pad00 = use_f4 ? 4 * row_bytes - N : 0;
+    HIPCHK(nldsc::launch_count_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, pad, n_pad00, e->counts.p, st));
+    HIPCHK(hipEventRecord(e->ev[1], st));
     HIPCHK(e->h_pos.ensure(sizeof(double) * (size_t)M));
     std::memcpy(e->h_pos.p, p->positions, sizeof(double) * (size_t)M);
-    HIPCHK(hipMemcpyAsync(e->pos.p, e->h_pos.p, sizeof(double) * M, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(e->pos.p, e->h_pos.p, sizeof(double) * M, hipMemcpyHostToDevice, e->plan_stream));
+    HIPCHK(hipEventRecord(e->ev_pos, e->plan_stream));
     if (gpu_plan) {
-        // the schedule depends only on the positions: it runs on a second stream beside the count kernel
-        HIPCHK(hipEventRecord(e->ev_pos, st));
-        HIPCHK(hipStreamWaitEvent(e->plan_stream, e->ev_pos, 0));
         HIPCHK(nldsc::launch_plan(e->pos.p, M, p->ld_wind, own_begin, own_end, e->Aw.p, e->Ew.p, e->Rw.p,
                                   e->plan_rows.p, e->plan_counts.p, e->plan_meta.p, e->plan_stream, nc2));
         if (t2_cand)
@@ -738,11 +740,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         HIPCHK(hipMemcpyAsync(e->h_meta.p, e->plan_meta.p, 8 * sizeof(int), hipMemcpyDeviceToHost, e->plan_stream));
         HIPCHK(hipEventRecord(e->ev_plan, e->plan_stream));
     }
-    // non-individual slots read as missing (0x55) for the int8 / fp32 kernels, as 00 (all fp4 planes zero) for fp4
-    const uint32_t pad = use_f4 ? 0x00u : 0x55u;
-    const int n_pad00 = use_f4 ? 4 * row_bytes - N : 0;
-    HIPCHK(nldsc::launch_count_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, pad, n_pad00, e->counts.p, st));
-    HIPCHK(hipEventRecord(e->ev[1], st));
+    HIPCHK(hipStreamWaitEvent(st, e->ev_pos, 0));
     HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->oriented ? e->flip.p : nullptr, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->cst.p,
                                    e->sflags.p, e->maf.p, e->rstd.p, st));
     // split runs: the pairs whose lower SNP is owned (flag bit 3), before the replay may touch the flags (ev_stats)
@@ -1090,36 +1088,29 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         sw = (double)s[0];
         sd = dom ? (double)s[1] : 0.0;
     } else {
-        // the owned slices land in pinned memory by DMA (pageable copies are staged by the runtime, slower), one copy
-        // and event per column, and each goes on to the caller's array as soon as it has landed, while the next column
-        // is still in flight; the pair counts are summed on the GPU
+        // the owned slices land in pinned memory by DMA (pageable copies are staged by the runtime, slower) in two
+        // strided copies (fp64 rows, int32 rows), then go to the caller's arrays; the pair counts are summed on the GPU
+        // (copying each column on as its own copy lands, polled with hipEventQuery, measured 0.07 ms faster at C2 in
+        // one process and up to 1.4 ms slower in others: the runtime's completion processing competes with the poll)
         const size_t o = own_begin, b8 = sizeof(double) * (size_t)std::max(n_own, 0),
                      b4 = sizeof(int) * (size_t)std::max(n_own, 0);
-        void* const dst[7] = {r->l2 + o, r->l2d + o, r->maf + o, r->residuals_std + o,
-                              r->l2_ws + o, r->l2d_ws + o, r->l2d_wse + o};
-        const void* const src[7] = {e->l2.p + o, e->l2d.p + o, e->maf.p + o, e->rstd.p + o,
-                                    e->ws3.p + o, e->ws3.p + M + o, e->ws3.p + 2 * (size_t)M + o};
+        double* const ddst[4] = {r->l2 + o, r->l2d + o, r->maf + o, r->residuals_std + o};
+        int32_t* const idst[3] = {r->l2_ws + o, r->l2d_ws + o, r->l2d_wse + o};
         if (n_own > 0) {
             HIPCHK(nldsc::launch_pack_table(e->l2.p, e->l2d.p, e->maf.p, e->rstd.p, e->ws3.p, M, own_begin, own_end,
                                             n_own, nullptr, e->sums.p, st));
             HIPCHK(e->h_res.ensure(4 * b8 + 3 * b4));
-            for (int k = 0; k < 7; ++k) {
-                HIPCHK(hipMemcpyAsync(e->h_res.p + (k < 4 ? k * b8 : 4 * b8 + (k - 4) * b4), src[k], k < 4 ? b8 : b4,
-                                      hipMemcpyDeviceToHost, st));
-                HIPCHK(hipEventRecord(e->ev_d2h[k], st));
-            }
+            HIPCHK(hipMemcpy2DAsync(e->h_res.p, b8, e->l2.p + o, sizeof(double) * (size_t)M, b8, 4,
+                                    hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpy2DAsync(e->h_res.p + 4 * b8, b4, e->ws3.p + o, sizeof(int) * (size_t)M, b4, 3,
+                                    hipMemcpyDeviceToHost, st));
         }
         HIPCHK(hipMemcpyAsync(e->h_sums.p, e->sums.p, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-        if (n_own > 0) {
-            for (int k = 0; k < 7; ++k) {
-                hipError_t q;
-                while ((q = hipEventQuery(e->ev_d2h[k])) == hipErrorNotReady) {  // (a blocking wait wakes late)
-                }
-                HIPCHK(q);
-                std::memcpy(dst[k], e->h_res.p + (k < 4 ? k * b8 : 4 * b8 + (k - 4) * b4), k < 4 ? b8 : b4);
-            }
-        }
         HIPCHK(hipStreamSynchronize(st));
+        if (n_own > 0) {
+            for (int k = 0; k < 4; ++k) std::memcpy(ddst[k], e->h_res.p + k * b8, b8);
+            for (int k = 0; k < 3; ++k) std::memcpy(idst[k], e->h_res.p + 4 * b8 + k * b4, b4);
+        }
         const unsigned long long* s = reinterpret_cast<const unsigned long long*>(e->h_sums.p);
         sw = (double)s[0];
         sd = dom ? (double)s[1] : 0.0;
