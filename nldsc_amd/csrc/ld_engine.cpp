@@ -15,10 +15,12 @@
 #include <cerrno>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -32,8 +34,9 @@
 namespace {
 
 constexpr int BLK = 32;             // SNPs per MFMA block
-constexpr int CHUNK_BYTES = 32;
-constexpr int kLoadThreads = 8;     // .bed file loads: reader threads (pread + H2D + placement per slice)     // one K-loop chunk of a 2-bit row (16 B per lane half)
+constexpr int CHUNK_BYTES = 32;     // one K-loop chunk of a 2-bit row (16 B per lane half)
+constexpr int kLoadThreads = 8;     // .bed file loads: reader threads (pread + H2D + placement per slice)
+constexpr int kCopyThreads = 3;     // host result copies: helper threads beside the calling one
 // resident row pitch: an even number of 32-byte chunks (the fp4 K loop takes two per iteration)
 constexpr int ROW_ALIGN_BYTES = 64;
 // item order of the single-block-pair schedule: tiles of TILE_R row blocks x TILE_C diagonal offsets
@@ -106,6 +109,85 @@ struct HostPinned {
     ~HostPinned() {
         if (p) (void)hipHostFree(p);
     }
+};
+
+// Host-to-host copies of a run's results (pinned landing buffer -> the caller's arrays, 3.5 MB at M = 80 000: ~0.33 ms
+// on one core) split by bytes over the calling thread and kCopyThreads helpers, which sleep on a condition variable
+// between runs.  Below kMinParallel bytes the caller copies alone (a wake-up costs more).
+class CopyPool {
+  public:
+    struct Seg {
+        void* dst;
+        const void* src;
+        size_t n;
+    };
+    static constexpr size_t kMinParallel = 256 << 10;
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void copy(const Seg* segs, int nseg) {
+        size_t total = 0;
+        for (int k = 0; k < nseg; ++k) total += segs[k].n;
+        if (total < kMinParallel) {
+            for (int k = 0; k < nseg; ++k) std::memcpy(segs[k].dst, segs[k].src, segs[k].n);
+            return;
+        }
+        if (th_.empty())
+            for (int t = 0; t < kCopyThreads; ++t) th_.emplace_back([this, t] { loop(t + 1); });
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            segs_ = segs;
+            nseg_ = nseg;
+            total_ = total;
+            pending_ = kCopyThreads;
+            ++gen_;
+        }
+        cv_.notify_all();
+        part(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+    }
+
+  private:
+    // bytes [total * idx / parts, total * (idx + 1) / parts) of the segments laid end to end
+    void part(int idx) {
+        const int parts = kCopyThreads + 1;
+        const size_t lo = total_ * idx / parts, hi = total_ * (idx + 1) / parts;
+        size_t base = 0;
+        for (int k = 0; k < nseg_ && base < hi; base += segs_[k].n, ++k) {
+            const size_t a = std::max(lo, base), b = std::min(hi, base + segs_[k].n);
+            if (a < b)
+                std::memcpy(static_cast<uint8_t*>(segs_[k].dst) + (a - base),
+                            static_cast<const uint8_t*>(segs_[k].src) + (a - base), b - a);
+        }
+    }
+    void loop(int idx) {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            lk.unlock();
+            part(idx);
+            lk.lock();
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const Seg* segs_ = nullptr;
+    int nseg_ = 0;
+    size_t total_ = 0;
+    int pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
 };
 
 }  // namespace
@@ -202,6 +284,7 @@ struct nldsc_engine {
     HostPinned h_meta;   // GPU plan counters (items, diagonal items)
     HostPinned h_pos;    // pinned copy of the positions (the upload does not stall this thread)
     HostPinned h_res;    // pinned landing buffer of the result copies (DMA, then host copies out)
+    CopyPool copies;     // the host copies out of h_res, split over threads
     // [0..1] device-table runs: sums of the positive WSA / WSD over the owned slice; [2] MFMA products issued
     DevBuf<unsigned long long> sums;
     HostPinned h_sums;
@@ -727,7 +810,10 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     HIPCHK(nldsc::launch_count_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, pad, n_pad00, e->counts.p, st));
     HIPCHK(hipEventRecord(e->ev[1], st));
     HIPCHK(e->h_pos.ensure(sizeof(double) * (size_t)M));
-    std::memcpy(e->h_pos.p, p->positions, sizeof(double) * (size_t)M);
+    {
+        const CopyPool::Seg seg = {e->h_pos.p, p->positions, sizeof(double) * (size_t)M};
+        e->copies.copy(&seg, 1);
+    }
     HIPCHK(hipMemcpyAsync(e->pos.p, e->h_pos.p, sizeof(double) * M, hipMemcpyHostToDevice, e->plan_stream));
     HIPCHK(hipEventRecord(e->ev_pos, e->plan_stream));
     if (gpu_plan) {
@@ -1090,8 +1176,9 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     } else {
         // the owned slices land in pinned memory by DMA (pageable copies are staged by the runtime, slower) in two
         // strided copies (fp64 rows, int32 rows), then go to the caller's arrays; the pair counts are summed on the GPU
-        // (copying each column on as its own copy lands, polled with hipEventQuery, measured 0.07 ms faster at C2 in
-        // one process and up to 1.4 ms slower in others: the runtime's completion processing competes with the poll)
+        // by four threads (copying each column on as its own copy lands, polled with hipEventQuery, measured 0.07 ms
+        // faster at C2 in one process and up to 1.4 ms slower in others: the runtime's completion processing competes
+        // with the poll)
         const size_t o = own_begin, b8 = sizeof(double) * (size_t)std::max(n_own, 0),
                      b4 = sizeof(int) * (size_t)std::max(n_own, 0);
         double* const ddst[4] = {r->l2 + o, r->l2d + o, r->maf + o, r->residuals_std + o};
@@ -1108,8 +1195,10 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         HIPCHK(hipMemcpyAsync(e->h_sums.p, e->sums.p, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         if (n_own > 0) {
-            for (int k = 0; k < 4; ++k) std::memcpy(ddst[k], e->h_res.p + k * b8, b8);
-            for (int k = 0; k < 3; ++k) std::memcpy(idst[k], e->h_res.p + 4 * b8 + k * b4, b4);
+            CopyPool::Seg segs[7];
+            for (int k = 0; k < 4; ++k) segs[k] = {ddst[k], e->h_res.p + k * b8, b8};
+            for (int k = 0; k < 3; ++k) segs[4 + k] = {idst[k], e->h_res.p + 4 * b8 + k * b4, b4};
+            e->copies.copy(segs, 7);
         }
         const unsigned long long* s = reinterpret_cast<const unsigned long long*>(e->h_sums.p);
         sw = (double)s[0];

@@ -8,7 +8,7 @@ NLDSC_DEBUG_TIMING=1 timeout -k 10 120 python bench.py --no-cpu --no-file --step
 done
 for f in b1 d1 b2 d2; do python3 -c "
 import json; d=json.loads(open('$O/$f.json').read().strip().splitlines()[-1]); print('$f', round(d['ms_per_step'],3), d['stages_ms'])"; done
-timeout -k 10 300 python tools/ab_libs.py --libs head=ab_libs/r4_head.so cur=nldsc_amd/libnldsc_amd.so --workload c2 c3 --runs 6 > $O/ab.json 2> $O/ab.err || { tail $O/ab.err; exit 1; }
+timeout -k 10 300 python tools/ab_libs.py --libs prev=ab_libs/r4_a7.so cur=ab_libs/r4_cur.so intree=nldsc_amd/libnldsc_amd.so --workload c2 c3 --runs 8 > $O/ab.json 2> $O/ab.err || { tail $O/ab.err; exit 1; }
 python3 -c "
 import json; d=json.loads(open('$O/ab.json').read().strip().splitlines()[-1])['ab']
 for w,v in d.items():
