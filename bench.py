@@ -451,6 +451,8 @@ def main():
              "band_f4_epi_kernel")  # (any super-item kernel + the single-block kernel + the K-split tail)
             if path == "f4" else kname.split("<")[0],
             N, M, args.missing)
+        if split:  # (the summaries are of the whole chromosome on one GPU, not of one rank's shard)
+            traffic, traffic_src = None, "no PMC summary of a sharded run (profiles' summaries: the whole chromosome)"
         roof.update(traffic=traffic, traffic_source=traffic_src,
                     algorithmic_bytes_per_launch=eng.n_snp * 4 * ((((N + 3) // 4) + 31) // 32 * 8),
                     avg_launch_ms=band_ms,
