@@ -802,6 +802,28 @@ def _env_run(var, value, fn):
             os.environ[var] = old
 
 
+@pytest.mark.parametrize("mode", ["f32", "i8", "f4"])
+def test_band_mode_env_selects_the_default_path(mode):
+    """$NLDSC_BAND_MODE (read when an engine is created) picks the path a run without a path flag takes: the same
+    path and the same results as that path's flag (include/nldsc_ld.h, FLAG_EXACT_F4 / EXACT_I8 / FP32)."""
+    from nldsc_amd import synth
+    from nldsc_amd.engine import Engine
+    N, M = 1003, 300
+    spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=3.0, seed=5, missing=0.01)
+    rows, pos = synth.pack_bed_rows(synth.genotypes(spec)), synth.positions_cm(spec)
+    args = (1.0, 0.01, 1e-5, 1.0 / M, pos)
+
+    def run(flags):
+        with Engine(0) as e:
+            e.load_bed_bytes(synth.bed_bytes(rows), M, N)
+            return e.run(*args, flags=flags), e.timings()["path"]
+    got, path = _env_run("NLDSC_BAND_MODE", mode, lambda: run(0))
+    ref, ref_path = run(MODES[mode])
+    assert path == ref_path == mode
+    for k in got:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
 T2_CASES = {
     # (N, M, length cM, window cM, missing, dom, own, rare): odd block counts, narrow and wide bands, missing-free
     # blocks (3 products) beside blocks with missing calls, an owned sub-range, additive only, replayed rare
