@@ -254,6 +254,9 @@ def main():
     ap.add_argument("--no-file", action="store_true",
                     help="skip the wall clock from a PLINK file (rank 0, N = 1: the synthetic .bed written to "
                          "$TMPDIR, then _ldscore.calculate timed from the file)")
+    ap.add_argument("--no-gather-overlap", action="store_true",
+                    help="strong scaling over RCCL: gather each step's table before the next step starts (default: "
+                         "on a side stream, beside the next step's compute)")
     ap.add_argument("--split-halo", action="store_true",
                     help="N > 1: compute each boundary pair once, on the rank owning the lower SNP, and send the right "
                          "halo's sums to the next rank point to point, instead of a two-sided halo on both ranks "
@@ -317,6 +320,7 @@ def main():
         s_rank, s_world = (int(x) for x in args.rehearse.split("/"))
     split = (s_world > 1 or (args.force_dist and not args.rehearse)) and not args.weak
     plan = None  # split halo plan (boundary pairs once), when `split`
+    overlap = False  # (strong scaling over RCCL: the gather beside the next step, below)
     buf, pos = synth.device_bed(M, N, seed=7 if split else 7 + rank, length_cm=args.length_cm,
                                 missing=args.missing, device=local)
     eng = Engine(local)
@@ -348,6 +352,14 @@ def main():
         table = torch.empty((len(RESULT_KEYS), table_width(spans)), dtype=torch.float64, device=f"cuda:{local}")
         gbuf = torch.empty(world * table.numel(), dtype=torch.float64,
                            device=table.device if coll == "cuda" else "cpu") if use_dist else None
+        # RCCL: step k's table is gathered on a side stream while step k + 1 computes into the other table buffer (the
+        # gather is an RCCL all-gather + rank 0's assembly and one D2H copy; every step's gather is still inside the
+        # timed region: the closing synchronize waits for the last)
+        overlap = use_dist and coll == "cuda" and plan is None and not args.no_gather_overlap
+        if overlap:
+            tables, gbufs = [table, torch.empty_like(table)], [gbuf, torch.empty_like(gbuf)]
+            gstream = torch.cuda.Stream(device=table.device)
+            gdone = [None, None]
         if plan is not None:
             export = torch.empty(6 * max(b - hi, 1), dtype=torch.int64, device=table.device)
             imported = torch.zeros(6 * max(n_recv, 1), dtype=torch.int64, device=table.device)
@@ -363,9 +375,26 @@ def main():
         f"{time.perf_counter() - t:.1f} s")
     w, rsq = args.window_cm, 1.0 / M
     out = None
+    n_step = 0
 
     def step():
-        nonlocal out
+        nonlocal out, n_step
+        if split and overlap:
+            cur = n_step % 2
+            n_step += 1
+            if gdone[cur] is not None:
+                gdone[cur].synchronize()  # the gather of step k - 2 has read this table buffer
+            eng.run_device(w, args.maf, args.std_thr, rsq, pos, tables[cur], own=own_rel, flags=flags)
+            tim = eng.timings()
+            tg = time.perf_counter()
+            with torch.cuda.stream(gstream):
+                full = gather_table(tables[cur], spans, M, out=gbufs[cur], raw=True, slot=cur, sync=False)
+                ev = torch.cuda.Event()
+                ev.record(gstream)
+            gdone[cur] = ev
+            out = full if full is not None else out  # (rank 0: read after the closing synchronize)
+            tim["gather_ms"] = 1e3 * (time.perf_counter() - tg)  # (the enqueue only)
+            return tim
         if split:  # owned slice of the one chromosome, then the table assembled on rank 0 (RCCL over xGMI)
             if plan is not None:  # (a rehearsal of one rank adds a zero block in place of its neighbour's)
                 n_send = eng.run_device_split(w, args.maf, args.std_thr, rsq, pos, table, export, own=own_rel,
@@ -506,7 +535,8 @@ def main():
                                 f"pair work, " + ("one window of right-halo rows per rank, boundary pairs computed "
                                                   "once and the halo's sums sent to the next rank point to point"
                                                   if plan is not None else "one window of halo rows per rank") +
-                                f", score table gathered over {'RCCL' if coll == 'cuda' else 'gloo'})"
+                                f", score table gathered over {'RCCL' if coll == 'cuda' else 'gloo'}" +
+                                (" on a side stream beside the next step's compute" if overlap else "") + ")"
                                 if split else f"position sharding, one chromosome unit per GPU x {world}"),
             },
             "roofline": roof,

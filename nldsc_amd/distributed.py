@@ -109,14 +109,17 @@ def assemble(arr: np.ndarray, spans: list[tuple[int, int]], n_snp: int) -> dict:
 _ASSEMBLY: dict = {}
 
 
-def _assemble_device(blocks, spans: list[tuple[int, int]], n_snp: int, raw: bool = False):
+def _assemble_device(blocks, spans: list[tuple[int, int]], n_snp: int, raw: bool = False, slot: int = 0,
+                     sync: bool = True):
     """Rank 0 with RCCL: the gathered [world, 7, width] device block -> the [7, n_snp] table in device memory (one
-    strided copy per rank), then one copy into a pinned host buffer (both buffers reused across calls), so only
-    the table itself crosses PCIe, not every rank's padded block, and no per-key host copies follow."""
+    strided copy per rank), then one copy into a pinned host buffer (both buffers reused across calls; `slot` picks
+    one of several such pairs), so only the table itself crosses PCIe, not every rank's padded block, and no per-key
+    host copies follow.  sync=False (raw only): the copies stay queued on the current stream."""
     import torch
-    key = (blocks.device, n_snp)
+    key = (blocks.device, n_snp, slot)
     if key not in _ASSEMBLY:
-        _ASSEMBLY.clear()
+        for k in [k for k in _ASSEMBLY if k[:2] != key[:2]]:
+            del _ASSEMBLY[k]
         _ASSEMBLY[key] = (torch.empty((len(RESULT_KEYS), n_snp), dtype=torch.float64, device=blocks.device),
                           torch.empty((len(RESULT_KEYS), n_snp), dtype=torch.float64, pin_memory=True))
     full, host = _ASSEMBLY[key]
@@ -133,6 +136,10 @@ def _assemble_device(blocks, spans: list[tuple[int, int]], n_snp: int, raw: bool
         full[:4, idx] = float("nan")
         full[4:, idx] = -1.0
     host.copy_(full, non_blocking=True)
+    if not sync:
+        if not raw:
+            raise ValueError("sync=False needs raw=True")
+        return host.numpy()  # (complete once the current stream has run the copies)
     torch.cuda.current_stream(full.device).synchronize()
     h = host.numpy()
     if raw:  # the [7, n_snp] table itself (a view of the pinned buffer the next gather reuses)
@@ -141,13 +148,16 @@ def _assemble_device(blocks, spans: list[tuple[int, int]], n_snp: int, raw: bool
     return {k: (h[i].copy() if i < 4 else h[i].astype(np.int32)) for i, k in enumerate(RESULT_KEYS)}
 
 
-def gather_table(table, spans: list[tuple[int, int]], n_snp: int, *, out=None, raw: bool = False):
+def gather_table(table, spans: list[tuple[int, int]], n_snp: int, *, out=None, raw: bool = False, slot: int = 0,
+                 sync: bool = True):
     """One all_gather of every rank's [7, width] fp64 table block (torch tensor; with RCCL it stays in device
     memory and rank 0 assembles the table there before one copy to pinned host memory); the full result dict on
     rank 0, None elsewhere.  `out`: a reusable flat buffer of world * 7 * width elements on the table's device.
     (Rank 0's arrays are its own: the pinned staging buffer reused by the next call is copied out.)  raw (RCCL, rank 0):
     the assembled [7, n_snp] fp64 table as a view of that pinned buffer instead — no host copies per call (the
-    strong-scaling bench gathers every step), valid until the next call."""
+    strong-scaling bench gathers every step), valid until the next call with the same `slot`.  sync=False (RCCL, raw):
+    everything stays queued on the current stream — the caller synchronises it before reading the table (the
+    strong-scaling bench gathers step k on a side stream while step k + 1 computes)."""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(), dist.get_rank()
@@ -158,7 +168,7 @@ def gather_table(table, spans: list[tuple[int, int]], n_snp: int, *, out=None, r
         return None
     blocks = out.view((world,) + tuple(table.shape))
     if blocks.is_cuda:
-        return _assemble_device(blocks, spans, n_snp, raw=raw)
+        return _assemble_device(blocks, spans, n_snp, raw=raw, slot=slot, sync=sync)
     return assemble(blocks.numpy(), spans, n_snp)
 
 
