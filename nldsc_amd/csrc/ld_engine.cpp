@@ -823,12 +823,14 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
             HIPCHK(nldsc::launch_plan_super(M, e->plan_rows.p, e->plan_rows2.p, e->plan_counts2.p, e->plan_meta.p + 4,
                                             route_shift,
                                             e->plan_stream));
+        for (int k = 0; k < 8; ++k) reinterpret_cast<volatile int*>(e->h_meta.p)[k] = -1;  // (counts land >= 0)
         HIPCHK(hipMemcpyAsync(e->h_meta.p, e->plan_meta.p, 8 * sizeof(int), hipMemcpyDeviceToHost, e->plan_stream));
         HIPCHK(hipEventRecord(e->ev_plan, e->plan_stream));
     }
     HIPCHK(hipStreamWaitEvent(st, e->ev_pos, 0));
     HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->oriented ? e->flip.p : nullptr, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->cst.p,
-                                   e->sflags.p, e->maf.p, e->rstd.p, st));
+                                   e->sflags.p, e->maf.p, e->rstd.p, st, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p,
+                                   e->blk_rep.p));
     // split runs: the pairs whose lower SNP is owned (flag bit 3), before the replay may touch the flags (ev_stats)
     if (split) HIPCHK(nldsc::launch_pair_range(e->sflags.p, M, own_begin, own_end, st));
     // rare variants: the reference's fp32 residual replayed (its sums assume N < 2^23); the flags per block here,
@@ -842,7 +844,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // them, stores Gram tiles without reading constants.  No other kernel writes sflags after snp_stats_kernel.
     if (replay) {
         HIPCHK(nldsc::launch_replay_flags(e->counts.p, e->oriented ? e->flip.p : nullptr, e->sflags.p, M,
-                                          e->blk_rep.p, st));
+                                          e->blk_rep.p, st, true));
         HIPCHK(hipEventRecord(e->ev_stats, st));
     }
     HIPCHK(hipEventRecord(e->ev[2], st));
@@ -852,7 +854,15 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     int n_items = 0;
     bool compact = false;
     if (gpu_plan) {
-        HIPCHK(hipEventSynchronize(e->ev_plan));  // the count kernel is running meanwhile
+        {  // the count kernel is running meanwhile; the host polls the pinned counters (a blocking event wait wakes
+           // the thread tens of microseconds late: the schedule is on the critical path of short runs — a 1/8 shard,
+           // C2 — whose count ends first), then the event confirms the whole copy
+            volatile const int* m = reinterpret_cast<volatile const int*>(e->h_meta.p);
+            const auto t0 = std::chrono::steady_clock::now();
+            while (m[1] < 0 && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2)) {
+            }
+            HIPCHK(hipEventSynchronize(e->ev_plan));
+        }
         const int* meta = reinterpret_cast<const int*>(e->h_meta.p);
         n_items = meta[1];
         ksplit = choose_ksplit(n_items);
@@ -974,9 +984,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                                                  e->sflags.p, e->rstd.p, rs));
         HIPCHK(hipEventRecord(e->ev_replay, rs));
     }
-    HIPCHK(hipMemsetAsync(e->l2_acc.p, 0, sizeof(double) * M, st));
-    HIPCHK(hipMemsetAsync(e->l2d_acc.p, 0, sizeof(double) * M, st));
-    HIPCHK(hipMemsetAsync(e->ws_acc.p, 0, sizeof(int) * 4 * (size_t)M, st));
+    // (l2_acc, l2d_acc and ws_acc were zeroed by snp_stats_kernel)
     auto t_host1 = std::chrono::steady_clock::now();
 
     HIPCHK(hipEventRecord(e->ev[3], st));

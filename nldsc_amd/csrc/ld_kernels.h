@@ -37,7 +37,9 @@ hipError_t launch_count_rows(uint8_t* img, const uint8_t* last, int n_snp, int n
 // flip: per-SNP stored-orientation flags (nullptr: none flipped)
 hipError_t launch_snp_stats(const int* counts, const uint8_t* flip, const double* pos, int n_snp, int n_snp_pad,
                             int n_org, double maf_thr, double std_thr, float2* lut, SnpConst* cst, uint8_t* sflags,
-                            double* maf_out, double* rstd_out, hipStream_t st);
+                            double* maf_out, double* rstd_out, hipStream_t st, double* l2_acc = nullptr,
+                            double* l2d_acc = nullptr, int* ws_acc = nullptr, uint8_t* blk_rep = nullptr);
+// (l2_acc, l2d_acc, ws_acc [4][n_snp] and blk_rep, when given: zeroed for the band and the replay flags)
 // SNPs with at most REF_RESIDUAL_MIN_CLASS calls in one genotype class (rare variants: residual nearly degenerate):
 // residual std, residual-pass flag bit 2, exact constants and fp32 table of the reference's fp32 residual,
 // replayed in its arithmetic (ld_kernels.hip reference_residual_kernel)
@@ -51,7 +53,7 @@ constexpr int REF_RESIDUAL_MIN_CLASS = 16;
 // kernel runs every item but uses flag bit 2 alone (the missing-block test; band_f4_body with PART); the KC
 // launches, the K-split epilogue of KC items and finalize wait on ev_replay.
 hipError_t launch_replay_flags(const int* counts, const uint8_t* flip, const uint8_t* sflags, int n_snp,
-                              uint8_t* blk_rep, hipStream_t st);
+                              uint8_t* blk_rep, hipStream_t st, bool zeroed = false);  // zeroed: by launch_snp_stats
 hipError_t launch_reference_residuals(const uint8_t* img, int row_bytes, int n_org, bool strict, const int* counts,
                                      const uint8_t* flip, int n_snp, double std_thr, SnpConst* cst, float2* lut,
                                      uint8_t* sflags, double* rstd_out, hipStream_t st);

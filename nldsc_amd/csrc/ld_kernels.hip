@@ -356,9 +356,17 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const uint8_t* 
                                  const double* __restrict__ pos, int n_snp, int n_snp_pad, int n_org, double maf_thr,
                                  double std_thr, float2* __restrict__ lut, SnpConst* __restrict__ cst,
                                  uint8_t* __restrict__ sflags, double* __restrict__ maf_out,
-                                 double* __restrict__ rstd_out) {
+                                 double* __restrict__ rstd_out, double* __restrict__ l2_acc,
+                                 double* __restrict__ l2d_acc, int* __restrict__ ws_acc, uint8_t* __restrict__ blk_rep) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_snp_pad) return;
+    if (j < n_snp && l2_acc != nullptr) {  // the band's per-SNP accumulators and the replay's block flags start at 0
+        l2_acc[j] = 0.0;
+        l2d_acc[j] = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ws_acc[(size_t)k * n_snp + j] = 0;
+        if (blk_rep != nullptr && (j & 31) == 0) blk_rep[j >> 5] = 0;
+    }
     float2 L[4] = {make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
     SnpConst K = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     uint8_t fl = 0;
@@ -739,21 +747,51 @@ __global__ void left_pointer_kernel(const int* __restrict__ A, const uint8_t* __
 // PLAN_C diagonal offsets (see order_items_tiled), each tile's items row by row.
 constexpr int PLAN_R = 16, PLAN_C = 16;
 
-__global__ void plan_edges_kernel(const double* __restrict__ pos, int n, double w, int* __restrict__ A,
-                                  int* __restrict__ E) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+// The searches run beside the count kernel, which keeps HBM saturated: a binary search over the whole array is ~17
+// dependent loads at loaded-memory latency (a 1/8 shard of C3: 55 us).  Each workgroup first stages the positions
+// around its 256 SNPs in LDS (PLAN_EDGE_TILE, coalesced, independent loads) and searches there; a window reaching past
+// the tile (wide windows: C5) falls back to the global search from the tile's edge.
+constexpr int PLAN_EDGE_TILE = 4096;  // positions staged per workgroup (32 KiB): 256 SNPs +- 1920
+__global__ void __launch_bounds__(256) plan_edges_kernel(const double* __restrict__ pos, int n, double w,
+                                                         int* __restrict__ A, int* __restrict__ E) {
+    __shared__ double tile[PLAN_EDGE_TILE];
+    const int j0 = blockIdx.x * 256, j = j0 + threadIdx.x;
+    const int t0 = max(0, j0 - (PLAN_EDGE_TILE - 256) / 2), t1 = min(n, t0 + PLAN_EDGE_TILE);  // tile: [t0, t1)
+    for (int k = t0 + threadIdx.x; k < t1; k += 256) tile[k - t0] = pos[k];
+    __syncthreads();
     if (j >= n) return;
-    const double pj = pos[j];
-    int lo = j + 1, hi = n;  // first k in (j, n] with pos_k - pos_j > w (n: none)
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (pos[mid] - pj > w) hi = mid; else lo = mid + 1;
+    const double pj = tile[j - t0];
+    // E[j]: first k in (j, n] with pos_k - pos_j > w (n: none)
+    int lo = j + 1, hi = n;
+    if (t1 == n || tile[t1 - 1 - t0] - pj > w) {  // the answer is in (j, t1 - 1] or is n
+        hi = t1 == n && !(tile[t1 - 1 - t0] - pj > w) ? n : t1 - 1;
+        if (hi == n) lo = n;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (tile[mid - t0] - pj > w) hi = mid; else lo = mid + 1;
+        }
+    } else {
+        lo = t1;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (pos[mid] - pj > w) hi = mid; else lo = mid + 1;
+        }
     }
     E[j] = lo;
-    lo = 0; hi = j;  // first k in [0, j] with pos_j - pos_k <= w
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (pj - pos[mid] <= w) hi = mid; else lo = mid + 1;
+    // A[j]: first k in [0, j] with pos_j - pos_k <= w
+    lo = 0; hi = j;
+    if (t0 == 0 || pj - tile[0] > w) {  // the answer is in [t0, j] (with t0 = 0: in [0, j])
+        lo = t0;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (pj - tile[mid - t0] <= w) hi = mid; else lo = mid + 1;
+        }
+    } else {
+        hi = t0;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (pj - pos[mid] <= w) hi = mid; else lo = mid + 1;
+        }
     }
     A[j] = lo;
 }
@@ -2623,17 +2661,18 @@ hipError_t launch_count_rows(uint8_t* img, const uint8_t* last, int n_snp, int n
 
 hipError_t launch_snp_stats(const int* counts, const uint8_t* flip, const double* pos, int n_snp, int n_snp_pad,
                             int n_org, double maf_thr, double std_thr, float2* lut, SnpConst* cst, uint8_t* sflags,
-                            double* maf_out, double* rstd_out, hipStream_t st) {
+                            double* maf_out, double* rstd_out, hipStream_t st, double* l2_acc, double* l2d_acc,
+                            int* ws_acc, uint8_t* blk_rep) {
     const int blocks = (n_snp_pad + 255) / 256;
     hipLaunchKernelGGL(snp_stats_kernel, dim3(blocks), dim3(256), 0, st, counts, flip, pos, n_snp, n_snp_pad, n_org,
-                       maf_thr, std_thr, lut, cst, sflags, maf_out, rstd_out);
+                       maf_thr, std_thr, lut, cst, sflags, maf_out, rstd_out, l2_acc, l2d_acc, ws_acc, blk_rep);
     return hipGetLastError();
 }
 
 hipError_t launch_replay_flags(const int* counts, const uint8_t* flip, const uint8_t* sflags, int n_snp,
-                              uint8_t* blk_rep, hipStream_t st) {
+                              uint8_t* blk_rep, hipStream_t st, bool zeroed) {
     if (n_snp <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(blk_rep, 0, (size_t)(n_snp + 31) / 32, st);
+    hipError_t e = zeroed ? hipSuccess : hipMemsetAsync(blk_rep, 0, (size_t)(n_snp + 31) / 32, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(replay_flags_kernel, dim3((n_snp + 255) / 256), dim3(256), 0, st, counts, flip, sflags, n_snp,
                        blk_rep);
