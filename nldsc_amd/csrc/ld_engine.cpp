@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -111,9 +112,10 @@ struct HostPinned {
     }
 };
 
-// Host-to-host copies of a run's results (pinned landing buffer -> the caller's arrays, 3.5 MB at M = 80 000: ~0.33 ms
-// on one core) split by bytes over the calling thread and kCopyThreads helpers, which sleep on a condition variable
-// between runs.  Below kMinParallel bytes the caller copies alone (a wake-up costs more).
+// Host work of a run split over the calling thread and kCopyThreads helpers, which sleep on a condition variable
+// between runs: the copies of its results (pinned landing buffer -> the caller's arrays, 3.5 MB at M = 80 000: ~0.33 ms
+// on one core; below kMinParallel bytes the caller copies alone, a wake-up costs more) and of its positions, and the
+// schedule's window edges.
 class CopyPool {
   public:
     struct Seg {
@@ -137,35 +139,35 @@ class CopyPool {
             for (int k = 0; k < nseg; ++k) std::memcpy(segs[k].dst, segs[k].src, segs[k].n);
             return;
         }
+        // part p: bytes [total * p / parts, total * (p + 1) / parts) of the segments laid end to end
+        parallel([&](int p, int parts) {
+            const size_t lo = total * p / parts, hi = total * (p + 1) / parts;
+            size_t base = 0;
+            for (int k = 0; k < nseg && base < hi; base += segs[k].n, ++k) {
+                const size_t a = std::max(lo, base), b = std::min(hi, base + segs[k].n);
+                if (a < b)
+                    std::memcpy(static_cast<uint8_t*>(segs[k].dst) + (a - base),
+                                static_cast<const uint8_t*>(segs[k].src) + (a - base), b - a);
+            }
+        });
+    }
+    // f(part, parts) for part = 0 .. parts - 1 (parts = kCopyThreads + 1), part 0 on the calling thread
+    void parallel(const std::function<void(int, int)>& f) {
         if (th_.empty())
             for (int t = 0; t < kCopyThreads; ++t) th_.emplace_back([this, t] { loop(t + 1); });
         {
             std::lock_guard<std::mutex> lk(mu_);
-            segs_ = segs;
-            nseg_ = nseg;
-            total_ = total;
+            job_ = &f;
             pending_ = kCopyThreads;
             ++gen_;
         }
         cv_.notify_all();
-        part(0);
+        f(0, kCopyThreads + 1);
         std::unique_lock<std::mutex> lk(mu_);
         done_.wait(lk, [this] { return pending_ == 0; });
     }
 
   private:
-    // bytes [total * idx / parts, total * (idx + 1) / parts) of the segments laid end to end
-    void part(int idx) {
-        const int parts = kCopyThreads + 1;
-        const size_t lo = total_ * idx / parts, hi = total_ * (idx + 1) / parts;
-        size_t base = 0;
-        for (int k = 0; k < nseg_ && base < hi; base += segs_[k].n, ++k) {
-            const size_t a = std::max(lo, base), b = std::min(hi, base + segs_[k].n);
-            if (a < b)
-                std::memcpy(static_cast<uint8_t*>(segs_[k].dst) + (a - base),
-                            static_cast<const uint8_t*>(segs_[k].src) + (a - base), b - a);
-        }
-    }
     void loop(int idx) {
         uint64_t seen = 0;
         std::unique_lock<std::mutex> lk(mu_);
@@ -173,8 +175,9 @@ class CopyPool {
             cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
             if (stop_) return;
             seen = gen_;
+            const std::function<void(int, int)>* f = job_;
             lk.unlock();
-            part(idx);
+            (*f)(idx, kCopyThreads + 1);
             lk.lock();
             if (--pending_ == 0) done_.notify_one();
         }
@@ -182,9 +185,7 @@ class CopyPool {
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_;
-    const Seg* segs_ = nullptr;
-    int nseg_ = 0;
-    size_t total_ = 0;
+    const std::function<void(int, int)>* job_ = nullptr;
     int pending_ = 0;
     uint64_t gen_ = 0;
     bool stop_ = false;
@@ -288,7 +289,7 @@ struct nldsc_engine {
     // [0..1] device-table runs: sums of the positive WSA / WSD over the owned slice; [2] MFMA products issued
     DevBuf<unsigned long long> sums;
     HostPinned h_sums;
-    DevBuf<int> Ew, plan_counts, plan_meta, plan_counts2;
+    DevBuf<int> plan_counts, plan_meta, plan_counts2;
     DevBuf<int2> plan_rows, plan_rows2;
     DevBuf<int4> items2;  // super-items of the 2 x 2 / quad kernel
     DevBuf<int4> items_u;  // routed runs: the single-block items no super-item kernel takes (compacted)
@@ -314,7 +315,7 @@ struct nldsc_engine {
         for (auto& e : ev) if (e) (void)hipEventDestroy(e);
         for (auto& e : ev_dbg) if (e) (void)hipEventDestroy(e);
         if (ev_plan) (void)hipEventDestroy(ev_plan);
-        Ew.release(); plan_counts.release(); plan_meta.release(); plan_rows.release();
+        plan_counts.release(); plan_meta.release(); plan_rows.release();
         plan_counts2.release(); plan_rows2.release(); items2.release(); blk_miss.release(); blk_zero.release(); sums.release();
         if (stream) (void)hipStreamDestroy(stream);
         if (plan_stream) (void)hipStreamDestroy(plan_stream);
@@ -786,8 +787,8 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     int n_items2 = 0;
     if (gpu_plan) {
         const size_t n_t = (size_t)(nblk + 15) / 16;
-        HIPCHK(e->Aw.ensure((size_t)M));
-        HIPCHK(e->Ew.ensure((size_t)M + (M + 255) / 256));  // (+ the right-pointer scan's tile maxima)
+        // window edges A | E, then the right-pointer scan's tile maxima
+        HIPCHK(e->Aw.ensure(2 * (size_t)M + (M + 255) / 256));
         HIPCHK(e->plan_rows.ensure((size_t)nblk));
         HIPCHK(e->plan_counts.ensure(n_t * n_t));
         HIPCHK(e->plan_meta.ensure(8));  // [0, 4) single-block plan, [4, 8) super-item plan
@@ -800,25 +801,28 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     }
 
     auto t_start = std::chrono::steady_clock::now();
-    HIPCHK(hipEventRecord(e->ev[0], st));
-    // the count kernel goes first: it reads only the resident rows; the positions go up and the schedule (which
-    // depends only on them) runs on the plan stream beside it, and the statistics wait for the positions (C2: the
-    // count starts ~0.09 ms earlier than behind the positions' host copy, upload and the schedule's launches)
+    // The positions go up and the schedule's window edges are searched first (~0.02 ms: beside the count kernel, whose
+    // streaming saturates HBM, those dependent loads took 0.05-0.1 ms on the critical path of short runs); then the
+    // count kernel, with the rest of the schedule beside it on the plan stream.
+    const size_t b_pos = sizeof(double) * (size_t)M;
+    HIPCHK(e->h_pos.ensure(b_pos));
+    {
+        const CopyPool::Seg seg = {e->h_pos.p, p->positions, b_pos};
+        e->copies.copy(&seg, 1);
+    }
+    HIPCHK(hipMemcpyAsync(e->pos.p, e->h_pos.p, b_pos, hipMemcpyHostToDevice, st));
+    if (gpu_plan) HIPCHK(nldsc::launch_plan_edges(e->pos.p, M, p->ld_wind, e->Aw.p, e->Aw.p + M, e->plan_meta.p, st));
+    HIPCHK(hipEventRecord(e->ev_pos, st));
     // non-individual slots read as missing (0x55) for the int8 / fp32 kernels, as 00 (all fp4 planes zero) for fp4
     const uint32_t pad = use_f4 ? 0x00u : 0x55u;
     const int n_pad00 = use_f4 ? 4 * row_bytes - N : 0;
+    HIPCHK(hipEventRecord(e->ev[0], st));  // (count_ms: the count kernel alone; the host total covers the above)
     HIPCHK(nldsc::launch_count_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, pad, n_pad00, e->counts.p, st));
     HIPCHK(hipEventRecord(e->ev[1], st));
-    HIPCHK(e->h_pos.ensure(sizeof(double) * (size_t)M));
-    {
-        const CopyPool::Seg seg = {e->h_pos.p, p->positions, sizeof(double) * (size_t)M};
-        e->copies.copy(&seg, 1);
-    }
-    HIPCHK(hipMemcpyAsync(e->pos.p, e->h_pos.p, sizeof(double) * M, hipMemcpyHostToDevice, e->plan_stream));
-    HIPCHK(hipEventRecord(e->ev_pos, e->plan_stream));
     if (gpu_plan) {
-        HIPCHK(nldsc::launch_plan(e->pos.p, M, p->ld_wind, own_begin, own_end, e->Aw.p, e->Ew.p, e->Rw.p,
-                                  e->plan_rows.p, e->plan_counts.p, e->plan_meta.p, e->plan_stream, nc2));
+        HIPCHK(hipStreamWaitEvent(e->plan_stream, e->ev_pos, 0));
+        HIPCHK(nldsc::launch_plan(M, own_begin, own_end, e->Aw.p, e->Aw.p + M, e->Rw.p, e->plan_rows.p,
+                                  e->plan_counts.p, e->plan_meta.p, e->plan_stream, nc2));
         if (t2_cand)
             HIPCHK(nldsc::launch_plan_super(M, e->plan_rows.p, e->plan_rows2.p, e->plan_counts2.p, e->plan_meta.p + 4,
                                             route_shift,
@@ -827,7 +831,6 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         HIPCHK(hipMemcpyAsync(e->h_meta.p, e->plan_meta.p, 8 * sizeof(int), hipMemcpyDeviceToHost, e->plan_stream));
         HIPCHK(hipEventRecord(e->ev_plan, e->plan_stream));
     }
-    HIPCHK(hipStreamWaitEvent(st, e->ev_pos, 0));
     HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->oriented ? e->flip.p : nullptr, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->cst.p,
                                    e->sflags.p, e->maf.p, e->rstd.p, st, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p,
                                    e->blk_rep.p));

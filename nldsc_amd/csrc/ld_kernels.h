@@ -76,14 +76,16 @@ hipError_t launch_block_missing_rows(const uint8_t* row_miss, int n_snp, int ord
 hipError_t launch_orient_rows(uint8_t* img, uint8_t* last, int n_snp, int row_bytes, uint8_t* flip, hipStream_t st);
 // exact left pointers L from the all-pass replay's A and the device MAF flags (sorted positions)
 hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const double* pos, int n, int* L, hipStream_t st);
-// band schedule on the GPU for non-negative sorted positions: all-pass left pointers A, window edges E (capacity
+// the schedule's window edges of sorted positions (all-pass left pointers A, window ends E) and meta[0..3] = 0
+hipError_t launch_plan_edges(const double* pos, int n, double w, int* A, int* E, int* meta, hipStream_t st);
+// band schedule on the GPU for non-negative sorted positions, from launch_plan_edges' A and E (capacity
 // n + ceil(n / 256): the right-pointer scan's tile maxima follow the n edges),
 // right pointers R, per-row-block offset ranges `rows` (nblk), tile item offsets `counts` (capacity
 // ceil(nblk/16) * ceil(nblk/16)); meta[1] = items, meta[2] = diagonal items (read after the stream
 // reaches it), then plan_emit writes the items (16 row blocks x 16 offsets tile order).  pair: items of two
 // neighbouring column blocks (I, J, 2) (the additive-only fp4 kernel's 32 x 64 tiles; a row's odd last one (I, J, 1))
-hipError_t launch_plan(const double* pos, int n, double w, int own_lo, int own_hi, int* A, int* E, int* R,
-                       int2* rows, int* counts, int* meta, hipStream_t st, bool pair = false);
+hipError_t launch_plan(int n, int own_lo, int own_hi, const int* A, int* E, int* R, int2* rows, int* counts, int* meta,
+                       hipStream_t st, bool pair = false);
 hipError_t launch_plan_emit(int n, const int2* rows, const int* meta, const int* offsets, int4* items, hipStream_t st,
                             bool pair = false);
 hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int pitch_words, int n_it,

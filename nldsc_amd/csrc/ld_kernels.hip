@@ -747,51 +747,27 @@ __global__ void left_pointer_kernel(const int* __restrict__ A, const uint8_t* __
 // PLAN_C diagonal offsets (see order_items_tiled), each tile's items row by row.
 constexpr int PLAN_R = 16, PLAN_C = 16;
 
-// The searches run beside the count kernel, which keeps HBM saturated: a binary search over the whole array is ~17
-// dependent loads at loaded-memory latency (a 1/8 shard of C3: 55 us).  Each workgroup first stages the positions
-// around its 256 SNPs in LDS (PLAN_EDGE_TILE, coalesced, independent loads) and searches there; a window reaching past
-// the tile (wide windows: C5) falls back to the global search from the tile's edge.
-constexpr int PLAN_EDGE_TILE = 4096;  // positions staged per workgroup (32 KiB): 256 SNPs +- 1920
+// Window edges of the sorted positions: A[j] = the first k <= j with pos_j - pos_k <= w, E[j] = the first k > j with
+// pos_k - pos_j > w (n: none) — the predicates of the reference's window (tools.h:41-49), as the epilogue evaluates
+// them.  Launched ahead of the count kernel: beside it, these dependent loads wait on its saturated HBM (a 1/8 shard of
+// C3: 55-100 us instead of ~5).  Block 0 also zeroes the schedule's counters for the kernels after it.
 __global__ void __launch_bounds__(256) plan_edges_kernel(const double* __restrict__ pos, int n, double w,
-                                                         int* __restrict__ A, int* __restrict__ E) {
-    __shared__ double tile[PLAN_EDGE_TILE];
-    const int j0 = blockIdx.x * 256, j = j0 + threadIdx.x;
-    const int t0 = max(0, j0 - (PLAN_EDGE_TILE - 256) / 2), t1 = min(n, t0 + PLAN_EDGE_TILE);  // tile: [t0, t1)
-    for (int k = t0 + threadIdx.x; k < t1; k += 256) tile[k - t0] = pos[k];
-    __syncthreads();
+                                                         int* __restrict__ A, int* __restrict__ E,
+                                                         int* __restrict__ meta) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < 4) meta[threadIdx.x] = 0;
     if (j >= n) return;
-    const double pj = tile[j - t0];
-    // E[j]: first k in (j, n] with pos_k - pos_j > w (n: none)
-    int lo = j + 1, hi = n;
-    if (t1 == n || tile[t1 - 1 - t0] - pj > w) {  // the answer is in (j, t1 - 1] or is n
-        hi = t1 == n && !(tile[t1 - 1 - t0] - pj > w) ? n : t1 - 1;
-        if (hi == n) lo = n;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (tile[mid - t0] - pj > w) hi = mid; else lo = mid + 1;
-        }
-    } else {
-        lo = t1;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (pos[mid] - pj > w) hi = mid; else lo = mid + 1;
-        }
+    const double pj = pos[j];
+    int lo = j + 1, hi = n;  // first k in (j, n] with pos_k - pos_j > w (n: none)
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (pos[mid] - pj > w) hi = mid; else lo = mid + 1;
     }
     E[j] = lo;
-    // A[j]: first k in [0, j] with pos_j - pos_k <= w
-    lo = 0; hi = j;
-    if (t0 == 0 || pj - tile[0] > w) {  // the answer is in [t0, j] (with t0 = 0: in [0, j])
-        lo = t0;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (pj - tile[mid - t0] <= w) hi = mid; else lo = mid + 1;
-        }
-    } else {
-        hi = t0;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (pj - pos[mid] <= w) hi = mid; else lo = mid + 1;
-        }
+    lo = 0; hi = j;  // first k in [0, j] with pos_j - pos_k <= w
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (pj - pos[mid] <= w) hi = mid; else lo = mid + 1;
     }
     A[j] = lo;
 }
@@ -2739,12 +2715,16 @@ hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const doubl
     return hipGetLastError();
 }
 
-hipError_t launch_plan(const double* pos, int n, double w, int own_lo, int own_hi, int* A, int* E, int* R,
-                       int2* rows, int* counts, int* meta, hipStream_t st, bool pair) {
+hipError_t launch_plan_edges(const double* pos, int n, double w, int* A, int* E, int* meta, hipStream_t st) {
+    if (n <= 0) return hipMemsetAsync(meta, 0, 4 * sizeof(int), st);
+    hipLaunchKernelGGL(plan_edges_kernel, dim3((n + 255) / 256), dim3(256), 0, st, pos, n, w, A, E, meta);
+    return hipGetLastError();
+}
+
+hipError_t launch_plan(int n, int own_lo, int own_hi, const int* A, int* E, int* R, int2* rows, int* counts, int* meta,
+                       hipStream_t st, bool pair) {
     const int nblk = (n + 31) / 32;
-    hipError_t e = hipMemsetAsync(meta, 0, 4 * sizeof(int), st);
-    if (e != hipSuccess || n <= 0 || own_hi <= own_lo) return e;
-    hipLaunchKernelGGL(plan_edges_kernel, dim3((n + 255) / 256), dim3(256), 0, st, pos, n, w, A, E);
+    if (n <= 0 || own_hi <= own_lo) return hipSuccess;  // (meta zeroed by launch_plan_edges)
     const int ntile = (n + PLAN_WG - 1) / PLAN_WG;  // (E holds n + ntile ints: the tiles' maxima after the n edges)
     hipLaunchKernelGGL(plan_tile_max_kernel, dim3(ntile), dim3(PLAN_WG), 0, st, E, n, E + n);
     hipLaunchKernelGGL(plan_tile_scan_kernel, dim3(1), dim3(PLAN_WG), 0, st, E + n, ntile);
