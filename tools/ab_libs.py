@@ -4,7 +4,8 @@ interleaved run by run (so clock drift and box-to-box spread fall on all of them
 per build and workload as one JSON line.
     python tools/ab_libs.py --libs new=nldsc_amd/libnldsc_amd.so old=ab_libs/r2base.so --workload c2 c3 --runs 8
 Workloads: c2 (N 50 000, additive only), c3 (N 315 599, add+dom, 1 % missing), c3m0 (c3 without missing calls),
-c5 (1000 kb windows, 288 bp per SNP, missing-free; --c5-snp SNPs)."""
+c5 (1000 kb windows, 288 bp per SNP, missing-free; --c5-snp SNPs), c3r0of8 (rank 0's owned range + halo of C3 over 8
+GPUs, as bench.py --rehearse 0/8)."""
 import argparse
 import json
 import os
@@ -19,6 +20,7 @@ WORKLOADS = {  # name: (N, M, length_cm, window, missing, additive_only)
     "c3": (315_599, 80_000, 280.0, 1.0, 0.01, False),
     "c3m0": (315_599, 80_000, 280.0, 1.0, 0.0, False),
     "c5": (315_599, None, None, 1.0e6, 0.0, False),
+    "c3r0of8": (315_599, 80_000, 280.0, 1.0, 0.01, False),  # rank 0's shard of the 8-GPU strong-scaling run
 }
 
 
@@ -43,6 +45,14 @@ def main():
         buf, pos = synth.device_bed(M, N, seed=7, length_cm=L, missing=miss)
         if wl == "c5":
             pos = np.round(pos)
+        own = None
+        if wl == "c3r0of8":
+            from nldsc_amd.distributed import halo_range, shard_ranges
+            lo, hi = shard_ranges(pos, w, 8)[0]
+            ha, hb = halo_range(pos, w, (lo, hi))
+            nb = (N + 3) // 4
+            buf = torch.cat([buf[:3], buf[3 + ha * nb:3 + hb * nb]])
+            pos, M, own = pos[ha:hb], hb - ha, (lo - ha, hi - ha)
         flags = _lib.FLAG_ADDITIVE_ONLY if add else 0
         engines = {}
         for name, spec in libs.items():
@@ -66,7 +76,7 @@ def main():
         ref = None
         for r in range(a.runs + 1):
             for name, e in engines.items():
-                got = e.run(w, 1e-4, 1e-5, 1.0 / M, pos, flags=flags)
+                got = e.run(w, 1e-4, 1e-5, 1.0 / (M if own is None else 80_000), pos, flags=flags, own=own)
                 t = e.timings()
                 res[name]["kernel"] = t.get("band_kernel")
                 if r > 0:  # run 0 is the warmup
