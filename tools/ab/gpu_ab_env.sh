@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of engine environment knobs on one box: each "label:ENV=VAL:bench args" runs bench.py with that
 # variable set, into gpurun_out/<tag>/bench_<label>.json.
-#   gpurun --timeout 900 -- bash tools/gpu_ab_env.sh <tag> "c3on:NLDSC_REPLAY_OVERLAP=1:" "c3off:NLDSC_REPLAY_OVERLAP=0:" ...
+#   gpurun --timeout 900 -- bash tools/ab/gpu_ab_env.sh <tag> "c3on:NLDSC_REPLAY_OVERLAP=1:" "c3off:NLDSC_REPLAY_OVERLAP=0:" ...
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 T=${1:-ab}; shift
 O=gpurun_out/$T

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Counter passes over one bench workload, each pass in its own rocprofv3 run (rocprofv3 does not split counters
 # over passes: at most 8 SQ / 4 TCC / 2 GRBM per pass).  Output: gpurun_out/<tag>/<label>_p<k>/ (+ a per-kernel sum).
-#   gpurun --timeout 900 -- bash tools/gpu_pmc_probe.sh <tag> <label> "<bench args>" "<counters pass 1>" ["<pass 2>" ...]
+#   gpurun --timeout 900 -- bash tools/ab/gpu_pmc_probe.sh <tag> <label> "<bench args>" "<counters pass 1>" ["<pass 2>" ...]
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 T=$1; label=$2; args=$3; shift 3
 O=gpurun_out/$T

@@ -2,7 +2,7 @@
 # Where the band kernel's cycles go, per engine variant: for each "label:ENV=VAL:bench args" a timed bench
 # (--steps 10) and two rocprofv3 --pmc passes of a 1-step bench (SQ wave-cycle buckets + MFMA busy + clock;
 # FETCH_SIZE), each pass in its own run.  Output: gpurun_out/<tag>/<label>_{bench.json,sq,fetch}.
-#   gpurun --timeout 900 -- bash tools/gpu_stall_probe.sh <tag> "c3:NLDSC_T2=1:" "c3all:NLDSC_T2=2:" ...
+#   gpurun --timeout 900 -- bash tools/ab/gpu_stall_probe.sh <tag> "c3:NLDSC_T2=1:" "c3all:NLDSC_T2=2:" ...
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 T=${1:-stall}; shift
 O=gpurun_out/$T

@@ -3,7 +3,7 @@
 #   genome  - the 22-autosome whole genome from .bed files (tools/e2e_genome.py --autosomes)
 #   c2      - C2 bench + SQ instruction-mix / wait counters of its band kernel (verdict r03 item 5)
 #   f32     - the fp32 MFMA GEMM path on C3 (north_star's GEMM) + its rocprofv3 kernel statistics (item 7)
-#   gpurun --timeout 1200 -- bash tools/gpu_study_batch.sh <tag> genome c2 f32
+#   gpurun --timeout 1200 -- bash tools/ab/gpu_study_batch.sh <tag> genome c2 f32
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/${1:-batch}; shift
 mkdir -p $O

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Bench lines of every BASELINE config the repo measures on one GPU, on the current kernels:
-#   gpurun --timeout 1200 -- bash tools/gpu_sweep.sh <tag>   ->  gpurun_out/<tag>/<name>.json
+#   gpurun --timeout 1200 -- bash tools/ab/gpu_sweep.sh <tag>   ->  gpurun_out/<tag>/<name>.json
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 T=${1:-sweep}
 O=gpurun_out/$T
