@@ -197,7 +197,7 @@ struct nldsc_engine {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t plan_stream = nullptr;  // the GPU schedule runs here, beside the count kernel
-    hipEvent_t ev_pos = nullptr;        // positions uploaded (the schedule's only input)
+    hipEvent_t ev_pos = nullptr;        // positions uploaded and their window edges searched (the schedule's input)
     hipEvent_t ev[6] = {};
     hipEvent_t ev_dbg[2] = {};  // $NLDSC_DEBUG_TIMING: after the super-item launch, before the single-block launches
     bool debug_timing = false;
