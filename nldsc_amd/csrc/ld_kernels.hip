@@ -2505,7 +2505,7 @@ __global__ void finalize_kernel(const int* __restrict__ Lw, const double* __rest
 
 // Owned slice of the score table for the multi-GPU gather (nldsc_engine_run_device): row k of `table` = l2, l2d,
 // maf, rstd, WSA, WSD, WSDE (doubles), column c = SNP own_lo + c, NaN past the slice; and the metric's pair counts
-// (positive window sizes) summed per wave, one 64-bit atomic per wave.
+// (positive window sizes) summed per workgroup, one 64-bit atomic per workgroup and counter.
 __global__ void __launch_bounds__(256) pack_table_kernel(const double* __restrict__ l2, const double* __restrict__ l2d,
                                                          const double* __restrict__ maf,
                                                          const double* __restrict__ rstd,
@@ -2531,13 +2531,23 @@ __global__ void __launch_bounds__(256) pack_table_kernel(const double* __restric
         table[6 * (size_t)width + c] = in ? (double)x : qnan;
     }
 sum:
+    // one 64-bit atomic pair per workgroup (per wave, the 1 250 waves of an 80 000-SNP table serialised on the two
+    // counters: 31 us of the kernel)
+    __shared__ unsigned long long wsum[2][4];
     for (int o = 32; o > 0; o >>= 1) {
         sa += __shfl_down(sa, o, 64);
         sd += __shfl_down(sd, o, 64);
     }
-    if ((threadIdx.x & 63) == 0 && (sa | sd)) {
-        atomicAdd(&sums[0], sa);
-        atomicAdd(&sums[1], sd);
+    if ((threadIdx.x & 63) == 0) {
+        wsum[0][threadIdx.x >> 6] = sa;
+        wsum[1][threadIdx.x >> 6] = sd;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        sa = wsum[0][0] + wsum[0][1] + wsum[0][2] + wsum[0][3];
+        sd = wsum[1][0] + wsum[1][1] + wsum[1][2] + wsum[1][3];
+        if (sa) atomicAdd(&sums[0], sa);
+        if (sd) atomicAdd(&sums[1], sd);
     }
 }
 
