@@ -120,13 +120,21 @@ def test_bench_force_dist_rccl_one_rank():
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--force-dist", "--no-cpu", "--no-file",
-                        "--steps", "2", "--warmup", "1", "--n-snp", "6000", "--n-org", "20000", "--length-cm", "21"],
-                       cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
-    assert p.returncode == 0, p.stderr[-3000:]
-    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    def bench(*extra):
+        p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--no-cpu", "--no-file", "--steps", "3",
+                            "--warmup", "1", "--n-snp", "6000", "--n-org", "20000", "--length-cm", "21", *extra],
+                           cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-3000:]
+        return json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    d = bench("--force-dist")
     assert d["n_gpus"] == 1 and d["value"] > 0 and "RCCL" in d["config"]["parallelism"], d
+    assert "side stream" in d["config"]["parallelism"], d  # each step's gather beside the next step's compute
     assert d["stages_ms"]["gather_ms"] >= 0 and d["per_rank"][0]["owned_snps"] == 6000
+    # the overlapped gather, the sequential one and the one-process run: the same table
+    seq, one = bench("--force-dist", "--no-gather-overlap"), bench()
+    assert "side stream" not in seq["config"]["parallelism"], seq
+    assert d["table_digest"] == seq["table_digest"] == one["table_digest"], (d["table_digest"], seq["table_digest"],
+                                                                              one["table_digest"])
 
 
 SPLIT_SCRIPT = r'''
