@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--workload", nargs="+", default=["c3"], choices=sorted(WORKLOADS))
     ap.add_argument("--runs", type=int, default=8)
     ap.add_argument("--c5-snp", type=int, default=300_000)
+    ap.add_argument("--no-check", action="store_true", help="study builds whose outputs differ (timing only)")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
@@ -86,7 +87,7 @@ def main():
                         res[name]["stages"][k].append(t[k])
                 if ref is None:
                     ref = got
-                else:  # every build must agree on the integer outputs
+                elif not a.no_check:  # every build must agree on the integer outputs
                     for k in ("l2_ws", "l2d_ws"):
                         assert np.array_equal(got[k], ref[k]), (wl, name, k)
         out[wl] = {name: {"band_ms_median": float(np.median(v["band"])), "band_ms_min": float(np.min(v["band"])),
