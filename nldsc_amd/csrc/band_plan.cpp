@@ -35,6 +35,13 @@ void replay_windows(const double* pos, const uint8_t* flags, int n, double w, in
 }
 
 // Positions non-decreasing over the used SNPs (pos >= 0)?
+// every position >= 0 (no NaN) and non-decreasing: one branch-free pass (the GPU schedule's condition)
+bool positions_nonneg_sorted(const double* pos, int M) {
+    int bad = M > 0 && !(pos[0] >= 0.0);
+    for (int j = 1; j < M; ++j) bad |= !(pos[j] >= 0.0) | (pos[j] < pos[j - 1]);
+    return !bad;
+}
+
 bool positions_sorted(const double* pos, int M) {
     double last = -1.0;
     for (int j = 0; j < M; ++j)

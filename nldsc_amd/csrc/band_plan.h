@@ -15,6 +15,7 @@ static_assert(sizeof(PlanItem) == 16, "PlanItem is the device int4");
 
 void replay_windows(const double* pos, const uint8_t* flags, int n, double w, int* L, int* R);
 bool positions_sorted(const double* pos, int M);
+bool positions_nonneg_sorted(const double* pos, int M);
 void plan_items(const double* pos, const uint8_t* flags, int M, double w, const int* L, const int* R, int own_begin,
                 int own_end, int max_nc, std::vector<PlanItem>& out);
 void order_items_tiled(std::vector<PlanItem>& items, int nblk, int R, int C, std::vector<PlanItem>& scratch);

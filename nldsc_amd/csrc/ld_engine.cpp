@@ -741,9 +741,9 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
 
     // band schedule: on the GPU when every position is >= 0 and sorted (the kernels run ahead of the
     // count and the host only waits for two counters), else the host replay of the reference's pointers
-    const bool sorted = nldsc::positions_sorted(p->positions, M);
-    const bool gpu_plan = e->gpu_plan && sorted && max_nc == 1 &&
-                          std::all_of(p->positions, p->positions + M, [](double x) { return x >= 0.0; });
+    const bool nonneg_sorted = nldsc::positions_nonneg_sorted(p->positions, M);
+    const bool sorted = nonneg_sorted || nldsc::positions_sorted(p->positions, M);
+    const bool gpu_plan = e->gpu_plan && nonneg_sorted && max_nc == 1;
     // the 2 x 2 block-pair workgroups: fp4, unsegmented rows, GPU plan, and no K-split (choose_ksplit below); with
     // super-item routing (t2 modes 1 and 3) only when a missing-free block exists in this run's sample order (routing
     // takes none otherwise: C3 / C2 synthetic data, 1 % missing — the super plan, the compaction and two empty quad

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/nldsc_ld.h"
+#include "../../nldsc_amd/csrc/band_plan.h"
 
 static int fails = 0;
 #define CHECK(c, ...)                                            \
@@ -160,9 +161,26 @@ static void check_tsv(std::mt19937_64& rng, int iter) {
     CHECK(small < 0, "undersized buffer accepted (%lld)", (long long)small);
 }
 
+// the GPU schedule's condition in one pass: equal to "sorted among the non-negative ones and all non-negative"
+static void check_sorted(std::mt19937_64& rng, int iter) {
+    const int M = (int)(rng() % 200);
+    std::vector<double> P(M);
+    double x = 0;
+    for (int j = 0; j < M; ++j) {
+        x += (double)(rng() % 3);
+        const int kind = (int)(rng() % 60);
+        P[j] = kind == 0 ? -1.0 : kind == 1 ? std::nan("") : kind == 2 ? x - 2.5 : x;
+    }
+    bool all_nonneg = true;
+    for (double v : P) all_nonneg &= v >= 0.0;
+    const bool expect = all_nonneg && nldsc::positions_sorted(P.data(), M);
+    CHECK(nldsc::positions_nonneg_sorted(P.data(), M) == expect, "positions_nonneg_sorted (M=%d, iter %d)", M, iter);
+}
+
 int main() {
     std::mt19937_64 rng(2024);
     for (int it = 0; it < 600; ++it) check_plan(rng, it);
+    for (int it = 0; it < 2000; ++it) check_sorted(rng, it);
     // argument checks of the C ABI
     double p1[2] = {0, 1};
     uint8_t f1[2] = {1, 1};
@@ -174,6 +192,6 @@ int main() {
         std::fprintf(stderr, "%d failures\n", fails);
         return 1;
     }
-    std::printf("plan_tsv_check OK (600 plans, 400 tables)\n");
+    std::printf("plan_tsv_check OK (600 plans, 2000 position checks, 400 tables)\n");
     return 0;
 }
