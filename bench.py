@@ -217,6 +217,58 @@ def file_wall_clock(bed_host: bytes, n_snp, n_org, w, maf, std_thr, rsq, pos, fl
     return out
 
 
+def extra_records(eng, img_dev, M, N, w, args, rsq, pos, flags, res, res_arrays) -> dict:
+    """After the timed region (N = 1, C3):
+    fp32_path — the north star's fp32 MFMA GEMM (band_kernel, v_mfma_f32_32x32x2_f32) on the same resident rows, 3 timed
+      runs after one warm-up: band time, its fraction of the 157.3 TF fp32 MFMA peak on the §8(d3) basis, and the table
+      digest (its window counts must equal the default path's);
+    oneshot_gpu_ms — what one `calculate(params)` costs per chromosome on the GPU beside the file read: the per-load
+      kernels (the rows of a device image placed, oriented and scanned for missing calls: nldsc_engine_load_bed_device)
+      and one run, wall clock around both (synchronous calls)."""
+    import torch
+    from nldsc_amd import _lib
+    out = {}
+    f32_flags = (flags & ~_lib.FLAG_EXACT_F4) | _lib.FLAG_FP32
+    r = None
+    eng.run(w, args.maf, args.std_thr, rsq, pos, flags=f32_flags)
+    tims, t0 = [], time.perf_counter()
+    for _ in range(3):
+        r = eng.run(w, args.maf, args.std_thr, rsq, pos, flags=f32_flags)
+        tims.append(eng.timings())
+    wall = (time.perf_counter() - t0) / 3
+    band = float(np.mean([t["band_ms"] for t in tims]))
+    flop = tims[-1]["flop_alg"]
+    dig = table_digest(r)
+    ref = res_arrays  # the default path's last table (same rows, same parameters)
+    ok = np.asarray(ref["l2_ws"]) > 0
+    cmp = {"l2_ws_equal": bool(np.array_equal(r["l2_ws"], ref["l2_ws"])),
+           "l2d_ws_equal": bool(np.array_equal(r["l2d_ws"], ref["l2d_ws"])),
+           # WSDE counts r2adj > rsq_thr: pairs within fp32 rounding of the threshold may flip (SURVEY Appendix B)
+           "l2d_wse_snps_differing": int(np.sum(np.asarray(r["l2d_wse"]) != np.asarray(ref["l2d_wse"]))),
+           "l2_max_abs_diff": float(np.max(np.abs(np.asarray(r["l2"])[ok] - np.asarray(ref["l2"])[ok])))
+           if ok.any() else 0.0}
+    out["fp32_path"] = {
+        "kernel": "band_kernel<true, 2> (v_mfma_f32_32x32x2_f32 on fp32 standardised values, LDS-staged lookup of the "
+                  "2-bit rows)", "steps": 3, "ms_per_step": round(1e3 * wall, 3), "band_ms": round(band, 3),
+        "achieved_tflops": flop / (band * 1e-3) / 1e12, "peak_tflops": FP32_MFMA_PEAK_TFLOPS,
+        "frac": flop / (band * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
+        "pairs_per_s": tims[-1]["pairs"] / wall, "table_digest": dig,
+        "counts_equal_default_path": dig["counts_sha16"] == res["table_digest"]["counts_sha16"],
+        "vs_default_path": cmp, "l2_sum_delta_vs_default": dig["l2_sum"] - res["table_digest"]["l2_sum"]}
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.load_bed_device(img_dev.data_ptr(), img_dev.numel(), M, N)
+    t1 = time.perf_counter()
+    eng.run(w, args.maf, args.std_thr, rsq, pos, flags=flags)
+    t2 = time.perf_counter()
+    out["oneshot_gpu_ms"] = {"total": round(1e3 * (t2 - t0), 3), "load": round(1e3 * (t1 - t0), 3),
+                             "run": round(1e3 * (t2 - t1), 3),
+                             "what": "nldsc_engine_load_bed_device (rows placed in the resident layout, oriented, scanned "
+                                     "for missing calls) + one run, from a .bed image already in HBM: the GPU side of "
+                                     "one calculate(params) per chromosome (the file read apart)"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -264,6 +316,9 @@ def main():
     ap.add_argument("--force-dist", action="store_true",
                     help="create the process group and run the sharded path (owned range, device table, collective "
                          "gather) even with one rank: the RCCL code of an N-GPU run rehearsed on one GPU")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the default line's extra records after the timed region (N = 1, C3): the fp32 MFMA path "
+                         "(fp32_path) and the one-shot load + run GPU time (oneshot_gpu_ms)")
     ap.add_argument("--concurrent", type=int, default=3,
                     help="c4: chromosomes computed at once per GPU (host threads, one engine stream each)")
     args = ap.parse_args()
@@ -365,35 +420,55 @@ def main():
             imported = torch.zeros(6 * max(n_recv, 1), dtype=torch.int64, device=table.device)
     else:
         eng.load_bed_device(buf.data_ptr(), buf.numel(), M, N)
+    if not split:
+        # the run's positions and result arrays in pinned host memory (nldsc_host_alloc): the positions go up by DMA in
+        # place and the GPU writes the results into the arrays themselves (include/nldsc_ld.h; ordinary numpy arrays work
+        # too, through the engine's landing buffer and a host copy)
+        pos_p = _lib.pinned_empty(M, np.float64)
+        pos_p[:] = pos
+        pos = pos_p
+        out = _lib.alloc_result(M, pinned=True)[0]
     bed_host = None
     want_file = rank == 0 and not use_dist and not args.no_file and args.workload == "c3"
     if rank == 0 and not use_dist and (not args.no_cpu or want_file):
         bed_host = buf.cpu().numpy().tobytes()
+    # (N = 1: the device image stays for the one-shot measurement after the timed region)
+    want_extra = rank == 0 and not use_dist and not args.no_extra and args.workload == "c3" and args.path == "f4"
+    img_dev = buf if want_extra else None
     del buf
     torch.cuda.empty_cache()
     log(f"[rank {rank}] data ready ({(3 + M * ((N + 3) // 4)) / 1e9:.2f} GB .bed image) in "
         f"{time.perf_counter() - t:.1f} s")
     w, rsq = args.window_cm, 1.0 / M
-    out = None
+    out = out if not split else None
     n_step = 0
+    gath = []  # overlapped gathers: (step, start event, end event) on gstream, read after the timed region
 
     def step():
         nonlocal out, n_step
         if split and overlap:
             cur = n_step % 2
             n_step += 1
+            tw = time.perf_counter()
             if gdone[cur] is not None:
                 gdone[cur].synchronize()  # the gather of step k - 2 has read this table buffer
+            wait_ms = 1e3 * (time.perf_counter() - tw)
             eng.run_device(w, args.maf, args.std_thr, rsq, pos, tables[cur], own=own_rel, flags=flags)
             tim = eng.timings()
             tg = time.perf_counter()
             with torch.cuda.stream(gstream):
+                # the gather's own GPU time (RCCL all-gather, rank 0's assembly and D2H) between two events on gstream,
+                # read after the timed region (gather_ms); the host's enqueue time apart (gather_enqueue_ms)
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record(gstream)
                 full = gather_table(tables[cur], spans, M, out=gbufs[cur], raw=True, slot=cur, sync=False)
-                ev = torch.cuda.Event()
+                ev = torch.cuda.Event(enable_timing=True)
                 ev.record(gstream)
             gdone[cur] = ev
+            gath.append((n_step - 1, e0, ev))
             out = full if full is not None else out  # (rank 0: read after the closing synchronize)
-            tim["gather_ms"] = 1e3 * (time.perf_counter() - tg)  # (the enqueue only)
+            tim["gather_enqueue_ms"] = 1e3 * (time.perf_counter() - tg)
+            tim["gather_wait_ms"] = wait_ms  # this step's wait for the gather of step k - 2
             return tim
         if split:  # owned slice of the one chromosome, then the table assembled on rank 0 (RCCL over xGMI)
             if plan is not None:  # (a rehearsal of one rank adds a zero block in place of its neighbour's)
@@ -427,12 +502,15 @@ def main():
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
+    gath.clear()
     t0 = time.perf_counter()
     tims = [step() for _ in range(args.steps)]
     torch.cuda.synchronize()
     if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    for (k, e0, e1), tim in zip(gath, tims):  # overlapped gathers: GPU time on gstream (all-gather + assembly + D2H)
+        tim["gather_ms"] = float(e0.elapsed_time(e1))
     el = torch.tensor([elapsed], dtype=torch.float64, device=coll)
     pairs_step = torch.tensor([tims[-1]["pairs"]], dtype=torch.float64, device=coll)
     if use_dist:
@@ -444,7 +522,9 @@ def main():
     mine = torch.tensor([float(np.mean([x["band_ms"] for x in tims])),
                          float(np.mean([x.get("gather_ms", 0.0) for x in tims])),
                          float(np.mean([x["total_ms"] for x in tims])), float(tims[-1]["pairs"]),
-                         float(own[1] - own[0])], dtype=torch.float64, device=coll)
+                         float(own[1] - own[0]), float(np.mean([x.get("gather_enqueue_ms", 0.0) for x in tims])),
+                         float(np.mean([x.get("gather_wait_ms", 0.0) for x in tims]))],
+                        dtype=torch.float64, device=coll)
     per_rank = [mine]
     if use_dist:
         per_rank = [torch.empty_like(mine) for _ in range(world)]
@@ -542,11 +622,22 @@ def main():
             "roofline": roof,
             "stages_ms": stages,
             "per_rank": [dict(rank=g, band_ms=round(float(v[0]), 3), gather_ms=round(float(v[1]), 3),
-                              engine_ms=round(float(v[2]), 3), pairs=int(v[3]), owned_snps=int(v[4]))
+                              engine_ms=round(float(v[2]), 3), pairs=int(v[3]), owned_snps=int(v[4]),
+                              **({"gather_enqueue_ms": round(float(v[5]), 3), "gather_wait_ms": round(float(v[6]), 3)}
+                                 if overlap else {}))
                          for g, v in enumerate(x.cpu() for x in per_rank)],
+            **({"rccl_world": dist.get_world_size(), "collectives_backend": dist.get_backend()} if use_dist else {}),
+            **({"gather_note": "gather_ms: each step's score-table gather (RCCL all-gather, rank 0's assembly and its "
+                               "D2H copy) timed with HIP events on the side stream it runs on, beside the next step's "
+                               "compute; gather_wait_ms: the host's wait for the gather two steps back before reusing its "
+                               "buffer; gather_enqueue_ms: the host time to enqueue it"} if overlap else {}),
             "cpu_baseline": None,
             "table_digest": table_digest(out),
         }
+    if want_extra:
+        res.update(extra_records(eng, img_dev, M, N, w, args, rsq, pos, flags, res,
+                                 {k: np.array(v) for k, v in out.items()}))
+        del img_dev
     if want_file:
         log("[rank 0] wall clock from a PLINK file ...")
         res.update(file_wall_clock(bed_host, M, N, w, args.maf, args.std_thr, rsq, pos, flags))

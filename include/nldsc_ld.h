@@ -51,8 +51,7 @@ extern "C" {
                                             not small against a nearly constant vector: the fp32 mean does not
                                             centre it, and a residual without hom-A1 calls is exactly constant
                                             (std 0) but rounding noise in the reference, often above --std-thr */
-/* None of EXACT_F4, EXACT_I8, FP32: the engine default, EXACT_F4 ($NLDSC_BAND_MODE = f4 | i8 | f32
- * overrides it). */
+/* None of EXACT_F4, EXACT_I8, FP32: the engine default, EXACT_F4 (engine option "band_mode" overrides it). */
 
 typedef struct nldsc_ld_params {
     const char* bedfile;      /* LDScoreParams::bedfile   (data.h:34) */
@@ -90,6 +89,28 @@ typedef struct nldsc_engine nldsc_engine;
 int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t errlen);
 void nldsc_engine_destroy(nldsc_engine* e);
 
+/* Engine options (no reference counterpart: the schedule and kernel choice of this engine; every setting gives the
+ * same results, which the GPU tests compare).  Read at each run (orient: at each load); NLDSC_E_ARG for an unknown
+ * name or a value out of range.  Defaults in brackets.
+ *   band_mode    default correlation path when a run's flags name none: 0 fp32, 1 exact int8, [2] exact fp4
+ *   gpu_plan     [1] band schedule on the GPU for sorted non-negative positions; 0 the host replay always
+ *   orient       [1] store rows minor-homozygote-as-00 at load (the exact kernels' operands mostly zero)
+ *   ksplit       [1] K-split small launches (a rank's shard of one chromosome)
+ *   t2           super-item kernels for missing-free blocks: 0 none, 1 2x2 routed, 2 2x2 for all, [3] 4x4 quad
+ *   band_rounds  [1] single-block fp4 band in launches of one round of wave slots; 0 one launch
+ *   f4_nc2       [1] additive-only fp4 items of two column blocks; 0 single block pairs
+ *   q_rounds     [1] quad super-items in launches of one workgroup per CU; 0 one launch
+ *   defer_rep    [1] K loops of items holding a replayed rare variant in the main launch; 0 a later KC launch
+ *   debug_timing [0] per-run stage timings on stderr */
+int nldsc_engine_set_option(nldsc_engine* e, const char* name, int64_t value, char* err, size_t errlen);
+
+/* Page-locked host memory mapped into every device's address space (hipHostMalloc), NULL on failure; free with
+ * nldsc_host_free (which ignores pointers it did not hand out).  A host-result run whose seven result arrays (owned
+ * slices) all lie in such buffers is written by the GPU directly — no landing buffer, no host copies — and positions
+ * there are uploaded by DMA in place. */
+void* nldsc_host_alloc(size_t bytes);
+void nldsc_host_free(void* p);
+
 /* Make a .bed image resident on the engine's device.  `bed` is the complete file content
  * (3 magic bytes + n_snp rows of ceil(n_org/4) bytes), in host memory (_host) or in device
  * memory of the engine's device (_device, e.g. a torch tensor's data pointer; copied).
@@ -105,7 +126,8 @@ int nldsc_engine_load_bed_device(nldsc_engine* e, const void* bed, size_t len, i
 /* Compute LD scores for the SNPs with index in [own_begin, own_end) (position sharding:
  * each GPU owns a contiguous SNP range and recomputes the pairs it shares with its
  * neighbours' ranges, so no partial sums cross GPUs).  Entries of `r` outside the owned
- * range are left untouched.  p->bedfile is ignored (the loaded image is used). */
+ * range are left untouched.  p->bedfile is ignored (the loaded image is used).  `r`'s arrays
+ * may be ordinary host memory or nldsc_host_alloc buffers (written by the GPU in place). */
 int nldsc_engine_run(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32_t own_end,
                      nldsc_ld_result* r, char* err, size_t errlen);
 
@@ -169,7 +191,7 @@ int nldsc_engine_band_tail_ksplit(const nldsc_engine* e);
 #define NLDSC_BAND_F4_KSPLIT 4
 #define NLDSC_BAND_F4_2X2 5
 #define NLDSC_BAND_F4_ROUTED 6
-#define NLDSC_BAND_F4_QUAD 7 /* $NLDSC_T2=3: missing-free 4x4 super-items in the quad workgroups (64x64 tiles per
+#define NLDSC_BAND_F4_QUAD 7 /* option t2 = 3: missing-free 4x4 super-items in the quad workgroups (64x64 tiles per
                                 wave), the rest in the single-block kernel */
 int nldsc_engine_band_kernel(const nldsc_engine* e);
 

@@ -32,7 +32,7 @@ EXPORTED = (
     "nldsc_synth_bed_device", "nldsc_engine_path", "nldsc_plan_band", "nldsc_engine_load_bed_file_range",
     "nldsc_format_scores", "nldsc_engine_ksplit", "nldsc_engine_band_kernel", "nldsc_engine_band_round_items",
     "nldsc_engine_band_tail_ksplit", "nldsc_engine_run_device", "nldsc_engine_run_device_split",
-    "nldsc_engine_run_device_finish",
+    "nldsc_engine_run_device_finish", "nldsc_engine_set_option", "nldsc_host_alloc", "nldsc_host_free",
 )
 
 
@@ -116,11 +116,19 @@ def lib(path: str | None = None) -> ctypes.CDLL:
         if path == LIB_PATH or hasattr(L, "nldsc_engine_load_bed_file_range"):
             L.nldsc_engine_load_bed_file_range.argtypes = [vp, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32,
                                                            ctypes.c_int32, ctypes.c_int32] + c_err
+        if hasattr(L, "nldsc_engine_set_option"):
+            L.nldsc_engine_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64] + c_err
+        if hasattr(L, "nldsc_host_alloc"):
+            L.nldsc_host_alloc.restype = vp
+            L.nldsc_host_alloc.argtypes = [ctypes.c_size_t]
+            L.nldsc_host_free.restype = None
+            L.nldsc_host_free.argtypes = [vp]
         L.nldsc_synth_bed_device.argtypes = [ctypes.c_int32, vp, ctypes.c_int32, ctypes.c_int32,
                                              ctypes.POINTER(ctypes.c_float), ctypes.c_float, ctypes.c_float,
                                              ctypes.c_uint64] + c_err
         for name in EXPORTED:
-            if name not in ("nldsc_version", "nldsc_device_count", "nldsc_engine_destroy") and hasattr(L, name):
+            if name not in ("nldsc_version", "nldsc_device_count", "nldsc_engine_destroy", "nldsc_host_alloc",
+                            "nldsc_host_free") and hasattr(L, name):
                 getattr(L, name).restype = ctypes.c_int
         if hasattr(L, "nldsc_format_scores"):
             L.nldsc_format_scores.restype = ctypes.c_int64
@@ -142,11 +150,45 @@ def errbuf():
     return ctypes.create_string_buffer(1024)
 
 
-def alloc_result(n: int):
-    """numpy arrays + the C struct pointing at them."""
-    arrs = dict(l2=np.full(n, np.nan), l2d=np.full(n, np.nan), maf=np.full(n, np.nan),
-                residuals_std=np.full(n, np.nan), l2_ws=np.full(n, -1, np.int32),
-                l2d_ws=np.full(n, -1, np.int32), l2d_wse=np.full(n, -1, np.int32))
+class _Pinned:
+    """Owner of one nldsc_host_alloc buffer (freed with the last numpy view of it)."""
+
+    def __init__(self, L, ptr: int, nbytes: int):
+        self._L, self.ptr, self.nbytes = L, ptr, nbytes
+
+    def __del__(self):
+        if self.ptr:
+            self._L.nldsc_host_free(ctypes.c_void_p(self.ptr))
+            self.ptr = 0
+
+
+def pinned_empty(n: int, dtype) -> np.ndarray:
+    """An uninitialised numpy array in page-locked, device-mapped host memory (nldsc_host_alloc).  Result arrays
+    there are written by the GPU directly (no landing buffer, no host copy) and positions there are read by DMA in
+    place.  Falls back to an ordinary array when the library cannot allocate one (no HIP device)."""
+    dt = np.dtype(dtype)
+    nbytes = max(int(n), 1) * dt.itemsize
+    L = lib()
+    ptr = L.nldsc_host_alloc(nbytes) if hasattr(L, "nldsc_host_alloc") else None
+    if not ptr:
+        return np.empty(n, dt)
+    owner = _Pinned(L, ptr, nbytes)
+    raw = (ctypes.c_char * nbytes).from_address(ptr)
+    raw._owner = owner  # the ctypes view keeps the buffer alive; numpy keeps the view alive (its .base)
+    return np.frombuffer(raw, dtype=dt, count=int(n))
+
+
+def alloc_result(n: int, pinned: bool = False):
+    """numpy arrays + the C struct pointing at them (pinned: in nldsc_host_alloc memory, see pinned_empty)."""
+    if pinned:
+        arrs = {k: pinned_empty(n, np.float64) for k in ("l2", "l2d", "maf", "residuals_std")}
+        arrs.update({k: pinned_empty(n, np.int32) for k in ("l2_ws", "l2d_ws", "l2d_wse")})
+        for k, v in arrs.items():
+            v.fill(np.nan if v.dtype == np.float64 else -1)
+    else:
+        arrs = dict(l2=np.full(n, np.nan), l2d=np.full(n, np.nan), maf=np.full(n, np.nan),
+                    residuals_std=np.full(n, np.nan), l2_ws=np.full(n, -1, np.int32),
+                    l2d_ws=np.full(n, -1, np.int32), l2d_wse=np.full(n, -1, np.int32))
     d, i = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)
     res = Result(arrs["l2"].ctypes.data_as(d), arrs["l2d"].ctypes.data_as(d), arrs["maf"].ctypes.data_as(d),
                  arrs["residuals_std"].ctypes.data_as(d), arrs["l2_ws"].ctypes.data_as(i),

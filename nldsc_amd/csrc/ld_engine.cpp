@@ -21,10 +21,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <immintrin.h>
 
 #include "../../include/nldsc_ld.h"
 #include "band_plan.h"
@@ -151,10 +154,29 @@ class CopyPool {
             }
         });
     }
-    // f(part, parts) for part = 0 .. parts - 1 (parts = kCopyThreads + 1), part 0 on the calling thread
+    // f(part, parts) for part = 0 .. parts - 1 (parts = kCopyThreads + 1), part 0 on the calling thread.  Helper
+    // threads start on first use; if the system refuses a thread, every part runs on the calling thread from then on
+    // (a std::system_error must not cross the C ABI: ADVICE r04)
     void parallel(const std::function<void(int, int)>& f) {
-        if (th_.empty())
-            for (int t = 0; t < kCopyThreads; ++t) th_.emplace_back([this, t] { loop(t + 1); });
+        if (th_.empty() && !serial_) {
+            try {
+                for (int t = 0; t < kCopyThreads; ++t) th_.emplace_back([this, t] { loop(t + 1); });
+            } catch (const std::exception&) {
+                {
+                    std::lock_guard<std::mutex> lk(mu_);
+                    stop_ = true;
+                }
+                cv_.notify_all();
+                for (auto& t : th_) t.join();
+                th_.clear();
+                stop_ = false;
+                serial_ = true;
+            }
+        }
+        if (serial_) {
+            for (int p = 0; p <= kCopyThreads; ++p) f(p, kCopyThreads + 1);
+            return;
+        }
         {
             std::lock_guard<std::mutex> lk(mu_);
             job_ = &f;
@@ -189,7 +211,43 @@ class CopyPool {
     int pending_ = 0;
     uint64_t gen_ = 0;
     bool stop_ = false;
+    bool serial_ = false;
 };
+
+// Spin on a pinned word the GPU writes (a blocking event wait wakes the thread tens of microseconds late: the host waits
+// on the critical path of short runs), with a CPU pause per poll, for at most ~1 ms — then the caller's blocking event
+// wait takes over (a stalled plan no longer burns 2 s of a core that loaders and RCCL proxies share).
+bool spin_until_nonneg(volatile const int* w) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (*w < 0) {
+        _mm_pause();
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(1000)) return false;
+    }
+    return true;
+}
+
+// Pinned host buffers handed out by nldsc_host_alloc: a run whose result arrays (or positions) lie inside one is
+// written (read) by the GPU directly, without the engine's own landing buffer and host copies.
+std::mutex g_host_mu;
+std::map<uintptr_t, size_t> g_host_bufs;  // start -> bytes
+
+// device pointer of [p, p + bytes) when it lies inside one nldsc_host_alloc buffer, else nullptr
+void* registered_device_ptr(const void* p, size_t bytes) {
+    if (!p) return nullptr;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    uintptr_t base = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_host_mu);
+        auto it = g_host_bufs.upper_bound(a);
+        if (it == g_host_bufs.begin()) return nullptr;
+        --it;
+        if (a + bytes > it->first + it->second) return nullptr;
+        base = it->first;
+    }
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, reinterpret_cast<void*>(base), 0) != hipSuccess || !d) return nullptr;
+    return static_cast<uint8_t*>(d) + (a - base);
+}
 
 }  // namespace
 
@@ -204,18 +262,22 @@ struct nldsc_engine {
     hipEvent_t ev_plan = nullptr;  // GPU plan counters landed in h_meta
     hipEvent_t ev_stats = nullptr;   // SNP constants and replay flags written (the replay's inputs)
     hipEvent_t ev_replay = nullptr;  // replayed constants written (the KC launch and finalize wait on it)
+    // side stream: the rare-variant replay beside the band (ev_replay), then the issued-product count (ev_issued)
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t ev_issued = nullptr;
     // resident .bed image
     DevBuf<uint8_t> bed;      // resident rows, block-interleaved (ld_kernels.hip tile_off)
     DevBuf<uint8_t> stage_dev;  // loads: rows of the .bed layout on their way into `bed` (released after the load)
     DevBuf<uint8_t> lastb;  // each row's original last byte (the per-run count kernel masks a copy of it)
     DevBuf<uint8_t> flip;   // per SNP: resident row stores the swapped (00 <-> 11) coding
     DevBuf<uint8_t> row_miss;  // per SNP: bit 0 / 1 = a missing call among the reference's / PLINK's individual slots
-    bool orient = true;     // store rows minor-homozygote-as-00 at load (NLDSC_ORIENT=0: file coding)
+    DevBuf<uint32_t> miss_flags;  // (the load kernels' per-row word of the same flags)
+    bool orient = true;     // store rows minor-homozygote-as-00 at load (option "orient" 0: file coding)
     bool oriented = false;  // the resident image was oriented
     int32_t n_snp = 0, n_org = 0;
     // work buffers
 
-    DevBuf<int> counts, Lw, Rw, Aw, ws_acc;
+    DevBuf<int> counts, cparts, Lw, Rw, Aw, ws_acc;  // (cparts: the count kernel's per-part counts)
     // the per-SNP results, one allocation: L2, L2D, MAF, RSTD (fp64) then WSA, WSD, WSDE (int32), each M long, so the
     // owned slices come back in two strided copies (one when a run owns every SNP)
     DevBuf<double> res;
@@ -231,7 +293,7 @@ struct nldsc_engine {
     DevBuf<uint8_t> blk_rep;  // per 32-SNP block: holds a rare variant with replayed fp32 vectors (KC items)
     DevBuf<float> gram;       // K-split partial Gram tiles
     // rare-variant items of the single-block fp4 kernel, deferred: their Gram tiles (8192 floats per block pair), the
-    // block pairs, the slot counter (launch_band_f4 rep_gram; $NLDSC_DEFER_REP=0: the separate KC launch instead)
+    // block pairs, the slot counter (launch_band_f4 rep_gram; option "defer_rep" 0: the separate KC launch instead)
     DevBuf<float> rep_gram;
     DevBuf<int4> rep_items;
     DevBuf<int> rep_count;
@@ -243,31 +305,26 @@ struct nldsc_engine {
     bool split_dom = true;
     double* split_table = nullptr;
     double split_ms1 = 0.0;  // the first call's host time
-    bool ksplit_ok = true;    // $NLDSC_KSPLIT=0 disables the K-split
+    bool ksplit_ok = true;    // option "ksplit" 0 disables the K-split
     static constexpr int round_min = 1;  // round launches from this many rounds of single-block items on
     // deferred rare-variant Gram tiles: at most this many block-pair slots (32 KiB each: 2 GiB)
     size_t rep_gram_max_slots = (size_t)1 << 16;
-    bool replay_overlap = true;  // $NLDSC_REPLAY_OVERLAP=0 runs the rare-variant replay in line on the main stream
     int last_ksplit = 1;
     int last_round_items = 0;
     int last_tail_ksplit = 1;
-    // fp4 band kernels on the GPU plan ($NLDSC_T2): 3 (default) missing-free 4 x 4 super-items in the quad
+    // fp4 band kernels on the GPU plan (option "t2"): 3 (default) missing-free 4 x 4 super-items in the quad
     // workgroups (64 x 64 tiles per wave), the rest in the single-block kernel (C5 slice band -25 % against 1, the
     // others unchanged: profiles/r03_ab_t2_quad.json); 1 the same with missing-free 2 x 2 super-items in the 2 x 2
     // block-pair workgroups; 2 everything in the 2 x 2 workgroups; 0 single-block only
     int t2_mode = 3;
     // additive-only fp4 band in 32 x 64 tiles (column-block pair items, the row strip decoded once for two column
-    // blocks; $NLDSC_F4_NC2=0 turns it off): C2 band 2.85 -> 2.78 ms, one engine per process (r03_c2_nc2.json)
+    // blocks; option "f4_nc2" 0 turns it off): C2 band 2.85 -> 2.78 ms, one engine per process (r03_c2_nc2.json)
     bool f4_nc2 = true;
-    // single-block fp4 band in launches of one round of wave slots ($NLDSC_BAND_ROUNDS=0: one launch)
+    // single-block fp4 band in launches of one round of wave slots (option "band_rounds" 0: one launch)
     bool band_rounds = true;
+    bool band_persist = false;  // (study) the round launches as one persistent launch walking the rounds
     DevBuf<uint8_t> blk_miss;
-    DevBuf<uint8_t> blk_zero;  // additive-only quad runs: the routing array of the other kernels (all super-items routed)
-    // $NLDSC_QUAD_ADD=1 (study, off): additive-only runs send every 4 x 4 super-item to the quad kernel, those holding
-    // missing calls with the four additive products per pair — C2 band 2.29 -> 4.13 ms (profiles/r03_ab_quad_add_rejected.json:
-    // short rows, one wave per SIMD, whole 64 x 64 tiles at the band edges)
-    bool quad_add = false;
-    // quad super-items in launches of one workgroup per CU when there are at least 16 such rounds ($NLDSC_Q_ROUNDS=0:
+    // quad super-items in launches of one workgroup per CU when there are at least 16 such rounds (option "q_rounds" 0:
     // one launch): the workgroups on an XCD then stream their shared strips at nearby K offsets; C5 slice band
     // 351 -> 333 ms, C3 missing-free (6 rounds, below the threshold) 12.34 -> 12.51 ms (profiles/r03_ab_q_rounds.json)
     bool q_rounds = true;
@@ -284,7 +341,7 @@ struct nldsc_engine {
     HostPinned h_stage;  // pinned upload staging of the plan (L, R, items)
     HostPinned h_meta;   // GPU plan counters (items, diagonal items)
     HostPinned h_pos;    // pinned copy of the positions (the upload does not stall this thread)
-    HostPinned h_res;    // pinned landing buffer of the result copies (DMA, then host copies out)
+    HostPinned h_res;    // pinned landing buffer of host-result runs (the GPU writes it, then host copies out)
     CopyPool copies;     // the host copies out of h_res, split over threads
     // [0..1] device-table runs: sums of the positive WSA / WSD over the owned slice; [2] MFMA products issued
     DevBuf<unsigned long long> sums;
@@ -296,19 +353,20 @@ struct nldsc_engine {
     DevBuf<int> compact_tmp;
     HostPinned h_route;    // their count
     hipEvent_t ev_route = nullptr;
-    bool gpu_plan = true;  // band schedule on the GPU for non-negative sorted positions (NLDSC_GPU_PLAN=0: host)
+    bool gpu_plan = true;  // band schedule on the GPU for non-negative sorted positions (option "gpu_plan" 0: host)
     // timings of the last run
     double ms[6] = {0, 0, 0, 0, 0, 0};
     double flop_alg = 0, flop_issued = 0, pairs = 0, ops_alg_i8 = 0;
     int32_t n_band_items = 0;
     int last_path = 0;     // path of the last run: 0 fp32, 1 exact int8, 2 exact fp4
-    int band_mode = 2;     // default correlation path (NLDSC_BAND_MODE=f32|i8|f4): exact fp4
+    int band_mode = 2;     // default correlation path (option "band_mode" 0 fp32, 1 int8, 2 fp4): exact fp4
                            // (int8 from N = 2^27)
     int n_cu = 256;
 
     ~nldsc_engine() {
         (void)hipSetDevice(device);
-        bed.release(); stage_dev.release(); lastb.release(); flip.release(); row_miss.release(); counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
+        bed.release(); stage_dev.release(); lastb.release(); flip.release(); row_miss.release(); miss_flags.release();
+        counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
         res.release(); lut.release(); cst.release(); sflags.release(); pos.release();
         l2_acc.release(); l2d_acc.release(); items.release(); gram.release();
         rep_gram.release(); rep_items.release(); rep_count.release();
@@ -316,7 +374,10 @@ struct nldsc_engine {
         for (auto& e : ev_dbg) if (e) (void)hipEventDestroy(e);
         if (ev_plan) (void)hipEventDestroy(ev_plan);
         plan_counts.release(); plan_meta.release(); plan_rows.release();
-        plan_counts2.release(); plan_rows2.release(); items2.release(); blk_miss.release(); blk_zero.release(); sums.release();
+        plan_counts2.release(); plan_rows2.release(); items2.release(); blk_miss.release(); sums.release();
+        cparts.release();
+        if (copy_stream) (void)hipStreamDestroy(copy_stream);
+        if (ev_issued) (void)hipEventDestroy(ev_issued);
         if (stream) (void)hipStreamDestroy(stream);
         if (plan_stream) (void)hipStreamDestroy(plan_stream);
         if (ev_pos) (void)hipEventDestroy(ev_pos);
@@ -362,31 +423,33 @@ int use_device(int32_t device, int* resolved, char* err, size_t errlen) {
     return NLDSC_OK;
 }
 
-// device buffers of a resident image of n_snp rows (all rows, pitch padding, saved last bytes)
+// device buffers of a resident image of n_snp rows (all rows, pitch padding, saved last bytes, per-row flags)
 hipError_t alloc_image(nldsc_engine* e, int32_t n_snp, int32_t n_org) {
     e->n_snp = e->n_org = 0;  // no valid image until finish_image
+    e->oriented = e->orient;  // (the load's slices all use the orientation rule in force when it starts)
     hipError_t he = e->bed.ensure((size_t)padded_rows(n_snp) * (size_t)row_pitch(n_org));
     if (he == hipSuccess) he = e->lastb.ensure((size_t)n_snp);
     if (he == hipSuccess) he = e->flip.ensure((size_t)n_snp);
     if (he == hipSuccess) he = e->row_miss.ensure((size_t)n_snp);
+    if (he == hipSuccess) he = e->miss_flags.ensure((size_t)n_snp);
     return he;
 }
 
-// after the rows are copied in: save last bytes, pad, and mark the image valid
-hipError_t finish_image(nldsc_engine* e, int32_t n_snp, int32_t n_org) {
-    const int nb = n_org / 4 + (n_org % 4 > 0);
-    hipError_t he = nldsc::launch_pad_rows(e->bed.p, e->lastb.p, n_snp, padded_rows(n_snp), nb, row_pitch(n_org),
-                                           e->stream);
-    e->oriented = e->orient;
-    if (he == hipSuccess && e->oriented)
-        he = nldsc::launch_orient_rows(e->bed.p, e->lastb.p, n_snp, row_pitch(n_org), e->flip.p, e->stream);
-    // rows holding a missing call in either sample order (the last byte keeps its high / low N % 4 pairs)
-    const int rem = n_org % 4;
+// Rows [row0, row0 + n_rows) (whole 32-SNP blocks but for the image's last) of n_snp from a .bed slice in device memory
+// into the resident layout, oriented, last bytes saved, missing flags of both sample orders (the last byte keeps its
+// high / low N % 4 pairs) — one pass over the slice (ld_kernels.h launch_load_slice)
+hipError_t load_slice(nldsc_engine* e, const uint8_t* src, int32_t row0, int32_t n_rows, int32_t n_snp, int32_t n_org,
+                      hipStream_t st) {
+    const int nb = n_org / 4 + (n_org % 4 > 0), rem = n_org % 4;
     const uint32_t keep_compat = rem ? (0xFFu << (8 - 2 * rem)) & 0xFFu : 0xFFu;
     const uint32_t keep_strict = rem ? (1u << (2 * rem)) - 1u : 0xFFu;
-    if (he == hipSuccess)
-        he = nldsc::launch_row_missing(e->bed.p, e->lastb.p, n_snp, nb, row_pitch(n_org), keep_compat, keep_strict,
-                                       e->row_miss.p, e->stream);
+    return nldsc::launch_load_slice(src, nb, row0, n_rows, n_snp, e->bed.p, row_pitch(n_org), e->oriented, e->flip.p,
+                                    e->lastb.p, keep_compat, keep_strict, e->miss_flags.p, st);
+}
+
+// after every slice is in: per-row missing flags, the missing-free block counts, and mark the image valid
+hipError_t finish_image(nldsc_engine* e, int32_t n_snp, int32_t n_org) {
+    hipError_t he = nldsc::launch_load_flags(e->miss_flags.p, n_snp, e->row_miss.p, e->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
     if (he == hipSuccess) {  // missing-free blocks per sample order
         std::vector<uint8_t> rm((size_t)n_snp);
@@ -426,19 +489,6 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     nldsc_engine* e = new (std::nothrow) nldsc_engine();
     if (!e) return set_err(err, errlen, NLDSC_E_OOM, "out of host memory");
     e->device = d;
-    if (const char* v = std::getenv("NLDSC_BAND_MODE"))
-        e->band_mode = std::strcmp(v, "f32") == 0 ? 0 : std::strcmp(v, "i8") == 0 ? 1 : 2;
-    if (const char* v = std::getenv("NLDSC_GPU_PLAN")) e->gpu_plan = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_ORIENT")) e->orient = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_KSPLIT")) e->ksplit_ok = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_REPLAY_OVERLAP")) e->replay_overlap = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_T2")) e->t2_mode = std::max(0, std::min(3, std::atoi(v)));
-    if (const char* v = std::getenv("NLDSC_BAND_ROUNDS")) e->band_rounds = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_DEBUG_TIMING")) e->debug_timing = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_F4_NC2")) e->f4_nc2 = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_QUAD_ADD")) e->quad_add = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_Q_ROUNDS")) e->q_rounds = std::atoi(v) != 0;
-    if (const char* v = std::getenv("NLDSC_DEFER_REP")) e->defer_rep = std::atoi(v) != 0;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d) == hipSuccess && prop.multiProcessorCount > 0)
@@ -446,6 +496,8 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
     }
     hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->plan_stream, hipStreamNonBlocking);
+    if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_issued, hipEventDisableTiming);
     if (he == hipSuccess) he = hipEventCreateWithFlags(&e->ev_pos, hipEventDisableTiming);
     for (auto& ev : e->ev)
         if (he == hipSuccess) he = hipEventCreate(&ev);
@@ -465,6 +517,56 @@ int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t er
 
 void nldsc_engine_destroy(nldsc_engine* e) { delete e; }
 
+int nldsc_engine_set_option(nldsc_engine* e, const char* name, int64_t value, char* err, size_t errlen) {
+    if (!e || !name) return set_err(err, errlen, NLDSC_E_ARG, "NULL engine or option name");
+    struct Opt {
+        const char* name;
+        int64_t lo, hi;
+        std::function<void(int64_t)> set;
+    };
+    const Opt opts[] = {
+        {"band_mode", 0, 2, [&](int64_t v) { e->band_mode = (int)v; }},
+        {"gpu_plan", 0, 1, [&](int64_t v) { e->gpu_plan = v != 0; }},
+        {"orient", 0, 1, [&](int64_t v) { e->orient = v != 0; }},
+        {"ksplit", 0, 1, [&](int64_t v) { e->ksplit_ok = v != 0; }},
+        {"t2", 0, 3, [&](int64_t v) { e->t2_mode = (int)v; }},
+        {"band_rounds", 0, 1, [&](int64_t v) { e->band_rounds = v != 0; }},
+        {"f4_nc2", 0, 1, [&](int64_t v) { e->f4_nc2 = v != 0; }},
+        {"q_rounds", 0, 1, [&](int64_t v) { e->q_rounds = v != 0; }},
+        {"band_persist", 0, 1, [&](int64_t v) { e->band_persist = v != 0; }},
+        {"defer_rep", 0, 1, [&](int64_t v) { e->defer_rep = v != 0; }},
+        {"debug_timing", 0, 1, [&](int64_t v) { e->debug_timing = v != 0; }},
+    };
+    for (const Opt& o : opts)
+        if (std::strcmp(o.name, name) == 0) {
+            if (value < o.lo || value > o.hi)
+                return set_err(err, errlen, NLDSC_E_ARG, "option %s: value %lld outside [%lld, %lld]", name,
+                               (long long)value, (long long)o.lo, (long long)o.hi);
+            o.set(value);
+            return NLDSC_OK;
+        }
+    return set_err(err, errlen, NLDSC_E_ARG, "unknown engine option \"%s\"", name);
+}
+
+void* nldsc_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (bytes == 0 || hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    g_host_bufs[reinterpret_cast<uintptr_t>(p)] = bytes;
+    return p;
+}
+
+void nldsc_host_free(void* p) {
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> lk(g_host_mu);
+        auto it = g_host_bufs.find(reinterpret_cast<uintptr_t>(p));
+        if (it == g_host_bufs.end()) return;  // not ours
+        g_host_bufs.erase(it);
+    }
+    (void)hipHostFree(p);
+}
+
 int nldsc_engine_load_bed_host(nldsc_engine* e, const uint8_t* bed, size_t len, int32_t n_snp, int32_t n_org,
                                char* err, size_t errlen) {
     if (!e || !bed) return set_err(err, errlen, NLDSC_E_ARG, "NULL engine or buffer");
@@ -475,14 +577,14 @@ int nldsc_engine_load_bed_host(nldsc_engine* e, const uint8_t* bed, size_t len, 
     HIPCHK(hipSetDevice(e->device));
     const size_t nb = (size_t)(n_org / 4 + (n_org % 4 > 0));
     HIPCHK(alloc_image(e, n_snp, n_org));
-    // rows go up in slices of ~64 MiB into a device staging buffer, then into the resident layout (load_rows_kernel);
-    // the stream orders each slice's kernel before the next copy over the same staging bytes
-    const size_t rows_per = std::max<size_t>(1, (size_t(64) << 20) / nb);
-    HIPCHK(e->stage_dev.ensure(std::min(rows_per, (size_t)n_snp) * nb));
+    // rows go up in slices of ~64 MiB of whole 32-SNP blocks into a device staging buffer, then into the resident
+    // layout (load_slice); the stream orders each slice's kernels before the next copy over the same staging bytes
+    const size_t rows_per = std::max<size_t>(32, (size_t(64) << 20) / nb / 32 * 32);
+    HIPCHK(e->stage_dev.ensure(std::min(rows_per, (size_t)n_snp) * nb + 16));
     for (size_t r0 = 0; r0 < (size_t)n_snp; r0 += rows_per) {
         const size_t nr = std::min(rows_per, (size_t)n_snp - r0);
         HIPCHK(hipMemcpyAsync(e->stage_dev.p, bed + 3 + r0 * nb, nr * nb, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(nldsc::launch_load_rows(e->stage_dev.p, (int)nb, (int)r0, (int)nr, e->bed.p, row_pitch(n_org), e->stream));
+        HIPCHK(load_slice(e, e->stage_dev.p, (int)r0, (int)nr, n_snp, n_org, e->stream));
     }
     HIPCHK(finish_image(e, n_snp, n_org));
     e->stage_dev.release();
@@ -503,10 +605,8 @@ int nldsc_engine_load_bed_device(nldsc_engine* e, const void* bed, size_t len, i
         return set_err(err, errlen, NLDSC_E_BAD_MAGIC, "%s", kBadMagic);
     if (len < need)
         return set_err(err, errlen, NLDSC_E_SIZE, "BED image too short: %zu bytes, expected at least %zu", len, need);
-    const size_t nb = (size_t)(n_org / 4 + (n_org % 4 > 0));
     HIPCHK(alloc_image(e, n_snp, n_org));
-    HIPCHK(nldsc::launch_load_rows(static_cast<const uint8_t*>(bed) + 3, (int)nb, 0, n_snp, e->bed.p, row_pitch(n_org),
-                                   e->stream));
+    HIPCHK(load_slice(e, static_cast<const uint8_t*>(bed) + 3, 0, n_snp, n_snp, n_org, e->stream));
     HIPCHK(finish_image(e, n_snp, n_org));
     return NLDSC_OK;
 }
@@ -557,7 +657,8 @@ int nldsc_engine_load_bed_file_range(nldsc_engine* e, const char* path, int32_t 
     // the slice's H2D copy and the kernel that places its rows (load_rows_kernel), and waits for both before it reuses
     // the slot.  Slices are independent (each names its rows), so their order does not matter.
     const int fd = fileno(f);
-    const size_t rows_per = std::max<size_t>(1, (size_t(32) << 20) / nb), CH = rows_per * nb;
+    // (slices of whole 32-SNP blocks: load_slice)
+    const size_t rows_per = std::max<size_t>(32, (size_t(32) << 20) / nb / 32 * 32), CH = rows_per * nb;
     const size_t n_slices = (bytes + CH - 1) / CH;
     const int T = (int)std::max<size_t>(1, std::min<size_t>(n_slices, (size_t)kLoadThreads));
     uint8_t* stage = nullptr;
@@ -565,7 +666,7 @@ int nldsc_engine_load_bed_file_range(nldsc_engine* e, const char* path, int32_t 
         std::fclose(f);
         return set_err(err, errlen, NLDSC_E_OOM, "cannot allocate pinned staging buffer");
     }
-    hipError_t he = e->stage_dev.ensure((size_t)T * CH);
+    hipError_t he = e->stage_dev.ensure((size_t)T * CH + 16);
     std::vector<hipStream_t> streams(T, nullptr);
     std::vector<hipEvent_t> done(T, nullptr);
     for (int t = 0; t < T && he == hipSuccess; ++t) {
@@ -575,8 +676,7 @@ int nldsc_engine_load_bed_file_range(nldsc_engine* e, const char* path, int32_t 
     std::atomic<bool> stop{false};
     std::atomic<size_t> short_at{SIZE_MAX};
     std::vector<hipError_t> terr(T, hipSuccess);
-    const int dev = e->device, pitch = row_pitch(n_org);
-    uint8_t* const img = e->bed.p;
+    const int dev = e->device;
     uint8_t* const dstage = e->stage_dev.p;
     auto reader = [&](int t) {
         hipError_t r = hipSetDevice(dev);
@@ -603,7 +703,7 @@ int nldsc_engine_load_bed_file_range(nldsc_engine* e, const char* path, int32_t 
             }
             r = hipMemcpyAsync(dslot, buf, n, hipMemcpyHostToDevice, streams[t]);
             if (r == hipSuccess)
-                r = nldsc::launch_load_rows(dslot, (int)nb, (int)(off / nb), (int)(n / nb), img, pitch, streams[t]);
+                r = load_slice(e, dslot, (int)(off / nb), (int)(n / nb), n_snp, n_org, streams[t]);
             if (r == hipSuccess) r = hipEventRecord(done[t], streams[t]);
             pending = true;
         }
@@ -694,6 +794,56 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         }
         return NLDSC_OK;
     }
+    HIPCHK(hipSetDevice(e->device));
+    // Host-result runs (nldsc_engine_run): where the owned slice lands.  `out_h` are host pointers (DMA targets),
+    // `out_d` their device-mapped views (finalize_out_kernel writes them over the host link, no DMA after the band):
+    // the caller's arrays themselves when they lie in nldsc_host_alloc buffers (`direct`), else the engine's pinned
+    // landing buffer h_res, copied out by the host.  h_res also takes finalize's per-workgroup pair-count sums.
+    const bool host_out = table_dev == nullptr;
+    const int n_own = own_end - own_begin;
+    const size_t b8 = sizeof(double) * (size_t)n_own, b4 = sizeof(int32_t) * (size_t)n_own;
+    struct Out {
+        double *l2, *l2d, *maf, *rstd;
+        int32_t *wsa, *wsd, *wsde;
+    } out_h = {}, out_d = {};
+    bool direct = false;
+    unsigned long long* wsum_h = nullptr;
+    unsigned long long* wsum_d = nullptr;
+    const int n_wsum = nldsc::finalize_out_blocks(n_own);
+    if (host_out) {
+        const size_t o = (size_t)own_begin, wsum_off = (4 * b8 + 3 * b4 + 7) / 8 * 8;
+        HIPCHK(e->h_res.ensure(wsum_off + 2 * sizeof(unsigned long long) * (size_t)n_wsum));
+        uint8_t* dres = nullptr;
+        HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&dres), e->h_res.p, 0));
+        wsum_h = reinterpret_cast<unsigned long long*>(e->h_res.p + wsum_off);
+        wsum_d = reinterpret_cast<unsigned long long*>(dres + wsum_off);
+        const Out callers = {r->l2 + o, r->l2d + o, r->maf + o, r->residuals_std + o, r->l2_ws + o, r->l2d_ws + o,
+                             r->l2d_wse + o};
+        Out reg = {};
+        reg.l2 = static_cast<double*>(registered_device_ptr(callers.l2, b8));
+        reg.l2d = static_cast<double*>(registered_device_ptr(callers.l2d, b8));
+        reg.maf = static_cast<double*>(registered_device_ptr(callers.maf, b8));
+        reg.rstd = static_cast<double*>(registered_device_ptr(callers.rstd, b8));
+        reg.wsa = static_cast<int32_t*>(registered_device_ptr(callers.wsa, b4));
+        reg.wsd = static_cast<int32_t*>(registered_device_ptr(callers.wsd, b4));
+        reg.wsde = static_cast<int32_t*>(registered_device_ptr(callers.wsde, b4));
+        direct = reg.l2 && reg.l2d && reg.maf && reg.rstd && reg.wsa && reg.wsd && reg.wsde;
+        if (direct) {
+            out_h = callers;
+            out_d = reg;
+        } else {
+            auto at = [&](uint8_t* base, size_t off) { return base + off; };
+            out_h = {reinterpret_cast<double*>(at(e->h_res.p, 0)), reinterpret_cast<double*>(at(e->h_res.p, b8)),
+                     reinterpret_cast<double*>(at(e->h_res.p, 2 * b8)), reinterpret_cast<double*>(at(e->h_res.p, 3 * b8)),
+                     reinterpret_cast<int32_t*>(at(e->h_res.p, 4 * b8)),
+                     reinterpret_cast<int32_t*>(at(e->h_res.p, 4 * b8 + b4)),
+                     reinterpret_cast<int32_t*>(at(e->h_res.p, 4 * b8 + 2 * b4))};
+            out_d = {reinterpret_cast<double*>(at(dres, 0)), reinterpret_cast<double*>(at(dres, b8)),
+                     reinterpret_cast<double*>(at(dres, 2 * b8)), reinterpret_cast<double*>(at(dres, 3 * b8)),
+                     reinterpret_cast<int32_t*>(at(dres, 4 * b8)), reinterpret_cast<int32_t*>(at(dres, 4 * b8 + b4)),
+                     reinterpret_cast<int32_t*>(at(dres, 4 * b8 + 2 * b4))};
+        }
+    }
     const bool dom = !(p->flags & NLDSC_FLAG_ADDITIVE_ONLY);
     const bool strict = (p->flags & NLDSC_FLAG_STRICT_PLINK_ORDER) != 0;
     int path = (p->flags & NLDSC_FLAG_EXACT_F4) ? 2 : (p->flags & NLDSC_FLAG_EXACT_I8) ? 1
@@ -722,6 +872,9 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // the band kernels read the resident rows (Mpad rows at row_bytes pitch) in place
     const uint32_t* geno = reinterpret_cast<const uint32_t*>(e->bed.p);
     HIPCHK(e->counts.ensure((size_t)M * 4));
+    const int count_parts = nldsc::count_parts(M, nb);
+    HIPCHK(e->cparts.ensure((size_t)count_parts * M * 3));
+    HIPCHK(e->rep_count.ensure(1));  // (zeroed by the statistics kernel)
     HIPCHK(e->lut.ensure((size_t)Mpad * 4));
     HIPCHK(e->cst.ensure((size_t)Mpad));
     HIPCHK(e->sflags.ensure((size_t)Mpad));
@@ -750,16 +903,13 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // launches cost ~50 us per run)
     const int order = strict ? 1 : 0;  // bit of row_miss: the individual slots of this run's sample order
     const bool t2_cand = e->t2_mode > 0 && gpu_plan && use_f4 && n_it <= nldsc::F4_SEG_CHUNKS && n_it >= 2 &&
-                         (e->t2_mode == 2 || e->free_blocks[order] > 0 || (e->quad_add && !dom));
+                         (e->t2_mode == 2 || e->free_blocks[order] > 0);
     // additive-only fp4 items of two column blocks (GPU plan, unsegmented rows; no K-split: its partial kernel takes
     // single block pairs)
     const bool nc2 = e->f4_nc2 && gpu_plan && use_f4 && !dom && n_it <= nldsc::F4_SEG_CHUNKS;
     const bool routed = e->t2_mode == 1 || e->t2_mode == 3;
     const bool quad = e->t2_mode == 3;
     const int route_shift = quad ? 2 : 1;  // super-items of 2^route_shift blocks a side
-    // ($NLDSC_QUAD_ADD=1, study) additive-only runs: every 4 x 4 super-item in the quad kernel, those holding missing
-    // calls with the four additive products in 64 x 64 tiles per wave; the other kernels get an all-zero routing array
-    const bool quad_add = quad && !dom && e->quad_add;
     // K-split (f4, unsegmented rows) when the items fill the wave slots (2 per SIMD) in few, partly empty
     // rounds — a rank's shard of one chromosome — and splitting the K loop in P pieces fills them better
     // Model: a round of items takes ~0.67 us per K chunk (C3: 2 466 chunks, 1.65 ms per round, 12.7 rounds in
@@ -805,19 +955,21 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // streaming saturates HBM, those dependent loads took 0.05-0.1 ms on the critical path of short runs); then the
     // count kernel, with the rest of the schedule beside it on the plan stream.
     const size_t b_pos = sizeof(double) * (size_t)M;
-    HIPCHK(e->h_pos.ensure(b_pos));
-    {
+    if (registered_device_ptr(p->positions, b_pos)) {  // (pinned: the DMA reads them in place)
+        HIPCHK(hipMemcpyAsync(e->pos.p, p->positions, b_pos, hipMemcpyHostToDevice, st));
+    } else {
+        HIPCHK(e->h_pos.ensure(b_pos));
         const CopyPool::Seg seg = {e->h_pos.p, p->positions, b_pos};
         e->copies.copy(&seg, 1);
+        HIPCHK(hipMemcpyAsync(e->pos.p, e->h_pos.p, b_pos, hipMemcpyHostToDevice, st));
     }
-    HIPCHK(hipMemcpyAsync(e->pos.p, e->h_pos.p, b_pos, hipMemcpyHostToDevice, st));
     if (gpu_plan) HIPCHK(nldsc::launch_plan_edges(e->pos.p, M, p->ld_wind, e->Aw.p, e->Aw.p + M, e->plan_meta.p, st));
     HIPCHK(hipEventRecord(e->ev_pos, st));
     // non-individual slots read as missing (0x55) for the int8 / fp32 kernels, as 00 (all fp4 planes zero) for fp4
     const uint32_t pad = use_f4 ? 0x00u : 0x55u;
     const int n_pad00 = use_f4 ? 4 * row_bytes - N : 0;
     HIPCHK(hipEventRecord(e->ev[0], st));  // (count_ms: the count kernel alone; the host total covers the above)
-    HIPCHK(nldsc::launch_count_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, pad, n_pad00, e->counts.p, st));
+    HIPCHK(nldsc::launch_count_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, pad, n_pad00, e->cparts.p, st));
     HIPCHK(hipEventRecord(e->ev[1], st));
     if (gpu_plan) {
         HIPCHK(hipStreamWaitEvent(e->plan_stream, e->ev_pos, 0));
@@ -831,9 +983,10 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         HIPCHK(hipMemcpyAsync(e->h_meta.p, e->plan_meta.p, 8 * sizeof(int), hipMemcpyDeviceToHost, e->plan_stream));
         HIPCHK(hipEventRecord(e->ev_plan, e->plan_stream));
     }
-    HIPCHK(nldsc::launch_snp_stats(e->counts.p, e->oriented ? e->flip.p : nullptr, e->pos.p, M, Mpad, N, p->maf, p->std_thr, e->lut.p, e->cst.p,
-                                   e->sflags.p, e->maf.p, e->rstd.p, st, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p,
-                                   e->blk_rep.p));
+    HIPCHK(nldsc::launch_snp_stats(e->cparts.p, count_parts, e->counts.p, e->rep_count.p,
+                                   e->oriented ? e->flip.p : nullptr, e->pos.p, M, Mpad, N, p->maf, p->std_thr,
+                                   e->lut.p, e->cst.p, e->sflags.p, e->maf.p, e->rstd.p, st, e->l2_acc.p, e->l2d_acc.p,
+                                   e->ws_acc.p, e->blk_rep.p));
     // split runs: the pairs whose lower SNP is owned (flag bit 3), before the replay may touch the flags (ev_stats)
     if (split) HIPCHK(nldsc::launch_pair_range(e->sflags.p, M, own_begin, own_end, st));
     // rare variants: the reference's fp32 residual replayed (its sums assume N < 2^23); the flags per block here,
@@ -851,6 +1004,24 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         HIPCHK(hipEventRecord(e->ev_stats, st));
     }
     HIPCHK(hipEventRecord(e->ev[2], st));
+    // What needs no schedule goes out before the host waits for it (C2 / a rank's shard: the count ends first, and
+    // the host's enqueue after that wait is on the critical path): the left pointers (the window edges came before the
+    // count), the blocks' missing flags (from the load) and the rare-variant replay — a few long sequential sums, on
+    // the side stream beside the band launch for the items without a replayed SNP; only the KC launch and finalize
+    // wait for it (ev_replay).  (Its sums assume N < 2^23.)
+    hipStream_t cs = e->copy_stream, ps = e->plan_stream;
+    if (gpu_plan) HIPCHK(nldsc::launch_left_pointers(e->Aw.p, e->sflags.p, e->pos.p, M, e->Lw.p, st));
+    if (use_f4) {  // per 32-SNP block: holds a missing call (the kernels' m-product predicate: routing, issued count)
+        HIPCHK(e->blk_miss.ensure((size_t)nblk));
+        HIPCHK(nldsc::launch_block_missing_rows(e->row_miss.p, M, order, e->blk_miss.p, gpu_plan ? ps : st));
+    }
+    if (replay) {
+        HIPCHK(hipStreamWaitEvent(cs, e->ev_stats, 0));
+        HIPCHK(nldsc::launch_reference_residuals(e->bed.p, row_bytes, N, strict, e->counts.p,
+                                                 e->oriented ? e->flip.p : nullptr, M, p->std_thr, e->cst.p, e->lut.p,
+                                                 e->sflags.p, e->rstd.p, cs));
+        HIPCHK(hipEventRecord(e->ev_replay, cs));
+    }
 
     // ---- window replay + schedule ----
     auto t_host0 = std::chrono::steady_clock::now();
@@ -860,10 +1031,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         {  // the count kernel is running meanwhile; the host polls the pinned counters (a blocking event wait wakes
            // the thread tens of microseconds late: the schedule is on the critical path of short runs — a 1/8 shard,
            // C2 — whose count ends first), then the event confirms the whole copy
-            volatile const int* m = reinterpret_cast<volatile const int*>(e->h_meta.p);
-            const auto t0 = std::chrono::steady_clock::now();
-            while (m[1] < 0 && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2)) {
-            }
+            (void)spin_until_nonneg(reinterpret_cast<volatile const int*>(e->h_meta.p) + 1);
             HIPCHK(hipEventSynchronize(e->ev_plan));
         }
         const int* meta = reinterpret_cast<const int*>(e->h_meta.p);
@@ -881,11 +1049,10 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
             ksplit = 1;
         }
         use_t2 = t2_cand && ksplit == 1 && n_items > 0 && !rounds_forced;
-        // The work lists go out on the plan stream, beside the count kernel: the items, the super-items, the routing
-        // (blk_miss, from the load-time row_miss: it needs no count) and, with super-item routing, the list of the
-        // items the single-block kernel keeps, compacted in order, so its launches (round launches, the K-split tail)
-        // are sized by its own work — its length reaches the host before the band.  The main stream waits for them.
-        hipStream_t ps = e->plan_stream;
+        // The work lists go out on the plan stream, beside the count kernel: the items, the super-items and, with
+        // super-item routing (blk_miss, above), the list of the items the single-block kernel keeps, compacted in order,
+        // so its launches (round launches, the K-split tail) are sized by its own work — its length reaches the host
+        // before the band.  The main stream waits for them.
         if (use_t2) {
             n_items2 = meta[5];
             HIPCHK(e->items2.ensure(std::max<size_t>((size_t)n_items2, 1)));
@@ -898,14 +1065,6 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                 HIPCHK(nldsc::launch_plan_emit(M, e->plan_rows.p, e->plan_meta.p, e->plan_counts.p, e->items.p, ps,
                                                nc2));
         }
-        if (use_f4) {  // per 32-SNP block: holds a missing call (the kernels' m-product predicate: routing, issued count)
-            HIPCHK(e->blk_miss.ensure((size_t)nblk));
-            HIPCHK(nldsc::launch_block_missing_rows(e->row_miss.p, M, order, e->blk_miss.p, ps));
-        }
-        if (use_t2 && quad_add) {
-            HIPCHK(e->blk_zero.ensure((size_t)nblk));
-            HIPCHK(hipMemsetAsync(e->blk_zero.p, 0, (size_t)nblk, ps));
-        }
         compact = use_t2 && routed && n_items > 0;
         if (compact) {
             const size_t n_chunks = ((size_t)n_items + 255) / 256;  // (ld_kernels.hip COMPACT_CHUNK)
@@ -913,14 +1072,13 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
             HIPCHK(e->compact_tmp.ensure(n_chunks + 1));
             HIPCHK(e->h_route.ensure(sizeof(int)));
             *reinterpret_cast<volatile int*>(e->h_route.p) = -1;  // (the copy below lands the count, >= 0)
-            HIPCHK(nldsc::launch_compact_items(e->items.p, n_items, quad_add ? e->blk_zero.p : e->blk_miss.p, route_shift,
+            HIPCHK(nldsc::launch_compact_items(e->items.p, n_items, e->blk_miss.p, route_shift,
                                                nblk, e->compact_tmp.p,
                                                e->compact_tmp.p + n_chunks, e->items_u.p, ps));
             HIPCHK(hipMemcpyAsync(e->h_route.p, e->compact_tmp.p + n_chunks, sizeof(int), hipMemcpyDeviceToHost, ps));
         }
         HIPCHK(hipEventRecord(e->ev_route, ps));
-        HIPCHK(hipStreamWaitEvent(st, e->ev_route, 0));  // left pointers / band read the schedule and the lists
-        HIPCHK(nldsc::launch_left_pointers(e->Aw.p, e->sflags.p, e->pos.p, M, e->Lw.p, st));
+        HIPCHK(hipStreamWaitEvent(st, e->ev_route, 0));  // the band reads the schedule and the lists
     } else {
     e->h_L.resize(M);
     e->h_R.resize(M);
@@ -972,21 +1130,6 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     n_items = (int)e->h_items.size();
     ksplit = choose_ksplit(n_items);
     }
-    if (use_f4 && !gpu_plan) {  // (the GPU plan computes it on the plan stream)
-        HIPCHK(e->blk_miss.ensure((size_t)nblk));
-        HIPCHK(nldsc::launch_block_missing_rows(e->row_miss.p, M, order, e->blk_miss.p, st));
-    }
-    // rare variants: the reference's fp32 residual replayed (its sums assume N < 2^23).  The flags went first on the
-    // main stream; the replay itself (a few long sequential sums) runs on the plan stream beside the band launch for
-    // the items without a replayed SNP, and only the KC launch and finalize wait for it.
-    if (replay) {
-        hipStream_t rs = e->replay_overlap ? e->plan_stream : st;
-        HIPCHK(hipStreamWaitEvent(rs, e->ev_stats, 0));
-        HIPCHK(nldsc::launch_reference_residuals(e->bed.p, row_bytes, N, strict, e->counts.p,
-                                                 e->oriented ? e->flip.p : nullptr, M, p->std_thr, e->cst.p, e->lut.p,
-                                                 e->sflags.p, e->rstd.p, rs));
-        HIPCHK(hipEventRecord(e->ev_replay, rs));
-    }
     // (l2_acc, l2d_acc and ws_acc were zeroed by snp_stats_kernel)
     auto t_host1 = std::chrono::steady_clock::now();
 
@@ -1033,8 +1176,6 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
             const size_t slots = (size_t)n_full * (nc2 ? 2 : 1);
             hipError_t r = e->rep_gram.ensure(slots * 8192);
             if (r == hipSuccess) r = e->rep_items.ensure(slots);
-            if (r == hipSuccess) r = e->rep_count.ensure(1);
-            if (r == hipSuccess) r = hipMemsetAsync(e->rep_count.p, 0, sizeof(int), st);
             if (r != hipSuccess) return r;
         }
         return tail_p > 1 ? e->gram.ensure((size_t)tail * tail_p * 8192) : hipSuccess;
@@ -1047,7 +1188,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
             return nldsc::launch_band_f4_q(dom, n_items2, geno, pitch_words, n_it, e->cst.p, e->items2.p,
                                            e->plan_rows.p, nblk, e->pos.p, e->Lw.p, e->Rw.p, e->sflags.p, M,
                                            p->ld_wind, (double)N, p->rsq_thr, own_begin, flush_hi, e->l2_acc.p,
-                                           e->l2d_acc.p, e->ws_acc.p, true, blk_rep, e->blk_miss.p, which, st, quad_add,
+                                           e->l2d_acc.p, e->ws_acc.p, true, blk_rep, e->blk_miss.p, which, st,
                                            e->q_rounds && n_items2 >= 16 * e->n_cu ? e->n_cu : 0);
         return nldsc::launch_band_f4_t2(
             dom, n_items2, geno, pitch_words, n_it, e->cst.p, e->items2.p, e->plan_rows.p, nblk, e->pos.p, e->Lw.p,
@@ -1057,7 +1198,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // (column-block pair items: the compaction keeps an item while one of its blocks is unrouted, the kernel drops
     // the other)
     const uint8_t* single_miss =
-        use_t2 && routed && (!compact || nc2) ? (quad_add ? e->blk_zero.p : e->blk_miss.p) : nullptr;
+        use_t2 && routed && (!compact || nc2) ? e->blk_miss.p : nullptr;
     auto launch_single = [&](int which) -> hipError_t {
         if (use_f4 && ksplit > 1)
             return nldsc::launch_band_f4_split(dom, ksplit, n_single, geno, pitch_words, n_it, e->cst.p, single,
@@ -1072,7 +1213,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                                                  e->ws_acc.p, true, blk_rep, which, st, single_miss, round_items,
                                                  route_shift,
                                                  dfr ? e->rep_gram.p : nullptr, dfr ? e->rep_items.p : nullptr,
-                                                 dfr ? e->rep_count.p : nullptr);
+                                                 dfr ? e->rep_count.p : nullptr, e->band_persist);
             if (r == hipSuccess && dfr && (which & 2))  // after the replay: the deferred items' epilogues
                 r = nldsc::launch_band_f4_deferred_epi(dom, n_full * (nc2 ? 2 : 1), e->cst.p, e->rep_items.p,
                                                        e->rep_count.p, e->rep_gram.p, e->pos.p, e->Lw.p, e->Rw.p,
@@ -1098,9 +1239,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
             // (polling the pinned word the copy lands in: a blocking event wait wakes the thread tens of
             // microseconds late, time the GPU would idle when the super-item kernel has nothing to do)
             volatile int* cnt = reinterpret_cast<volatile int*>(e->h_route.p);
-            const auto t0 = std::chrono::steady_clock::now();
-            while (*cnt < 0 && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2)) {
-            }
+            (void)spin_until_nonneg(cnt);
             HIPCHK(hipEventSynchronize(e->ev_route));  // (returns at once when the count has landed)
             n_single = *cnt;
             single = e->items_u.p;
@@ -1138,17 +1277,20 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     HIPCHK(hipEventRecord(e->ev[4], st));
     // matrix-core products the band kernels issued, counted on the GPU per work item as each kernel decides them
     // (missing-free blocks skip the m products, diagonal blocks the transposed ones, routed items run in the 2 x 2
-    // kernel): sums[2]; sums[0..1] are the device-table run's pair counts
+    // kernel): sums[2], counted beside the band on the copy stream (after the work lists: ev[3]) and landed in
+    // h_sums[2] (ev_issued); sums[0..1] are the device-table run's pair counts
     HIPCHK(e->sums.ensure(3));
     HIPCHK(e->h_sums.ensure(3 * sizeof(unsigned long long)));
-    HIPCHK(hipMemsetAsync(e->sums.p, 0, 3 * sizeof(unsigned long long), st));
+    HIPCHK(hipStreamWaitEvent(cs, e->ev[3], 0));
+    HIPCHK(hipMemsetAsync(e->sums.p + 2, 0, sizeof(unsigned long long), cs));
     HIPCHK(nldsc::launch_issued_products(single, run_single ? n_single : 0, use_t2 ? e->items2.p : nullptr,
                                          n_items2, gpu_plan ? e->plan_rows.p : nullptr,
                                          use_f4 ? e->blk_miss.p : nullptr, nblk, path, dom,
-                                         (use_t2 && routed ? 2 : 0) | (single_miss != nullptr ? 1 : 0) |
-                                             (use_t2 && quad_add ? 4 : 0),
-                                         route_shift,
-                                         e->sums.p + 2, st));
+                                         (use_t2 && routed ? 2 : 0) | (single_miss != nullptr ? 1 : 0), route_shift,
+                                         e->sums.p + 2, cs));
+    HIPCHK(hipMemcpyAsync(e->h_sums.p + 2 * sizeof(unsigned long long), e->sums.p + 2, sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, cs));
+    HIPCHK(hipEventRecord(e->ev_issued, cs));
     if (split) {  // the right halo's sums out; finalize waits for the left neighbour's (run_device_finish)
         HIPCHK(nldsc::launch_export_acc(e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, own_end, M, export_dev, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -1169,51 +1311,63 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         e->split_width = width;
         return NLDSC_OK;
     }
-    HIPCHK(nldsc::launch_finalize(e->Lw.p, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, own_begin, own_end, dom,
-                                  e->l2.p, e->l2d.p, e->ws3.p, st));
-    HIPCHK(hipEventRecord(e->ev[5], st));
-    const int n_own = own_end - own_begin;
     double sw = 0, sd = 0;
     if (table_dev) {
         // the owned slice stays on the device (the caller gathers it device to device); only the pair counts of
         // the metric come back
+        HIPCHK(nldsc::launch_finalize(e->Lw.p, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, own_begin, own_end, dom,
+                                      e->l2.p, e->l2d.p, e->ws3.p, st));
+        HIPCHK(hipEventRecord(e->ev[5], st));
+        HIPCHK(hipMemsetAsync(e->sums.p, 0, 2 * sizeof(unsigned long long), st));
         HIPCHK(nldsc::launch_pack_table(e->l2.p, e->l2d.p, e->maf.p, e->rstd.p, e->ws3.p, M, own_begin, own_end, width,
                                         table_dev, e->sums.p, st));
-        HIPCHK(hipMemcpyAsync(e->h_sums.p, e->sums.p, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(e->h_sums.p, e->sums.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         const unsigned long long* s = reinterpret_cast<const unsigned long long*>(e->h_sums.p);
         sw = (double)s[0];
         sd = dom ? (double)s[1] : 0.0;
     } else {
-        // the owned slices land in pinned memory by DMA (pageable copies are staged by the runtime, slower) in two
-        // strided copies (fp64 rows, int32 rows), then go to the caller's arrays; the pair counts are summed on the GPU
-        // by four threads (copying each column on as its own copy lands, polled with hipEventQuery, measured 0.07 ms
-        // faster at C2 in one process and up to 1.4 ms slower in others: the runtime's completion processing competes
-        // with the poll)
-        const size_t o = own_begin, b8 = sizeof(double) * (size_t)std::max(n_own, 0),
-                     b4 = sizeof(int) * (size_t)std::max(n_own, 0);
-        double* const ddst[4] = {r->l2 + o, r->l2d + o, r->maf + o, r->residuals_std + o};
-        int32_t* const idst[3] = {r->l2_ws + o, r->l2d_ws + o, r->l2d_wse + o};
-        if (n_own > 0) {
-            HIPCHK(nldsc::launch_pack_table(e->l2.p, e->l2d.p, e->maf.p, e->rstd.p, e->ws3.p, M, own_begin, own_end,
-                                            n_own, nullptr, e->sums.p, st));
-            HIPCHK(e->h_res.ensure(4 * b8 + 3 * b4));
-            HIPCHK(hipMemcpy2DAsync(e->h_res.p, b8, e->l2.p + o, sizeof(double) * (size_t)M, b8, 4,
-                                    hipMemcpyDeviceToHost, st));
-            HIPCHK(hipMemcpy2DAsync(e->h_res.p + 4 * b8, b4, e->ws3.p + o, sizeof(int) * (size_t)M, b4, 3,
-                                    hipMemcpyDeviceToHost, st));
-        }
-        HIPCHK(hipMemcpyAsync(e->h_sums.p, e->sums.p, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        // Host results: finalize writes the owned slice's seven columns straight into host memory (out_d) with its
+        // per-workgroup pair-count sums — no pack kernel, no copy engine (the runtime moves device-to-pinned copies
+        // with blit kernels: a 0.6 MB RSTD copy beside the C2 band took ~1 ms of its CU slots); without `direct`, the
+        // host copies them from the landing buffer to the caller's arrays.
+        HIPCHK(nldsc::launch_finalize_out(e->Lw.p, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, e->maf.p, e->rstd.p, M,
+                                          own_begin, own_end, dom, out_d.l2, out_d.l2d, out_d.maf, out_d.rstd,
+                                          out_d.wsa, out_d.wsd, out_d.wsde, wsum_d, st));
+        HIPCHK(hipEventRecord(e->ev[5], st));
+        const size_t o = own_begin;
+        using clk = std::chrono::steady_clock;
+        clk::time_point tq[5];
+        tq[2] = clk::now();
         HIPCHK(hipStreamSynchronize(st));
-        if (n_own > 0) {
-            CopyPool::Seg segs[7];
-            for (int k = 0; k < 4; ++k) segs[k] = {ddst[k], e->h_res.p + k * b8, b8};
-            for (int k = 0; k < 3; ++k) segs[4 + k] = {idst[k], e->h_res.p + 4 * b8 + k * b4, b4};
+        tq[3] = clk::now();
+        if (!direct) {
+            const CopyPool::Seg segs[7] = {{r->l2 + o, out_h.l2, b8},           {r->l2d + o, out_h.l2d, b8},
+                                           {r->maf + o, out_h.maf, b8},         {r->residuals_std + o, out_h.rstd, b8},
+                                           {r->l2_ws + o, out_h.wsa, b4},       {r->l2d_ws + o, out_h.wsd, b4},
+                                           {r->l2d_wse + o, out_h.wsde, b4}};
             e->copies.copy(segs, 7);
         }
-        const unsigned long long* s = reinterpret_cast<const unsigned long long*>(e->h_sums.p);
-        sw = (double)s[0];
-        sd = dom ? (double)s[1] : 0.0;
+        unsigned long long ta = 0, td = 0;
+        for (int b = 0; b < n_wsum; ++b) {
+            ta += wsum_h[2 * b];
+            td += wsum_h[2 * b + 1];
+        }
+        sw = (double)ta;
+        sd = dom ? (double)td : 0.0;
+        tq[4] = clk::now();
+        if (e->debug_timing) {
+            auto ms = [&](int a, int b) { return std::chrono::duration<double, std::milli>(tq[b] - tq[a]).count(); };
+            std::fprintf(stderr, "[nldsc debug] host results (%s): band wait %.3f, copies and sums %.3f ms\n",
+                         direct ? "direct" : "landing buffer", ms(2, 3), ms(3, 4));
+        }
+    }
+    {
+        const auto t0 = std::chrono::steady_clock::now();
+        HIPCHK(hipEventSynchronize(e->ev_issued));
+        if (e->debug_timing)
+            std::fprintf(stderr, "[nldsc debug] issued-count wait %.3f ms\n",
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     }
     auto t_end = std::chrono::steady_clock::now();
 
@@ -1284,10 +1438,12 @@ int nldsc_engine_run_device_finish(nldsc_engine* e, const int64_t* import_dev, i
     HIPCHK(nldsc::launch_finalize(e->Lw.p, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, M, lo, hi, e->split_dom, e->l2.p,
                                   e->l2d.p, e->ws3.p, st));
     HIPCHK(hipEventRecord(e->ev[5], st));
+    HIPCHK(hipMemsetAsync(e->sums.p, 0, 2 * sizeof(unsigned long long), st));
     HIPCHK(nldsc::launch_pack_table(e->l2.p, e->l2d.p, e->maf.p, e->rstd.p, e->ws3.p, M, lo, hi, e->split_width,
                                     e->split_table, e->sums.p, st));
-    HIPCHK(hipMemcpyAsync(e->h_sums.p, e->sums.p, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(e->h_sums.p, e->sums.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipEventSynchronize(e->ev_issued));  // (h_sums[2]: the first call's issued-product count)
     const unsigned long long* s = reinterpret_cast<const unsigned long long*>(e->h_sums.p);
     const double sw = (double)s[0], sd = e->split_dom ? (double)s[1] : 0.0, N = (double)e->split_N;
     float f = 0;

@@ -22,23 +22,32 @@ struct SnpConst {
     double isa, is;
 };
 
-// resident rows (block-interleaved, ld_kernels.hip tile_off): rows [row0, row0 + n_rows) of a .bed image (row r of nb
-// bytes at src + r * nb) into place, with the pitch padding as 0x55
-hipError_t launch_load_rows(const uint8_t* src, int nb, int row0, int n_rows, uint8_t* img, int row_bytes,
-                            hipStream_t st);
-// after a load, save each row's last byte (rows >= n_snp all 0x55)
-hipError_t launch_pad_rows(uint8_t* img, uint8_t* last, int n_snp, int n_rows, int nb, int row_bytes,
-                           hipStream_t st);
+// A load, one slice of whole 32-SNP blocks at a time (row0 % 32 == 0; only the image's last slice may end mid-block):
+// rows [row0, row0 + n_rows) of a .bed image (row r of nb bytes at src + r * nb, any alignment) into the resident
+// layout (block-interleaved, ld_kernels.hip tile_off) — pitch padding 0x55, the last block's rows past n_snp all 0x55 —
+// each stored in the orientation flip[j] chosen from its head (orient: rows with more hom-A2 than hom-A1 calls there
+// stored 00 <-> 11 swapped; !orient: as in the file), its stored last byte saved to last[j], and its missing calls
+// among the individual slots of the reference's (bit 0) / PLINK's (bit 1) sample order ORed into miss_flags[j]
+// (keep_*: the last byte's individual bit pairs per order).  After every slice: launch_load_flags -> row_miss.
+hipError_t launch_load_slice(const uint8_t* src, int nb, int row0, int n_rows, int n_snp, uint8_t* img, int row_bytes,
+                             bool orient, uint8_t* flip, uint8_t* last, uint32_t keep_compat, uint32_t keep_strict,
+                             uint32_t* miss_flags, hipStream_t st);
+hipError_t launch_load_flags(const uint32_t* miss_flags, int n_snp, uint8_t* row_miss, hipStream_t st);
 // per run: set each row's non-individual slots (last byte outside tail_keep, pitch padding) to `pad`
 // (0x55 missing, or 0x00 for the fp4 kernel) and count genotype codes; n_pad00 = 00-coded non-individual
-// slots per row (discounted from hom-A1)
+// slots per row (discounted from hom-A1).  Counts of part p (count_parts per 32-SNP block) of SNP j land in
+// parts[(p n_snp + j) 3 + k], k = hom A1, het, hom A2 (count_parts(n_snp, nb) * n_snp * 3 ints, no zeroing needed)
+int count_parts(int n_snp, int nb);
 hipError_t launch_count_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
-                             uint32_t pad, int n_pad00, int* counts, hipStream_t st);
-// flip: per-SNP stored-orientation flags (nullptr: none flipped)
-hipError_t launch_snp_stats(const int* counts, const uint8_t* flip, const double* pos, int n_snp, int n_snp_pad,
-                            int n_org, double maf_thr, double std_thr, float2* lut, SnpConst* cst, uint8_t* sflags,
-                            double* maf_out, double* rstd_out, hipStream_t st, double* l2_acc = nullptr,
-                            double* l2d_acc = nullptr, int* ws_acc = nullptr, uint8_t* blk_rep = nullptr);
+                             uint32_t pad, int n_pad00, int* parts, hipStream_t st);
+// parts / P: the count kernel's output, summed into counts[4 j + k] (n_snp * 4 ints; the rare-variant kernels read
+// them); zero: one int cleared on the way (nullptr: none).  flip: per-SNP stored-orientation flags (nullptr: none
+// flipped)
+hipError_t launch_snp_stats(const int* parts, int P, int* counts, int* zero, const uint8_t* flip, const double* pos,
+                            int n_snp, int n_snp_pad, int n_org, double maf_thr, double std_thr, float2* lut,
+                            SnpConst* cst, uint8_t* sflags, double* maf_out, double* rstd_out, hipStream_t st,
+                            double* l2_acc = nullptr, double* l2d_acc = nullptr, int* ws_acc = nullptr,
+                            uint8_t* blk_rep = nullptr);
 // (l2_acc, l2d_acc, ws_acc [4][n_snp] and blk_rep, when given: zeroed for the band and the replay flags)
 // SNPs with at most REF_RESIDUAL_MIN_CLASS calls in one genotype class (rare variants: residual nearly degenerate):
 // residual std, residual-pass flag bit 2, exact constants and fp32 table of the reference's fp32 residual,
@@ -57,10 +66,6 @@ hipError_t launch_replay_flags(const int* counts, const uint8_t* flip, const uin
 hipError_t launch_reference_residuals(const uint8_t* img, int row_bytes, int n_org, bool strict, const int* counts,
                                      const uint8_t* flip, int n_snp, double std_thr, SnpConst* cst, float2* lut,
                                      uint8_t* sflags, double* rstd_out, hipStream_t st);
-// after a load: row_miss[j] bit 0 / bit 1 = row j holds a missing call (01) among the individual slots of the
-// reference's / PLINK's sample order (keep masks of the last byte as the count kernel's tail_keep)
-hipError_t launch_row_missing(const uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes,
-                              uint32_t keep_compat, uint32_t keep_strict, uint8_t* row_miss, hipStream_t st);
 // halo pairs once across ranks: clear flag bit 3 (the pair's lower SNP: computed here) outside [pair_lo, pair_hi);
 // the accumulator rows of SNPs [lo, hi) out to a [6][hi - lo] int64 block, and such a block added into SNPs [lo, lo + n)
 hipError_t launch_pair_range(uint8_t* sflags, int n_snp, int pair_lo, int pair_hi, hipStream_t st);
@@ -72,8 +77,6 @@ hipError_t launch_import_acc(double* l2_acc, double* l2d_acc, int* ws_acc, int n
 // band kernels, known without the count kernel
 hipError_t launch_block_missing_rows(const uint8_t* row_miss, int n_snp, int order, uint8_t* blk_miss,
                                      hipStream_t st);
-// after a load: swap 00 <-> 11 in rows (and saved last bytes) with more hom-A2 than hom-A1 calls; flip[j] = 1
-hipError_t launch_orient_rows(uint8_t* img, uint8_t* last, int n_snp, int row_bytes, uint8_t* flip, hipStream_t st);
 // exact left pointers L from the all-pass replay's A and the device MAF flags (sorted positions)
 hipError_t launch_left_pointers(const int* A, const uint8_t* sflags, const double* pos, int n, int* L, hipStream_t st);
 // the schedule's window edges of sorted positions (all-pass left pointers A, window ends E) and meta[0..3] = 0
@@ -109,7 +112,8 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
                           int which, hipStream_t st, const uint8_t* blk_miss = nullptr, int round_items = 0,
-                          int route_shift = 1, float* rep_gram = nullptr, int4* rep_items = nullptr, int* rep_count = nullptr);
+                          int route_shift = 1, float* rep_gram = nullptr, int4* rep_items = nullptr, int* rep_count = nullptr,
+                          bool persist = false);
 // rep_gram (unsegmented rows): the items holding a replayed rare variant run their K loops in the main launch and store
 // each block pair's exact Gram tiles (rep_gram slot = atomicAdd(rep_count), 8192 floats; rep_items[slot] = the block
 // pair); after the replay, launch_band_f4_deferred_epi runs their epilogues (max_items >= the slots used) in place of
@@ -144,20 +148,27 @@ hipError_t launch_band_f4_t2(bool dom, int n_items2, const uint32_t* geno, int p
                              hipStream_t st);
 // 4 x 4 block-pair workgroups (the quad kernel: one wave per SIMD, 64 x 64 SNP tiles) for the missing-free 4 x 4
 // super-items (I4, J4, 1, 0) of launch_plan_super(shift 2); blk_miss required (route_shift 2 for the other kernels).
-// add_all (additive-only runs): every super-item, those holding missing calls with the four additive products (the
-// other kernels are then routed nothing: an all-zero routing array)
 constexpr int Q_STAGES = 4;
 hipError_t launch_band_f4_q(bool dom, int n_items4, const uint32_t* geno, int pitch_words, int n_it,
                             const SnpConst* cst, const int4* items4, const int2* rows, int nblk, const double* pos,
                             const int* Lw, const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind,
                             double n_org, double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
                             int* ws_acc, bool xcd, const uint8_t* blk_rep, const uint8_t* blk_miss, int which,
-                            hipStream_t st, bool add_all, int round_items = 0);
+                            hipStream_t st, int round_items = 0);
 // blk_miss[b] = block b holds a missing call (launch_block_missing_rows).  Passed to the fp4 kernels (unsegmented rows)
 // it routes the super-items: missing-free ones to a super-item kernel (operand-feed bound at 3 products per K step,
 // where sharing the strips pays), the block pairs of the others to the single-block kernel (MFMA bound at 8 products)
 hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2d_acc, const int* ws_acc, int n_snp,
                            int own_lo, int own_hi, bool dom, double* l2, double* l2d, int* ws3, hipStream_t st);
+// Results of a host-result run straight to host memory (zero-copy: device-accessible pinned pointers, index 0 = SNP
+// own_lo): the finalized l2, l2d, the MAF and RSTD (from maf_in / rstd_in), WSA, WSD, WSDE of the owned slice; and per
+// workgroup of finalize_out_blocks(n) the sums of positive WSA / WSD to wsum[2 b], wsum[2 b + 1] (the metric's pair
+// counts; the host adds them)
+int finalize_out_blocks(int n_own);
+hipError_t launch_finalize_out(const int* Lw, const double* l2_acc, const double* l2d_acc, const int* ws_acc,
+                               const double* maf_in, const double* rstd_in, int n_snp, int own_lo, int own_hi, bool dom,
+                               double* l2, double* l2d, double* maf, double* rstd, int* wsa, int* wsd, int* wsde,
+                               unsigned long long* wsum, hipStream_t st);
 // the matrix-core products the band kernels issued (one per 32x32 block product over all K), counted per work item
 // as each kernel decides them: kind 2 fp4 single-block items (+ the super-items when items2 != nullptr; `routed`
 // bit 0: skip single items routed to a super-item kernel, bit 1: count only routed super-items), 1 int8, 0 fp32

@@ -57,45 +57,165 @@ __device__ __forceinline__ void count_codes(uint32_t word, int& c0, int& c1, int
     c1 += __popc(hi & ~lo);                 // 10 het
     c2 += __popc(hi & lo);                  // 11 hom A2
 }
+__device__ __forceinline__ int count_missing(uint32_t word) {
+    return __popc(~(word >> 1) & word & 0x55555555u);  // pairs 01
+}
 
-// Loads: rows [row0, row0 + n_rows) of a .bed image (src: row r at r * nb bytes, any alignment) into the resident
-// layout, the pitch padding [nb, row_bytes) as 0x55.  One thread per 16-byte unit in source order (coalesced byte
-// reads; each thread writes one whole 16-byte unit), grid-stride: an HSA dispatch counts its grid in work-items in 32
-// bits, so a launch of one thread per unit of a C5 slice (98.6 GB, 6.2e9 units) would wrap.
-__global__ void __launch_bounds__(256) load_rows_kernel(const uint8_t* __restrict__ src, int nb, int row0, int n_rows,
-                                                        uint8_t* __restrict__ img, int row_bytes) {
-    const int units = row_bytes >> 4;
-    const size_t n = (size_t)n_rows * units, stride = (size_t)gridDim.x * 256;
-    for (size_t g = (size_t)blockIdx.x * 256 + threadIdx.x; g < n; g += stride) {
-        const int r = (int)(g / units), u = (int)(g % units);
-        const uint8_t* s = src + (size_t)r * nb;
-        uint32_t w[4];
+// ---- loads: .bed rows -> the resident layout, oriented, with per-row missing flags (one pass over the rows) ----
+// A load takes slices of whole 32-SNP blocks (row0 a multiple of 32; the last slice may end mid-block) of a .bed image
+// (src: the slice's row r at r * nb bytes, any alignment: the file's rows follow a 3-byte magic number).  Per slice:
+//   load_orient_kernel   per row: the stored orientation (flip) from the codes of its first LOAD_ORIENT_BYTES bytes
+//                        (rows with more hom-A2 than hom-A1 calls there are stored 00 <-> 11 swapped, see below) and
+//                        its missing-flag word cleared;
+//   load_tiled_kernel    per (block, part): the block's chunks in the interleaved layout (a wave writes whole 1 KiB
+//                        chunks: lane l = row l / 2, half l % 2 of its 32 bytes), swapped where flipped, the pitch
+//                        padding and the padding rows of the last block 0x55, each row's (stored) last byte saved, and
+//                        the row's missing calls among the individual slots of both sample orders ORed into its flags.
+// Then load_flags_kernel narrows the flags to row_miss.  Any orientation gives the same results (the stats and the
+// replay take flip into account); deciding it from the row's head keeps the load one pass over the rows, where the
+// whole-row count it replaces needed a second pass that read and rewrote every swapped row (PLINK data, A1 minor:
+// nearly all).
+constexpr int LOAD_ORIENT_BYTES = 1024;
+
+// 16 source bytes at any alignment: aligned dword loads + byte shifts (src + o .. + 16 must lie within the buffer and
+// so must the dword after it when o is not a multiple of 4: the caller keeps the last units of a row on the byte path)
+__device__ __forceinline__ uint4 load16_unaligned(const uint8_t* __restrict__ src, size_t o) {
+    const size_t a = o & ~(size_t)3;
+    const uint32_t sh = (uint32_t)(o & 3);
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(src + a);
+    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3];
+    const uint32_t d4 = sh ? p[4] : 0u;
+    return make_uint4(__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                      __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh));
+}
+// bytes [p0, p0 + 16) of a row of nb bytes (bytes past it read as `fill`), one byte at a time
+__device__ __forceinline__ uint4 load16_bytes(const uint8_t* __restrict__ row, int p0, int nb, uint32_t fill) {
+    uint32_t w[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            uint32_t v = 0;
+    for (int q = 0; q < 4; ++q) {
+        uint32_t v = 0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int p = 16 * u + 4 * q + k;
-                v |= (uint32_t)(p < nb ? s[p] : 0x55u) << (8 * k);
-            }
-            w[q] = v;
+        for (int k = 0; k < 4; ++k) {
+            const int p = p0 + 4 * q + k;
+            v |= (uint32_t)(p < nb ? row[p] : fill) << (8 * k);
         }
-        *reinterpret_cast<uint4*>(img + tile_off(row0 + r, 16 * u, row_bytes)) = make_uint4(w[0], w[1], w[2], w[3]);
+        w[q] = v;
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ uint32_t swap_hom(uint32_t v) {  // 00 <-> 11 in every bit pair (het, missing unchanged)
+    const uint32_t q = ~(v ^ (v >> 1)) & 0x55555555u;
+    return v ^ (q | (q << 1));
+}
+
+// one wave per row (4 per workgroup): flip[row0 + r] and the row's missing-flag word cleared
+__global__ void __launch_bounds__(256) load_orient_kernel(const uint8_t* __restrict__ src, int nb, int row0, int n_rows,
+                                                          int orient, uint8_t* __restrict__ flip,
+                                                          uint32_t* __restrict__ miss_flags) {
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r >= n_rows) return;
+    int c0 = 0, c1 = 0, c2 = 0;
+    if (orient) {
+        const int head = min(nb, LOAD_ORIENT_BYTES);
+        const uint8_t* row = src + (size_t)r * nb;
+        const int p0 = 16 * lane;
+        if (p0 < head) {
+            // (bytes past the head, or past the row, read as 0x55: missing, counted in neither class)
+            const uint4 v = p0 + 20 <= nb && p0 + 16 <= head ? load16_unaligned(src, (size_t)r * nb + p0)
+                                                               : load16_bytes(row, p0, head, 0x55u);
+            count_codes(v.x, c0, c1, c2);
+            count_codes(v.y, c0, c1, c2);
+            count_codes(v.z, c0, c1, c2);
+            count_codes(v.w, c0, c1, c2);
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            c0 += __shfl_xor(c0, o, 64);
+            c2 += __shfl_xor(c2, o, 64);
+        }
+    }
+    if (lane == 0) {
+        flip[row0 + r] = (uint8_t)(c2 > c0);
+        miss_flags[row0 + r] = 0u;
     }
 }
 
-// After a load: save every row's last byte; rows [n_snp, n_rows) (the last 32-SNP block's padding SNPs) all 0x55.
-// One thread per row.
-__global__ void pad_rows_kernel(uint8_t* __restrict__ img, uint8_t* __restrict__ last, int n_snp, int n_rows, int nb,
-                                int row_bytes) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n_rows) return;
-    if (j < n_snp) {
-        last[j] = img[tile_off(j, nb - 1, row_bytes)];
-    } else {
-        const uint4 m = make_uint4(0x55555555u, 0x55555555u, 0x55555555u, 0x55555555u);
-        for (int p = 0; p < row_bytes; p += 16) *reinterpret_cast<uint4*>(img + tile_off(j, p, row_bytes)) = m;
+// grid (block of the slice, part): part p of P sweeps the block's chunks [p n_ch / P, (p + 1) n_ch / P); wave w
+// chunks t = lo + w, lo + w + 4, ...  n_snp: the image's SNPs (rows past it, in its last block: 0x55).  keep_compat /
+// keep_strict: the last byte's bit pairs that are individuals in the reference's / PLINK's sample order.
+constexpr int LOAD_U = 4;  // chunks in flight per lane
+__global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restrict__ src, int nb, int row0,
+                                                         int n_rows, int n_snp, uint8_t* __restrict__ img,
+                                                         int row_bytes, int P, const uint8_t* __restrict__ flip,
+                                                         uint8_t* __restrict__ last, uint32_t keep_compat,
+                                                         uint32_t keep_strict, uint32_t* __restrict__ miss_flags) {
+    __shared__ uint32_t rowflags[4][32];
+    const int bl = blockIdx.x / P, part = blockIdx.x % P, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i = lane >> 1, h = lane & 1;
+    const int r = 32 * bl + i, j = row0 + r;  // the lane's row: in the slice, in the image
+    const bool real = r < n_rows && j < n_snp;
+    const bool fl = real && flip[j];
+    const int n_ch = row_bytes >> 5;
+    const int t_lo = (int)((long long)n_ch * part / P), t_hi = (int)((long long)n_ch * (part + 1) / P);
+    uint8_t* blk = img + (size_t)(row0 / 32 + bl) * 32 * (size_t)row_bytes;
+    const size_t rbase = (size_t)r * nb;
+    // units [0, n_fast) of 16 bytes take the aligned-dword path (one dword past the unit stays inside the row)
+    const int n_fast = nb >= 20 ? (nb - 20) / 16 + 1 : 0;
+    uint32_t mflags = 0;  // bit 0 / 1: a missing call among the reference's / PLINK's individual slots
+    auto one = [&](int t, const uint4 v_in) {
+        const int u = 2 * t + h, p0 = 16 * u;
+        uint4 v = v_in;
+        if (fl) v = make_uint4(swap_hom(v.x), swap_hom(v.y), swap_hom(v.z), swap_hom(v.w));
+        *reinterpret_cast<uint4*>(blk + (size_t)t * 1024 + (size_t)i * 32 + 16 * h) = v;
+        if (!real) return;
+        if (p0 + 16 <= nb - 1) {
+            if (count_missing(v.x) + count_missing(v.y) + count_missing(v.z) + count_missing(v.w)) mflags |= 3u;
+        } else if (p0 <= nb - 1) {  // the unit holding the last byte: the bytes before it, then the byte per order
+            const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int p = p0 + 4 * q + k;
+                    const uint32_t byte = (wd[q] >> (8 * k)) & 0xFFu;
+                    if (p < nb - 1 && count_missing(byte)) mflags |= 3u;
+                    if (p == nb - 1) {
+                        last[j] = (uint8_t)byte;
+                        if (count_missing(byte & keep_compat)) mflags |= 1u;
+                        if (count_missing(byte & keep_strict)) mflags |= 2u;
+                    }
+                }
+        }
+    };
+    auto fetch = [&](int t) -> uint4 {
+        const int u = 2 * t + h;
+        // (rows past the slice end the image: the last block's padding rows)
+        if (r >= n_rows) return make_uint4(0x55555555u, 0x55555555u, 0x55555555u, 0x55555555u);
+        return u < n_fast ? load16_unaligned(src, rbase + 16 * (size_t)u) : load16_bytes(src + rbase, 16 * u, nb, 0x55u);
+    };
+    int t = t_lo + w;
+    for (; t + 4 * (LOAD_U - 1) < t_hi; t += 4 * LOAD_U) {
+        uint4 v[LOAD_U];
+#pragma unroll
+        for (int k = 0; k < LOAD_U; ++k) v[k] = fetch(t + 4 * k);
+#pragma unroll
+        for (int k = 0; k < LOAD_U; ++k) one(t + 4 * k, v[k]);
     }
+    for (; t < t_hi; t += 4) one(t, fetch(t));
+    // rows' flags: the lane pair, then the four waves, then one atomic per row and workgroup
+    mflags |= __shfl_xor(mflags, 1, 64);
+    if (h == 0) rowflags[w][i] = mflags;
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        const uint32_t f = rowflags[0][threadIdx.x] | rowflags[1][threadIdx.x] | rowflags[2][threadIdx.x] |
+                           rowflags[3][threadIdx.x];
+        const int jj = row0 + 32 * bl + threadIdx.x;
+        if (f && 32 * bl + threadIdx.x < n_rows && jj < n_snp) atomicOr(miss_flags + jj, f);
+    }
+}
+
+__global__ void load_flags_kernel(const uint32_t* __restrict__ miss_flags, int n_snp, uint8_t* __restrict__ row_miss) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n_snp) row_miss[j] = (uint8_t)miss_flags[j];
 }
 
 // Block sweeps of the resident layout: a workgroup of 4 waves takes 32-SNP block b; per chunk t a wave reads the
@@ -120,94 +240,6 @@ __device__ __forceinline__ void block_row_sums(BlockRed& sh, const int (&c)[3], 
 #pragma unroll
         for (int k = 0; k < 3; ++k) out[k] = sh.v[0][threadIdx.x][k] + sh.v[1][threadIdx.x][k] + sh.v[2][threadIdx.x][k] +
                                              sh.v[3][threadIdx.x][k];
-    }
-}
-
-// After a load (after pad_rows_kernel): store every SNP in its minor-homozygote-is-00 orientation.
-// Rows with more hom-A2 (11) than hom-A1 (00) calls get 00 <-> 11 swapped in place (het 10 and
-// missing 01 unchanged; the saved last byte too) and flip[j] = 1.  The exact kernels' operands are then
-// mostly zero whatever the file's allele order (PLINK usually writes A1 = minor, so A2 = major), which
-// keeps the matrix cores' power, and the chip's clock, where the synthetic A2-minor data has it.
-// One workgroup per block: count every byte of the rows, then swap the rows that need it.
-__global__ void __launch_bounds__(256) orient_rows_kernel(uint8_t* __restrict__ img, uint8_t* __restrict__ last,
-                                                          int n_snp, int row_bytes, uint8_t* __restrict__ flip) {
-    __shared__ BlockRed red;
-    __shared__ int swap[32];
-    const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int n_ch = row_bytes >> 5, j = 32 * b + (lane >> 1);
-    uint4* blk = reinterpret_cast<uint4*>(img + (size_t)b * 32 * (size_t)row_bytes);
-    int c[3] = {0, 0, 0};
-    for (int t = w; t < n_ch; t += 4) {
-        const uint4 v = blk[(size_t)t * 64 + lane];
-        count_codes(v.x, c[0], c[1], c[2]);
-        count_codes(v.y, c[0], c[1], c[2]);
-        count_codes(v.z, c[0], c[1], c[2]);
-        count_codes(v.w, c[0], c[1], c[2]);
-    }
-    int tot[3];
-    block_row_sums(red, c, tot);
-    if (threadIdx.x < 32) {
-        const int jj = 32 * b + threadIdx.x;
-        const int sw = jj < n_snp && tot[2] > tot[0];
-        swap[threadIdx.x] = sw;
-        if (jj < n_snp) {
-            flip[jj] = (uint8_t)sw;
-            if (sw) {
-                const uint32_t lb = last[jj], q = ~(lb ^ (lb >> 1)) & 0x55u;
-                last[jj] = (uint8_t)(lb ^ (q | (q << 1)));
-            }
-        }
-    }
-    __syncthreads();
-    if (j >= n_snp || !swap[lane >> 1]) return;
-    auto sw4 = [](uint32_t v) {
-        const uint32_t q = ~(v ^ (v >> 1)) & 0x55555555u;  // pairs 00 or 11
-        return v ^ (q | (q << 1));
-    };
-    for (int t = w; t < n_ch; t += 4) {
-        const uint4 v = blk[(size_t)t * 64 + lane];
-        blk[(size_t)t * 64 + lane] = make_uint4(sw4(v.x), sw4(v.y), sw4(v.z), sw4(v.w));
-    }
-}
-
-// After a load: which rows hold a missing call (code 01) among the individual slots of each sample order —
-// row_miss[j] bit 0 for the reference's order (the last byte keeps its high N % 4 pairs), bit 1 for PLINK's (the low
-// pairs); the other slots of the last byte and the pitch padding are not individuals.  It does not depend on the run's
-// parameters, so the fp4 band's routing (blk_miss) is known before the per-run count kernel finishes.  One workgroup
-// per block; bytes [0, nb - 1) in the sweep, the last byte from its saved copy.
-__device__ __forceinline__ int count_missing(uint32_t word) {
-    return __popc(~(word >> 1) & word & 0x55555555u);  // pairs 01
-}
-__global__ void __launch_bounds__(256) row_missing_kernel(const uint8_t* __restrict__ img,
-                                                          const uint8_t* __restrict__ last, int n_snp, int nb,
-                                                          int row_bytes, uint32_t keep_compat, uint32_t keep_strict,
-                                                          uint8_t* __restrict__ row_miss) {
-    __shared__ BlockRed red;
-    const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int h = lane & 1;
-    const uint4* blk = reinterpret_cast<const uint4*>(img + (size_t)b * 32 * (size_t)row_bytes);
-    const int n_full = (nb - 1) >> 5;  // chunks wholly before the last byte
-    int c[3] = {0, 0, 0};
-    for (int t = w; t < n_full; t += 4) {
-        const uint4 v = blk[(size_t)t * 64 + lane];
-        c[0] += count_missing(v.x) + count_missing(v.y) + count_missing(v.z) + count_missing(v.w);
-    }
-    if (w == 0 && 32 * n_full < nb - 1) {  // the chunk holding the last byte: its bytes before it
-        const uint4 v = blk[(size_t)n_full * 64 + lane];
-        const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (32 * n_full + 16 * h + 4 * q + k < nb - 1) c[0] += count_missing((wd[q] >> (8 * k)) & 0xFFu);
-    }
-    int tot[3];
-    block_row_sums(red, c, tot);
-    const int j = 32 * b + threadIdx.x;
-    if (threadIdx.x < 32 && j < n_snp) {
-        const uint32_t lb = last[j];
-        const int mc = tot[0] | count_missing(lb & keep_compat), ms = tot[0] | count_missing(lb & keep_strict);
-        row_miss[j] = (uint8_t)((mc ? 1 : 0) | (ms ? 2 : 0));
     }
 }
 
@@ -255,8 +287,9 @@ __global__ void block_missing_rows_kernel(const uint8_t* __restrict__ row_miss, 
 // plane (their m products are skipped); its epilogue counts o = 1 - m over the n_org individual slots.
 // Grid: (block, part): part p of P sweeps chunks [p n_tail / P, (p + 1) n_tail / P) of the chunks before the last
 // byte's (16-byte non-temporal loads, 8 in flight per lane); part P - 1's wave 0 also rebuilds, writes and counts the
-// tail chunks (the last byte's and the padding after it), discounting 00-coded padding (n_pad00 slots).  Partial
-// counts go to `counts` (zeroed first) by atomics.
+// tail chunks (the last byte's and the padding after it), discounting 00-coded padding (n_pad00 slots).  Part p's
+// counts of SNP j go to parts[(p n_snp + j) 3 + k] (plain stores: no memset before the kernel, no atomics);
+// snp_stats_kernel adds the P parts.
 typedef uint32_t u32x4nt __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void count_chunk(const u32x4nt o, int (&c)[3]) {
     count_codes(o.x, c[0], c[1], c[2]);
@@ -267,7 +300,7 @@ __device__ __forceinline__ void count_chunk(const u32x4nt o, int (&c)[3]) {
 
 __global__ void __launch_bounds__(256) count_rows_kernel(uint8_t* __restrict__ img, const uint8_t* __restrict__ last,
                                                          int n_snp, int nb, int row_bytes, uint32_t tail_keep,
-                                                         uint32_t pad, int n_pad00, int P, int* __restrict__ counts) {
+                                                         uint32_t pad, int n_pad00, int P, int* __restrict__ parts) {
     __shared__ BlockRed red;
     const int b = blockIdx.x / P, part = blockIdx.x % P, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int h = lane & 1, j = 32 * b + (lane >> 1);
@@ -311,9 +344,10 @@ __global__ void __launch_bounds__(256) count_rows_kernel(uint8_t* __restrict__ i
     block_row_sums(red, c, tot);
     const int jj = 32 * b + threadIdx.x;
     if (threadIdx.x < 32 && jj < n_snp) {
-        atomicAdd(counts + (size_t)jj * 4 + 0, tot[0]);
-        atomicAdd(counts + (size_t)jj * 4 + 1, tot[1]);
-        atomicAdd(counts + (size_t)jj * 4 + 2, tot[2]);
+        int* o = parts + ((size_t)part * n_snp + jj) * 3;
+        o[0] = tot[0];
+        o[1] = tot[1];
+        o[2] = tot[2];
     }
 }
 
@@ -352,7 +386,10 @@ __device__ __forceinline__ Coding coding_moments(double c0, double c1, double c2
 // the exact epilogue and the fp32 lookup table describe the stored coding the band kernels read.
 // Swapping the alleles negates A and leaves R unchanged (the residual of [x >= 1] and of [x <= 1] on
 // span{1, x} is the same vector), so every r^2 is the same.
-__global__ void snp_stats_kernel(const int* __restrict__ counts, const uint8_t* __restrict__ flip,
+// parts / P: the count kernel's per-part genotype counts, summed here into counts[4 j + k] (read by the rare-variant
+// kernels after this one).  zero: a word to clear (the deferred rare-variant slot counter), no memset of its own.
+__global__ void snp_stats_kernel(const int* __restrict__ parts, int P, int* __restrict__ counts, int* __restrict__ zero,
+                                 const uint8_t* __restrict__ flip,
                                  const double* __restrict__ pos, int n_snp, int n_snp_pad, int n_org, double maf_thr,
                                  double std_thr, float2* __restrict__ lut, SnpConst* __restrict__ cst,
                                  uint8_t* __restrict__ sflags, double* __restrict__ maf_out,
@@ -360,6 +397,7 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const uint8_t* 
                                  double* __restrict__ l2d_acc, int* __restrict__ ws_acc, uint8_t* __restrict__ blk_rep) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_snp_pad) return;
+    if (j == 0 && zero != nullptr) *zero = 0;
     if (j < n_snp && l2_acc != nullptr) {  // the band's per-SNP accumulators and the replay's block flags start at 0
         l2_acc[j] = 0.0;
         l2d_acc[j] = 0.0;
@@ -372,7 +410,17 @@ __global__ void snp_stats_kernel(const int* __restrict__ counts, const uint8_t* 
     uint8_t fl = 0;
     double sX = 0.0, sH = 0.0, sOb = 0.0;
     if (j < n_snp) {
-        const double s0 = counts[4 * (size_t)j], c1 = counts[4 * (size_t)j + 1], s2 = counts[4 * (size_t)j + 2];
+        int q[3] = {0, 0, 0};
+        for (int p = 0; p < P; ++p) {
+            const int* o = parts + ((size_t)p * n_snp + j) * 3;
+            q[0] += o[0];
+            q[1] += o[1];
+            q[2] += o[2];
+        }
+        counts[4 * (size_t)j] = q[0];
+        counts[4 * (size_t)j + 1] = q[1];
+        counts[4 * (size_t)j + 2] = q[2];
+        const double s0 = q[0], c1 = q[1], s2 = q[2];
         const bool fj = flip != nullptr && flip[j];
         const double c0 = fj ? s2 : s0, c2 = fj ? s0 : s2;  // the file's coding
         sX = c1 + 2.0 * s2;  // sums over the stored coding's indicators
@@ -1810,7 +1858,7 @@ __device__ __forceinline__ bool routed_item(const uint8_t* blk_miss, int route_s
 // NCX 2 (additive-only, unsegmented): items (I, J, 2) pair column blocks J and J + 1 in one wave (a 32 x 64 tile: the
 // row strip decoded once for both), as the plan emits them with pairing; a column block the super-item routing sends
 // elsewhere (blk_miss) is dropped from its item here.
-template <bool DOM, int WPS, int SEG, bool KC, int NCX = 1>
+template <bool DOM, int WPS, int SEG, bool KC, int NCX = 1, bool PERSIST = false>
 __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
                                                         const SnpConst* __restrict__ cst, const int4* __restrict__ items,
                                                         const double* __restrict__ pos, const int* __restrict__ Lw,
@@ -1821,10 +1869,10 @@ __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __rest
                                                         const uint8_t* __restrict__ blk_rep,
                                                         const uint8_t* __restrict__ blk_miss, int route_shift,
                                                         float* __restrict__ rep_gram, int4* __restrict__ rep_items,
-                                                        int* __restrict__ rep_count) {
+                                                        int* __restrict__ rep_count, int persist_items) {
     __shared__ BandI8Lds sh;
     __shared__ float tr[32 * 33];
-    const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
+    auto item = [&](const int4 it) __attribute__((always_inline)) {  // (not a call: the body's registers stay live)
     if (skip_item<KC>(blk_rep, it)) {
         // rep_gram (unsegmented rows): an item holding a replayed rare variant runs its K loop here anyway, storing the
         // exact Gram tiles of each of its block pairs in a slot of rep_gram; band_f4_epi_kernel<DOM, true> applies the
@@ -1877,6 +1925,21 @@ __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __rest
     if (blk_miss != nullptr && routed_item(blk_miss, route_shift, it.x, it.y, (n_snp + 31) >> 5)) return;
     if (it.y == it.x) NLDSC_BODY(1, true, it); else NLDSC_BODY(1, false, it);
 #undef NLDSC_BODY
+    };
+    if constexpr (!PERSIST) {
+        item(items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x]);
+    } else {
+        // persistent rounds (study: option band_persist): one workgroup per wave slot walks the rounds of `items`, round
+        // k = items [k S, k S + S) with S = gridDim.x in the same per-XCD order as a round launch, without the launch
+        // boundary between rounds (a wave starts its next item as soon as it finishes one)
+        const int S = gridDim.x;
+        for (int base = 0; base < persist_items; base += S) {
+            const int n = min(S, persist_items - base);
+            if ((int)blockIdx.x >= n) break;
+            __syncthreads();  // (the slot tables of the previous item were read)
+            item(items[base + (xcd ? xcd_slot(blockIdx.x, n) : blockIdx.x)]);
+        }
+    }
 }
 
 // ---- 2 x 2 block-pair workgroups: the operand feed ----
@@ -2067,13 +2130,13 @@ struct QLds {
     SnpConst cst[Q_SLOTS];
 };
 
-// one K step of a wave's four block pairs (a, b).  WM = false (missing-free): g0 = x.x, g1 = x.h, g2 = h.x (2^-1-scaled
-// h planes; additive-only: x.x alone).  WM (additive-only super-items holding missing calls): g0 = v.v, g1 = v.m,
-// g2 = m.v, g3 = m.m — the single-block kernel's four additive products.
-template <bool DOM, bool WM>
+// one K step of a wave's four block pairs (a, b) of a missing-free super-item: g0 = x.x, g1 = x.h, g2 = h.x
+// (2^-1-scaled h planes; additive-only: x.x alone).  (Round 3's study mode that also sent additive-only super-items
+// holding missing calls here, with the four products of the missing basis, measured C2 band 2.29 -> 4.13 ms and is
+// gone: profiles/r03_ab_quad_add_rejected.json.)
+template <bool DOM>
 __device__ __forceinline__ void q_step(const F4Frag (&A)[2], const F4Frag (&B)[2], f32x16v (&g0)[4], f32x16v (&g1)[4],
-                                       f32x16v (&g2)[4], f32x16v (&g3)[4]) {
-    static_assert(!(DOM && WM), "add+dom quad super-items are missing-free");
+                                       f32x16v (&g2)[4]) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         const F4Frag& a = A[p >> 1];
@@ -2083,14 +2146,9 @@ __device__ __forceinline__ void q_step(const F4Frag (&A)[2], const F4Frag (&B)[2
             g1[p] = mfma_f4<E8M0_ONE, E8M0_HALF>(a.x, b.h, g1[p]);
             g2[p] = mfma_f4<E8M0_HALF, E8M0_ONE>(a.h, b.x, g2[p]);
         }
-        if (WM) {
-            g1[p] = mfma_f4(a.x, b.o, g1[p]);
-            g2[p] = mfma_f4(a.o, b.x, g2[p]);
-            g3[p] = mfma_f4(a.o, b.o, g3[p]);
-        }
     }
-    constexpr int n_mfma = DOM || WM ? (WM ? 16 : 12) : 4;
-    constexpr int n_valu = 4 * (WM ? 14 : DOM ? 12 : 8);  // the next step's four decodes
+    constexpr int n_mfma = DOM ? 12 : 4;
+    constexpr int n_valu = 4 * (DOM ? 12 : 8);  // the next step's four decodes
 #pragma unroll
     for (int m = 0; m < n_mfma; ++m) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -2098,9 +2156,7 @@ __device__ __forceinline__ void q_step(const F4Frag (&A)[2], const F4Frag (&B)[2
     }
 }
 
-// ADDM (additive-only runs): every super-item runs here (the host routes none to the single-block kernel); those whose
-// blocks hold missing calls take the four additive products of the missing basis (WM), the others x.x alone.
-template <bool DOM, int S, bool KC, bool ADDM = false>
+template <bool DOM, int S, bool KC>
 __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
     const uint32_t* __restrict__ geno, int pitch_words, int n_it, const SnpConst* __restrict__ cst,
     const int4* __restrict__ items, const int2* __restrict__ rows, int nblk, const double* __restrict__ pos,
@@ -2120,9 +2176,7 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
         for (int s = 0; s < 8; ++s) rep |= blk_rep[min(strip_blk(s), nblk - 1)] != 0;
         if (KC ? !rep : rep) return;
     }
-    static_assert(!(ADDM && DOM), "ADDM: additive-only runs");
-    const bool wm = ADDM && !q_routed(blk_miss, I4, J4, nblk);  // (workgroup-uniform)
-    if (!ADDM && !q_routed(blk_miss, I4, J4, nblk)) return;  // the single-block kernel's
+    if (!q_routed(blk_miss, I4, J4, nblk)) return;  // the single-block kernel's
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, i = lane & 31, h = lane >> 5;
     {
         const int b = strip_blk(tid >> 5);
@@ -2178,9 +2232,9 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
 #pragma unroll
     for (int t = 0; t < S; ++t) issue(t);
 
-    f32x16v g0[4], g1[4], g2[4], g3[4];
+    f32x16v g0[4], g1[4], g2[4];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) g0[p] = g1[p] = g2[p] = g3[p] = f32x16v{};
+    for (int p = 0; p < 4; ++p) g0[p] = g1[p] = g2[p] = f32x16v{};
     // as the 2 x 2 kernel's ring: stage t read into registers one stage ahead, S - 1 stages in flight
     auto read_stage = [&](int t, uint4 (&ra)[2][2], uint4 (&rb)[2][2]) {
 #pragma unroll
@@ -2191,8 +2245,8 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
                 rb[k][c] = sh.stage[t % S][cs + k][c][lane];
             }
     };
-    auto kloop = [&](auto ACTc, auto WMc) {
-        constexpr bool ACT = decltype(ACTc)::value, WM = decltype(WMc)::value;
+    auto kloop = [&](auto ACTc) {
+        constexpr bool ACT = decltype(ACTc)::value;
         uint4 ra[2][2], rb[2][2];
         wait_vmcnt<4 * (S - 1)>();  // stage 0 landed (this wave's loads)
         __builtin_amdgcn_s_barrier();  // every wave's
@@ -2213,16 +2267,16 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
                     F4Frag A[2], B[2];
 #pragma unroll
                     for (int k = 0; k < 2; ++k) {
-                        A[k] = decode_f4<WM>(ra[k][c].x, ra[k][c].y);
-                        B[k] = decode_f4<WM>(rb[k][c].x, rb[k][c].y);
+                        A[k] = decode_f4<false>(ra[k][c].x, ra[k][c].y);
+                        B[k] = decode_f4<false>(rb[k][c].x, rb[k][c].y);
                     }
-                    q_step<DOM, WM>(A, B, g0, g1, g2, g3);
+                    q_step<DOM>(A, B, g0, g1, g2);
 #pragma unroll
                     for (int k = 0; k < 2; ++k) {
-                        A[k] = decode_f4<WM>(ra[k][c].z, ra[k][c].w);
-                        B[k] = decode_f4<WM>(rb[k][c].z, rb[k][c].w);
+                        A[k] = decode_f4<false>(ra[k][c].z, ra[k][c].w);
+                        B[k] = decode_f4<false>(rb[k][c].z, rb[k][c].w);
                     }
-                    q_step<DOM, WM>(A, B, g0, g1, g2, g3);
+                    q_step<DOM>(A, B, g0, g1, g2);
                 }
 #pragma unroll
                 for (int k = 0; k < 2; ++k)
@@ -2231,13 +2285,8 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
             }
         }
     };
-    if (!any) kloop(std::false_type{}, std::false_type{});
-    else if constexpr (ADDM) {
-        if (wm) kloop(std::true_type{}, std::true_type{});
-        else kloop(std::true_type{}, std::false_type{});
-    } else {
-        kloop(std::true_type{}, std::false_type{});
-    }
+    if (!any) kloop(std::false_type{});
+    else kloop(std::true_type{});
     wait_vmcnt<0>();  // the tail's surplus loads
     if (!any) return;  // no barrier follows
     const f32x16v z = {};
@@ -2245,16 +2294,10 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
     for (int p = 0; p < 4; ++p) {
         if (!need[p]) continue;
         const int rb = strip_blk(rs + (p >> 1)), cb = 4 * J4 + 2 * (w & 1) + (p & 1);
-        // (missing-free: the m products are 0, as in the single-block kernel's RM = CM = false loop; WM: g1..g3 are
-        // v.m, m.v, m.m, all computed on a diagonal pair too)
-        if constexpr (ADDM)
-            pair_epilogue<false, f32x16v, true, KC>(sh.info, sh.cst, 32 * (rs + (p >> 1)), 32 * (cs + (p & 1)), rb == cb,
-                                                    i, h, g0[p], g1[p], g2[p], g3[p], z, z, z, z, ld_wind, n_org,
-                                                    rsq_thr, n_org, own_lo, own_hi, n_snp, l2_acc, l2d_acc, ws_acc);
-        else
-            pair_epilogue<DOM, f32x16v, true, KC>(sh.info, sh.cst, 32 * (rs + (p >> 1)), 32 * (cs + (p & 1)), rb == cb,
-                                                  i, h, g0[p], z, z, z, g1[p], z, g2[p], z, ld_wind, n_org, rsq_thr,
-                                                  n_org, own_lo, own_hi, n_snp, l2_acc, l2d_acc, ws_acc);
+        // (missing-free: the m products are 0, as in the single-block kernel's RM = CM = false loop)
+        pair_epilogue<DOM, f32x16v, true, KC>(sh.info, sh.cst, 32 * (rs + (p >> 1)), 32 * (cs + (p & 1)), rb == cb, i,
+                                              h, g0[p], z, z, z, g1[p], z, g2[p], z, ld_wind, n_org, rsq_thr, n_org,
+                                              own_lo, own_hi, n_snp, l2_acc, l2d_acc, ws_acc);
     }
 }
 
@@ -2314,8 +2357,7 @@ __global__ void issued_products_kernel(const int4* __restrict__ items, int n_ite
                                        int nblk, int kind, int dom, int routed, int route_shift,
                                        unsigned long long* __restrict__ out) {
     // routed bit 0: single items the routing sends to a super-item kernel are not counted here (an uncompacted
-    // list); bit 1: super-items count only when routed to their kernel; bit 2: additive-only quad run — every
-    // super-item goes to the quad kernel (4 products per pair where its blocks hold missing calls), no single item
+    // list); bit 1: super-items count only when routed to their kernel
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long n = 0;
     if (t < n_items) {
@@ -2324,7 +2366,7 @@ __global__ void issued_products_kernel(const int4* __restrict__ items, int n_ite
         if (kind == 2) {  // (it.z == 2: additive-only column-block pairs, one product set per column block)
             for (int c = 0; c < it.z; ++c) {
                 const int J = it.y + c;
-                if ((routed & 1) && ((routed & 4) || routed_item(blk_miss, route_shift, it.x, J, nblk))) continue;
+                if ((routed & 1) && routed_item(blk_miss, route_shift, it.x, J, nblk)) continue;
                 const int rm = blk_miss[it.x] != 0, cm = blk_miss[J] != 0, nd = it.x != J;
                 n += 1 + cm + rm * nd + rm * cm + (dom ? 1 + nd + rm + cm * nd : 0);
             }
@@ -2336,15 +2378,14 @@ __global__ void issued_products_kernel(const int4* __restrict__ items, int n_ite
     } else if (items2 != nullptr && t < n_items + n_items2 && route_shift == 2) {
         // quad super-items (missing-free): a wave with any needed block pair issues all four pairs' products
         const int4 it = items2[t - n_items];
-        const bool wm = (routed & 4) && !q_routed(blk_miss, it.x, it.y, nblk);
-        if (!(routed & 2) || (routed & 4) || q_routed(blk_miss, it.x, it.y, nblk)) {
+        if (!(routed & 2) || q_routed(blk_miss, it.x, it.y, nblk)) {
             for (int w = 0; w < 4; ++w) {
                 bool any = false;
                 for (int p = 0; p < 4; ++p) {
                     const int rb = 4 * it.x + 2 * (w >> 1) + (p >> 1), cb = 4 * it.y + 2 * (w & 1) + (p & 1);
                     any |= rb < nblk && cb < nblk && cb - rb >= rows[rb].x && cb - rb <= rows[rb].y;
                 }
-                n += any ? 4 * (dom ? 3 : wm ? 4 : 1) : 0;
+                n += any ? 4 * (dom ? 3 : 1) : 0;
             }
         }
     } else if (items2 != nullptr && t < n_items + n_items2) {
@@ -2503,6 +2544,61 @@ __global__ void finalize_kernel(const int* __restrict__ Lw, const double* __rest
     }
 }
 
+// finalize_kernel for host-result runs (nldsc_engine_run): the owned slice goes straight to host memory (pinned,
+// device-mapped: the caller's arrays when they are nldsc_host_alloc buffers, else the engine's landing buffer) — no
+// device copy, no DMA after the band — and each workgroup's sums of positive WSA / WSD to wsum (host memory, plain
+// stores: a same-address atomic per workgroup serialised to ~30 us at 80 000 SNPs).
+constexpr int FINALIZE_OUT_WG = 256;
+__global__ void __launch_bounds__(FINALIZE_OUT_WG) finalize_out_kernel(
+    const int* __restrict__ Lw, const double* __restrict__ l2_acc, const double* __restrict__ l2d_acc,
+    const int* __restrict__ ws_acc, const double* __restrict__ maf_in, const double* __restrict__ rstd_in, int n_snp,
+    int own_lo, int own_hi, int dom, double* __restrict__ l2, double* __restrict__ l2d, double* __restrict__ maf,
+    double* __restrict__ rstd, int* __restrict__ wsa, int* __restrict__ wsd, int* __restrict__ wsde,
+    unsigned long long* __restrict__ wsum) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x, g = own_lo + c;
+    unsigned long long sa = 0, sd = 0;
+    if (g < own_hi) {
+        const double qnan = __builtin_nan("");
+        double a2 = qnan, d2 = qnan;
+        int a = -1, d = -1, x = -1;
+        if (Lw[g] >= 0) {  // computed SNP (ldscalc.h:49-54)
+            const int nanf = ws_acc[3 * (size_t)n_snp + g];
+            const long long la = reinterpret_cast<const long long*>(l2_acc)[g];
+            const long long ld = reinterpret_cast<const long long*>(l2d_acc)[g];
+            a2 = (nanf & 1) ? qnan : 1.0 + (double)la / ACC_SCALE;
+            d2 = dom && !(nanf & 2) ? (double)ld / ACC_SCALE : qnan;
+            a = ws_acc[g];
+            d = dom ? ws_acc[(size_t)n_snp + g] : -1;
+            x = dom ? ws_acc[2 * (size_t)n_snp + g] : -1;
+        }
+        l2[c] = a2;
+        l2d[c] = d2;
+        maf[c] = maf_in[g];
+        rstd[c] = rstd_in[g];
+        wsa[c] = a;
+        wsd[c] = d;
+        wsde[c] = x;
+        sa = a > 0 ? (unsigned long long)a : 0ull;
+        sd = d > 0 ? (unsigned long long)d : 0ull;
+    }
+    __shared__ unsigned long long part[2][FINALIZE_OUT_WG / 64];
+    for (int o = 32; o > 0; o >>= 1) {
+        sa += __shfl_down(sa, o, 64);
+        sd += __shfl_down(sd, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        part[0][threadIdx.x >> 6] = sa;
+        part[1][threadIdx.x >> 6] = sd;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long ta = 0, td = 0;
+        for (int w = 0; w < FINALIZE_OUT_WG / 64; ++w) { ta += part[0][w]; td += part[1][w]; }
+        wsum[2 * blockIdx.x] = ta;
+        wsum[2 * blockIdx.x + 1] = td;
+    }
+}
+
 // Owned slice of the score table for the multi-GPU gather (nldsc_engine_run_device): row k of `table` = l2, l2d,
 // maf, rstd, WSA, WSD, WSDE (doubles), column c = SNP own_lo + c, NaN past the slice; and the metric's pair counts
 // (positive window sizes) summed per workgroup, one 64-bit atomic per workgroup and counter.
@@ -2613,45 +2709,51 @@ __global__ void __launch_bounds__(256) synth_bed_kernel(uint8_t* __restrict__ ro
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
-hipError_t launch_pad_rows(uint8_t* img, uint8_t* last, int n_snp, int n_rows, int nb, int row_bytes,
-                           hipStream_t st) {
+hipError_t launch_load_slice(const uint8_t* src, int nb, int row0, int n_rows, int n_snp, uint8_t* img, int row_bytes,
+                             bool orient, uint8_t* flip, uint8_t* last, uint32_t keep_compat, uint32_t keep_strict,
+                             uint32_t* miss_flags, hipStream_t st) {
     if (n_rows <= 0) return hipSuccess;
-    hipLaunchKernelGGL(pad_rows_kernel, dim3((n_rows + 255) / 256), dim3(256), 0, st, img, last, n_snp, n_rows, nb,
-                       row_bytes);
+    if (row0 % 32 != 0 || row0 + n_rows > n_snp) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(load_orient_kernel, dim3((n_rows + 3) / 4), dim3(256), 0, st, src, nb, row0, n_rows,
+                       orient ? 1 : 0, flip, miss_flags);
+    // parts per block: about 16 k workgroups over the whole image (as the count kernel), at least 8 chunks each
+    const int n_ch = row_bytes >> 5, nblk_img = (n_snp + 31) / 32, nblk = (n_rows + 31) / 32;
+    const int P = std::max(1, std::min(std::max(n_ch / 8, 1), (16384 + nblk_img - 1) / nblk_img));
+    hipLaunchKernelGGL(load_tiled_kernel, dim3(nblk * P), dim3(256), 0, st, src, nb, row0, n_rows, n_snp, img,
+                       row_bytes, P, flip, last, keep_compat, keep_strict, miss_flags);
     return hipGetLastError();
 }
 
-hipError_t launch_load_rows(const uint8_t* src, int nb, int row0, int n_rows, uint8_t* img, int row_bytes,
-                            hipStream_t st) {
-    if (n_rows <= 0) return hipSuccess;
-    const size_t n = (size_t)n_rows * (size_t)(row_bytes / 16);
-    const size_t blocks = std::min<size_t>((n + 255) / 256, (size_t)1 << 20);  // <= 2^28 work-items per dispatch
-    hipLaunchKernelGGL(load_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, nb, row0, n_rows, img,
-                       row_bytes);
-    return hipGetLastError();
-}
-
-hipError_t launch_count_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
-                             uint32_t pad, int n_pad00, int* counts, hipStream_t st) {
+hipError_t launch_load_flags(const uint32_t* miss_flags, int n_snp, uint8_t* row_miss, hipStream_t st) {
     if (n_snp <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * 4 * (size_t)n_snp, st);
-    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(load_flags_kernel, dim3((n_snp + 255) / 256), dim3(256), 0, st, miss_flags, n_snp, row_miss);
+    return hipGetLastError();
+}
+
+int count_parts(int n_snp, int nb) {
     // parts per block: about 16 k workgroups in all (8 resident per CU: several rounds, small tails), at least 8
     // chunks each
     const int nblk = (n_snp + 31) / 32, tc0 = (nb - 1) >> 5;
-    const int P = std::max(1, std::min(std::max(tc0 / 8, 1), (16384 + nblk - 1) / nblk));
+    return std::max(1, std::min(std::max(tc0 / 8, 1), (16384 + nblk - 1) / nblk));
+}
+
+hipError_t launch_count_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
+                             uint32_t pad, int n_pad00, int* parts, hipStream_t st) {
+    if (n_snp <= 0) return hipSuccess;
+    const int nblk = (n_snp + 31) / 32, P = count_parts(n_snp, nb);
     hipLaunchKernelGGL(count_rows_kernel, dim3(nblk * P), dim3(256), 0, st, img, last, n_snp, nb, row_bytes, tail_keep,
-                       pad, n_pad00, P, counts);
+                       pad, n_pad00, P, parts);
     return hipGetLastError();
 }
 
-hipError_t launch_snp_stats(const int* counts, const uint8_t* flip, const double* pos, int n_snp, int n_snp_pad,
-                            int n_org, double maf_thr, double std_thr, float2* lut, SnpConst* cst, uint8_t* sflags,
-                            double* maf_out, double* rstd_out, hipStream_t st, double* l2_acc, double* l2d_acc,
-                            int* ws_acc, uint8_t* blk_rep) {
+hipError_t launch_snp_stats(const int* parts, int P, int* counts, int* zero, const uint8_t* flip, const double* pos,
+                            int n_snp, int n_snp_pad, int n_org, double maf_thr, double std_thr, float2* lut,
+                            SnpConst* cst, uint8_t* sflags, double* maf_out, double* rstd_out, hipStream_t st,
+                            double* l2_acc, double* l2d_acc, int* ws_acc, uint8_t* blk_rep) {
     const int blocks = (n_snp_pad + 255) / 256;
-    hipLaunchKernelGGL(snp_stats_kernel, dim3(blocks), dim3(256), 0, st, counts, flip, pos, n_snp, n_snp_pad, n_org,
-                       maf_thr, std_thr, lut, cst, sflags, maf_out, rstd_out, l2_acc, l2d_acc, ws_acc, blk_rep);
+    hipLaunchKernelGGL(snp_stats_kernel, dim3(blocks), dim3(256), 0, st, parts, P, counts, zero, flip, pos, n_snp,
+                       n_snp_pad, n_org, maf_thr, std_thr, lut, cst, sflags, maf_out, rstd_out, l2_acc, l2d_acc, ws_acc,
+                       blk_rep);
     return hipGetLastError();
 }
 
@@ -2671,14 +2773,6 @@ hipError_t launch_reference_residuals(const uint8_t* img, int row_bytes, int n_o
     if (n_snp <= 0) return hipSuccess;
     hipLaunchKernelGGL(reference_residual_kernel, dim3(n_snp), dim3(64), 0, st, img, row_bytes, n_org, (int)strict,
                        counts, flip, n_snp, std_thr, cst, lut, sflags, rstd_out);
-    return hipGetLastError();
-}
-
-hipError_t launch_row_missing(const uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes,
-                              uint32_t keep_compat, uint32_t keep_strict, uint8_t* row_miss, hipStream_t st) {
-    if (n_snp <= 0) return hipSuccess;
-    hipLaunchKernelGGL(row_missing_kernel, dim3((n_snp + 31) / 32), dim3(256), 0, st, img, last, n_snp, nb, row_bytes, keep_compat,
-                       keep_strict, row_miss);
     return hipGetLastError();
 }
 
@@ -2710,12 +2804,6 @@ hipError_t launch_block_missing_rows(const uint8_t* row_miss, int n_snp, int ord
     if (nblk <= 0) return hipSuccess;
     hipLaunchKernelGGL(block_missing_rows_kernel, dim3((nblk + 255) / 256), dim3(256), 0, st, row_miss, n_snp, order,
                        blk_miss);
-    return hipGetLastError();
-}
-
-hipError_t launch_orient_rows(uint8_t* img, uint8_t* last, int n_snp, int row_bytes, uint8_t* flip, hipStream_t st) {
-    if (n_snp <= 0) return hipSuccess;
-    hipLaunchKernelGGL(orient_rows_kernel, dim3((n_snp + 31) / 32), dim3(256), 0, st, img, last, n_snp, row_bytes, flip);
     return hipGetLastError();
 }
 
@@ -2827,28 +2915,25 @@ hipError_t launch_band_f4_q(bool dom, int n_items4, const uint32_t* geno, int pi
                             const int* Lw, const int* Rw, const uint8_t* sflags, int n_snp, double ld_wind,
                             double n_org, double rsq_thr, int own_lo, int own_hi, double* l2_acc, double* l2d_acc,
                             int* ws_acc, bool xcd, const uint8_t* blk_rep, const uint8_t* blk_miss, int which,
-                            hipStream_t st, bool add_all, int round_items) {
+                            hipStream_t st, int round_items) {
     if (n_items4 <= 0) return hipSuccess;
-    if (n_it > F4_SEG_CHUNKS || n_it < 2 || (n_it & 1) || blk_miss == nullptr || (add_all && dom))
-        return hipErrorInvalidValue;
+    if (n_it > F4_SEG_CHUNKS || n_it < 2 || (n_it & 1) || blk_miss == nullptr) return hipErrorInvalidValue;
     // round_items > 0: launches of that many super-items (one workgroup per CU each), so the workgroups on an XCD
     // start together and stream their shared strips at nearby K offsets (not the KC launch)
     int chunk = round_items > 0 ? round_items : n_items4;
-#define NLDSC_BAND(DOM_, KC_, ADDM_)                                                                                \
+#define NLDSC_BAND(DOM_, KC_)                                                                                       \
     for (int o = 0; o < n_items4; o += chunk)                                                                        \
-    hipLaunchKernelGGL((band_f4_q_kernel<DOM_, Q_STAGES, KC_, ADDM_>), dim3(std::min(chunk, n_items4 - o)), dim3(256), \
+    hipLaunchKernelGGL((band_f4_q_kernel<DOM_, Q_STAGES, KC_>), dim3(std::min(chunk, n_items4 - o)), dim3(256),     \
                        0, st, geno, pitch_words, n_it, cst, items4 + o, rows, nblk, pos, Lw, Rw, sflags, n_snp,     \
                        ld_wind, n_org, rsq_thr, own_lo, own_hi, l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss)
     if (which & 1) {
-        if (dom) NLDSC_BAND(true, false, false);
-        else if (add_all) NLDSC_BAND(false, false, true);
-        else NLDSC_BAND(false, false, false);
+        if (dom) NLDSC_BAND(true, false);
+        else NLDSC_BAND(false, false);
     }
     chunk = n_items4;
     if (blk_rep && (which & 2)) {
-        if (dom) NLDSC_BAND(true, true, false);
-        else if (add_all) NLDSC_BAND(false, true, true);
-        else NLDSC_BAND(false, true, false);
+        if (dom) NLDSC_BAND(true, true);
+        else NLDSC_BAND(false, true);
     }
 #undef NLDSC_BAND
     return hipGetLastError();
@@ -2901,7 +2986,7 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
                           int which, hipStream_t st, const uint8_t* blk_miss, int round_items, int route_shift,
-                          float* rep_gram, int4* rep_items, int* rep_count) {
+                          float* rep_gram, int4* rep_items, int* rep_count, bool persist) {
     if (n_items <= 0) return hipSuccess;
     // single block-pair items, or (additive-only, unsegmented rows) column-block pairs
     if (max_nc != 1 && !(max_nc == 2 && !dom && n_it <= F4_SEG_CHUNKS)) return hipErrorInvalidValue;
@@ -2909,13 +2994,26 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
     // round_items > 0: the items go in launches of that many (one round of the wave slots each), see ld_engine.cpp;
     // not the KC launch (items holding a replayed rare variant: few, the others return at once)
     int chunk = round_items > 0 ? round_items : n_items;
-#define NLDSC_BAND_NC(DOM_, WPS_, SEG_, KC_, NCX_)                                                                  \
-    for (int o = 0; o < n_items; o += chunk)                                                                      \
-    hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_, KC_, NCX_>), dim3(std::min(chunk, n_items - o)), dim3(64), 0, \
-                       st, geno, pitch_words,                                                                         \
+    // persist (round launches only): one launch of `chunk` workgroups walking every round (band_f4_kernel
+    // persist_items)
+    // (add+dom, unsegmented rows, single block pairs: the variant instantiated with PERSIST)
+    int persist_n = persist && dom && n_it <= F4_SEG_CHUNKS && max_nc == 1 && round_items > 0 && n_items > chunk
+                        ? n_items : 0;
+#define NLDSC_BAND_LAUNCH(DOM_, WPS_, SEG_, KC_, NCX_, P_)                                                          \
+    hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_, KC_, NCX_, P_>), dim3(std::min(chunk, n_items - o)), dim3(64), \
+                       0, st, geno, pitch_words,                                                                      \
                        n_it, cst, items + o, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi,       \
                        l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss, route_shift, SEG_ ? nullptr : rep_gram, \
-                       rep_items, rep_count)
+                       rep_items, rep_count, persist_n)
+#define NLDSC_BAND_NC(DOM_, WPS_, SEG_, KC_, NCX_)                                                                  \
+    do {                                                                                                             \
+        for (int o = 0; o < n_items; o += (persist_n ? n_items : chunk)) {                                        \
+            if constexpr (DOM_ && SEG_ == 0 && !KC_ && NCX_ == 1) {                                                 \
+                if (persist_n) { NLDSC_BAND_LAUNCH(DOM_, WPS_, SEG_, KC_, NCX_, true); continue; }                   \
+            }                                                                                                        \
+            NLDSC_BAND_LAUNCH(DOM_, WPS_, SEG_, KC_, NCX_, false);                                                   \
+        }                                                                                                            \
+    } while (0)
 #define NLDSC_BAND(DOM_, WPS_, SEG_, KC_) NLDSC_BAND_NC(DOM_, WPS_, SEG_, KC_, 1)
 #define NLDSC_PICK(KC_)                                                                                              \
     if (n_it > F4_SEG_CHUNKS) { if (dom) NLDSC_BAND(true, 1, F4_SEG_CHUNKS, KC_); else NLDSC_BAND(false, 2, F4_SEG_CHUNKS, KC_); } \
@@ -2925,11 +3023,13 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
     // segmented kernel: the add+dom variant needs more than 256 registers (2 waves / SIMD would spill)
     if (which & 1) { NLDSC_PICK(false); }
     chunk = n_items;
+    persist_n = 0;
     // (with rep_gram the KC items ran their K loops in the main launch: launch_band_f4_deferred_epi after the replay)
     if (blk_rep && (which & 2) && (rep_gram == nullptr || n_it > F4_SEG_CHUNKS)) { NLDSC_PICK(true); }
 #undef NLDSC_PICK
 #undef NLDSC_BAND
 #undef NLDSC_BAND_NC
+#undef NLDSC_BAND_LAUNCH
     return hipGetLastError();
 }
 
@@ -2939,6 +3039,20 @@ hipError_t launch_finalize(const int* Lw, const double* l2_acc, const double* l2
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, st, Lw, l2_acc, l2d_acc, ws_acc, n_snp,
                        own_lo, own_hi, dom ? 1 : 0, l2, l2d, ws3);
+    return hipGetLastError();
+}
+
+int finalize_out_blocks(int n_own) { return (n_own + FINALIZE_OUT_WG - 1) / FINALIZE_OUT_WG; }
+
+hipError_t launch_finalize_out(const int* Lw, const double* l2_acc, const double* l2d_acc, const int* ws_acc,
+                               const double* maf_in, const double* rstd_in, int n_snp, int own_lo, int own_hi, bool dom,
+                               double* l2, double* l2d, double* maf, double* rstd, int* wsa, int* wsd, int* wsde,
+                               unsigned long long* wsum, hipStream_t st) {
+    const int n = own_hi - own_lo;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(finalize_out_kernel, dim3(finalize_out_blocks(n)), dim3(FINALIZE_OUT_WG), 0, st, Lw, l2_acc,
+                       l2d_acc, ws_acc, maf_in, rstd_in, n_snp, own_lo, own_hi, dom ? 1 : 0, l2, l2d, maf, rstd, wsa,
+                       wsd, wsde, wsum);
     return hipGetLastError();
 }
 

@@ -28,13 +28,25 @@ def _torch_ready(*tensors):
 
 
 class Engine:
-    def __init__(self, device: int = -1, lib_path: str | None = None):
+    # Engine options (C ABI nldsc_engine_set_option) applied to every new engine before `options`: test and study
+    # knobs of the schedule and kernel choice (all paths give the same results: the GPU tests compare them), empty by
+    # default.  See nldsc_amd/csrc/ld_engine.cpp nldsc_engine_set_option for the names.
+    default_options: dict = {}
+
+    def __init__(self, device: int = -1, lib_path: str | None = None, options: dict | None = None):
         self._L = L = _lib.lib(lib_path)
         self._h = ctypes.c_void_p()
         err = _lib.errbuf()
         _lib.check(L.nldsc_engine_create(int(device), ctypes.byref(self._h), err, len(err)), err)
         self.n_snp = 0
         self.n_org = 0
+        for name, value in {**Engine.default_options, **(options or {})}.items():
+            self.set_option(name, value)
+
+    def set_option(self, name: str, value: int):
+        """One engine option (nldsc_engine_set_option); "orient" applies from the next load."""
+        err = _lib.errbuf()
+        _lib.check(self._L.nldsc_engine_set_option(self._h, name.encode(), int(value), err, len(err)), err)
 
     def close(self):
         if self._h:

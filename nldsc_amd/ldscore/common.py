@@ -122,7 +122,9 @@ class FAMFile(PLINKFile):
         if not os.path.exists(self._path):
             raise FileNotFoundError(f'No such file: "{self._path}"')
         with open(self._path, "rb") as fh:
-            self._n_org = sum(1 for line in fh.read().split(b"\n") if line.rstrip(b"\r"))
+            # \n, \r\n and lone \r all end a row for pandas' C parser, which skips lines that are empty or hold
+            # only spaces (an empty file is 0 rows, as the reference's read_csv with `names` gives)
+            self._n_org = sum(1 for line in fh.read().splitlines() if line.strip(b" "))
         self._table = None
 
     @property

@@ -475,10 +475,8 @@ def test_halo_loaded_shards_assemble_to_full(engine, tmp_path):
 @pytest.mark.parametrize("seed", range(6))
 def test_gpu_schedule_matches_host_schedule(engine, seed):
     """Non-negative sorted positions take the GPU schedule (window edges by binary search, the drifting
-    right pointer as a prefix max, tile-ordered items by a prefix sum); NLDSC_GPU_PLAN=0 forces the host
+    right pointer as a prefix max, tile-ordered items by a prefix sum); engine option gpu_plan 0 forces the host
     replay.  Same block pairs, same scores, for whole runs and owned sub-ranges, narrow and wide bands."""
-    import os
-
     from nldsc_amd import synth
     from nldsc_amd.engine import Engine
     rng = np.random.default_rng(500 + seed)
@@ -492,27 +490,19 @@ def test_gpu_schedule_matches_host_schedule(engine, seed):
     w = float(rng.choice([0.5, 1.0, 5.0]))
     args = (w, 0.01, 1e-5, 1.0 / M, pos)
     owns = [(0, M), (M // 3, 2 * M // 3), (M - 1, M), (0, 1)]
-    old = os.environ.get("NLDSC_GPU_PLAN")
     out = {}
-    try:
-        for g in ("1", "0"):
-            os.environ["NLDSC_GPU_PLAN"] = g
-            with Engine(0) as e:
-                e.load_bed_bytes(synth.bed_bytes(rows), M, N)
-                out[g] = [(e.run(*args, own=o, flags=MODES["f4"] | _lib_flag("FLAG_EXACT_RARE")),
-                           e.timings()["band_items"]) for o in owns]
-    finally:
-        if old is None:
-            os.environ.pop("NLDSC_GPU_PLAN", None)
-        else:
-            os.environ["NLDSC_GPU_PLAN"] = old
-    for o, (a, na), (b, nb) in zip(owns, out["1"], out["0"]):
+    for g in (1, 0):
+        with Engine(0, options={"gpu_plan": g}) as e:
+            e.load_bed_bytes(synth.bed_bytes(rows), M, N)
+            out[g] = [(e.run(*args, own=o, flags=MODES["f4"] | _lib_flag("FLAG_EXACT_RARE")),
+                       e.timings()["band_items"]) for o in owns]
+    for o, (a, na), (b, nb) in zip(owns, out[1], out[0]):
         assert na == nb, (o, na, nb)
         sub = {k: v[o[0]:o[1]] for k, v in a.items()}
         ref = {k: v[o[0]:o[1]] for k, v in b.items()}
         same_gram(sub, ref, f"own {o}")
     exp = O.run_f64(rows, N, *args)
-    assert_ld_close(out["1"][0][0], exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
+    assert_ld_close(out[1][0][0], exp, tol=dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10),
                                                    maf=(0.0, 0.0)), label=f"gpu plan seed {seed}")
 
 
@@ -529,9 +519,7 @@ def _swap_alleles(rows, which):
 def test_allele_orientation_is_invisible(name):
     """The engine stores every SNP minor-homozygote-as-00 (rows with more 11 than 00 calls are swapped at
     load).  On a file whose alleles are swapped for half of the SNPs (A2 = major, PLINK's usual order), the
-    scores equal the fp64 truth of that file, and equal a run that keeps the file coding (NLDSC_ORIENT=0)."""
-    import os
-
+    scores equal the fp64 truth of that file, and equal a run that keeps the file coding (engine option orient 0)."""
     import torch
     torch.cuda.init()
     from nldsc_amd.engine import Engine
@@ -541,20 +529,12 @@ def test_allele_orientation_is_invisible(name):
     swapped = _swap_alleles(rows, np.arange(0, M, 2))
     args = (meta["ld_wind"], meta["maf"], meta["std_thr"], meta["rsq_thr"], pos)
     exp = O.run_f64(swapped, N, *args)
-    old = os.environ.get("NLDSC_ORIENT")
     out = {}
-    try:
-        for o in ("1", "0"):
-            os.environ["NLDSC_ORIENT"] = o
-            for mode in ("f4", "i8", "f32"):
-                with Engine(0) as e:  # swapped rare SNPs may lack hom-A1 calls: exact residuals vs the truth
-                    e.load_bed_bytes(b"\x6c\x1b\x01" + swapped.tobytes(), M, N)
-                    out[o, mode] = e.run(*args, flags=MODES[mode] | _lib_flag("FLAG_EXACT_RARE"))
-    finally:
-        if old is None:
-            os.environ.pop("NLDSC_ORIENT", None)
-        else:
-            os.environ["NLDSC_ORIENT"] = old
+    for o in ("1", "0"):
+        for mode in ("f4", "i8", "f32"):
+            with Engine(0, options={"orient": int(o)}) as e:  # swapped rare SNPs may lack hom-A1 calls: exact residuals
+                e.load_bed_bytes(b"\x6c\x1b\x01" + swapped.tobytes(), M, N)
+                out[o, mode] = e.run(*args, flags=MODES[mode] | _lib_flag("FLAG_EXACT_RARE"))
     exact = dict(l2=(1e-9, 1e-12), l2d=(1e-9, 1e-12), residuals_std=(1e-12, 1e-10), maf=(0.0, 0.0))
     for mode in ("f4", "i8"):
         assert_ld_close(out["1", mode], exp, tol=exact, label=f"{name} oriented {mode}")
@@ -615,8 +595,8 @@ def test_routing_reads_this_runs_individual_slots(engine, strict, t2):
         with Engine(0) as e:
             e.load_bed_bytes(synth.bed_bytes(rows), M, N)
             return e.run(*args, flags=flags)
-    got = _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", t2, fresh))
-    ref = _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", "0", fresh))
+    got = _opt_run("ksplit", 0, lambda: _opt_run("t2", t2, fresh))
+    ref = _opt_run("ksplit", 0, lambda: _opt_run("t2", 0, fresh))
     for k in got:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
     exp = O.run_f64(rows, N, *args, strict=strict)
@@ -630,10 +610,8 @@ def test_issued_products_counted_per_item(engine, t2, dom):
     """flop_issued (the bench's mfma_pipe_frac) counts what each kernel issues per work item: fp4 single-block items
     1 + cm + rm + rm cm + dom (2 + rm + cm) 32x32 block products over all K, less the transposed ones of diagonal
     blocks; items the routing sends to the 2 x 2 kernel (missing-free super-items) 1 + 2 dom; int8 4 + dom (2 + 2
-    !diag); fp32 1 + dom (2 - diag); with the quad kernel ($NLDSC_T2=3) every wave of a routed 4 x 4 super-item that
-    needs one of its four block pairs issues all four (4 (1 + 2 dom)); additive-only runs route every super-item
-    there with $NLDSC_QUAD_ADD=1 (the study mode, set here), 4 x 4 products per such wave where the super-item holds
-    missing calls.  Groups of four blocks alternate between
+    !diag); fp32 1 + dom (2 - diag); with the quad kernel (option t2 = 3) every wave of a routed 4 x 4 super-item that
+    needs one of its four block pairs issues all four (4 (1 + 2 dom)).  Groups of four blocks alternate between
     missing-free, one missing call and 2 % missing."""
     from nldsc_amd import _lib, synth
     from nldsc_amd.engine import Engine
@@ -660,16 +638,13 @@ def test_issued_products_counted_per_item(engine, t2, dom):
     if t2 == "3":  # 4 x 4 super-items whose eight blocks are missing-free run in the quad kernel
         free = ~np.any([mb(4 * (I >> 2) + k) | mb(4 * (J >> 2) + k) for k in range(4)], axis=0).astype(bool)
         assert free.any() and not free.all()
-        # additive-only: every super-item, 4 products per pair where its blocks hold missing calls
-        routed = free if dom else np.ones_like(free)
-        free4 = {(a >> 2, b >> 2): bool(f) for a, b, f in zip(I.tolist(), J.tolist(), free.tolist())}
+        routed = free
         needed = set(zip(I.tolist(), J.tolist()))
         quad = 0
         for I4, J4 in sorted(set(zip((I[routed] >> 2).tolist(), (J[routed] >> 2).tolist()))):
             for w in range(4):
                 pairs = [(4 * I4 + 2 * (w >> 1) + a, 4 * J4 + 2 * (w & 1) + b) for a in (0, 1) for b in (0, 1)]
-                per = 3 if dom else 1 if free4[(I4, J4)] else 4
-                quad += 4 * per if any(p in needed for p in pairs) else 0
+                quad += 4 * (3 if dom else 1) if any(p in needed for p in pairs) else 0
         f4 = np.append(np.where(routed, 0, f4), quad)
     i8 = 4 + (2 + 2 * nd if dom else 0 * nd)
     f32 = 1 + (1 + nd if dom else 0 * nd)
@@ -685,7 +660,7 @@ def test_issued_products_counted_per_item(engine, t2, dom):
                 e.run(1.0, 0.01, 1e-5, 1.0 / M, pos, flags=flags | MODES[mode])
                 out[mode] = e.timings()["flop_issued"] / (2.0 * 32 * 32 * 4 * row_bytes)
         return out
-    got = _env_run("NLDSC_QUAD_ADD", "1", lambda: _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", t2, run)))
+    got = _opt_run("ksplit", 0, lambda: _opt_run("t2", t2, run))
     assert got == {k: float(v) for k, v in expect.items()}, (got, expect)
 
 
@@ -761,8 +736,8 @@ def test_rare_variants_reference_residual(engine, mode, n_org, strict):
 def test_ksplit_equals_single_pass(engine, N, M, dom):
     """Launches too small to fill the GPU (a rank's shard) split every item's K loop into P pieces whose exact
     integer Gram tiles are summed by an epilogue kernel: every output is bitwise the single-pass one
-    ($NLDSC_KSPLIT=0), and both equal the fp64 truth.  Additive-only bands pair column blocks by default
-    ($NLDSC_F4_NC2), which takes no K-split: those runs here use single-block items ($NLDSC_F4_NC2=0)."""
+    (option ksplit 0), and both equal the fp64 truth.  Additive-only bands pair column blocks by default
+    (option f4_nc2), which takes no K-split: those runs here use single-block items (option f4_nc2 0)."""
     from nldsc_amd import synth
     from nldsc_amd.engine import Engine
     spec = synth.SynthSpec(n_org=N, n_snp=M, length_cm=6.0, seed=N + M, missing=0.02)
@@ -779,8 +754,8 @@ def test_ksplit_equals_single_pass(engine, N, M, dom):
             return r
 
     def both():
-        return fresh(True), _env_run("NLDSC_KSPLIT", "0", lambda: fresh(False))
-    got, ref = both() if dom else _env_run("NLDSC_F4_NC2", "0", both)
+        return fresh(True), _opt_run("ksplit", 0, lambda: fresh(False))
+    got, ref = both() if dom else _opt_run("f4_nc2", 0, both)
     for k in got:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
     exp = O.run_f64(rows, N, *args)
@@ -790,21 +765,37 @@ def test_ksplit_equals_single_pass(engine, N, M, dom):
                                        maf=(0.0, 0.0)), label=f"ksplit N={N}")
 
 
-def _env_run(var, value, fn):
-    old = os.environ.get(var)
-    os.environ[var] = value
+def missing_free_blocks(rows, n_org):
+    """32-SNP blocks without a missing call (code 01) among the individual slots the reference reads — every pair
+    of the bytes before the last, the last byte's high n_org % 4 pairs (stream.h:55-66) — as the engine counts them
+    at load (row_missing_kernel, free_blocks) to gate the super-item kernels."""
+    rows = np.asarray(rows, np.uint8)
+    M, nb = rows.shape
+    miss = np.stack([((rows >> (2 * k)) & 3) == 1 for k in range(4)], axis=-1)  # [M, nb, pair k = bits 2k+1:2k]
+    r = n_org % 4
+    keep = [k >= 4 - r for k in range(4)] if r else [True] * 4
+    row_miss = miss[:, :nb - 1, :].any(axis=(1, 2)) | miss[:, nb - 1, keep].any(axis=1)
+    return int(sum(not row_miss[32 * b:32 * b + 32].any() for b in range((M + 31) // 32)))
+
+
+def _opt_run(name, value, fn):
+    """fn() with engine option `name` = value on every engine it creates (Engine.default_options; C ABI
+    nldsc_engine_set_option)."""
+    from nldsc_amd.engine import Engine
+    had, old = name in Engine.default_options, Engine.default_options.get(name)
+    Engine.default_options[name] = int(value)
     try:
         return fn()
     finally:
-        if old is None:
-            os.environ.pop(var)
+        if had:
+            Engine.default_options[name] = old
         else:
-            os.environ[var] = old
+            Engine.default_options.pop(name, None)
 
 
 @pytest.mark.parametrize("mode", ["f32", "i8", "f4"])
-def test_band_mode_env_selects_the_default_path(mode):
-    """$NLDSC_BAND_MODE (read when an engine is created) picks the path a run without a path flag takes: the same
+def test_band_mode_option_selects_the_default_path(mode):
+    """Engine option band_mode (nldsc_engine_set_option) picks the path a run without a path flag takes: the same
     path and the same results as that path's flag (include/nldsc_ld.h, FLAG_EXACT_F4 / EXACT_I8 / FP32)."""
     from nldsc_amd import synth
     from nldsc_amd.engine import Engine
@@ -817,7 +808,7 @@ def test_band_mode_env_selects_the_default_path(mode):
         with Engine(0) as e:
             e.load_bed_bytes(synth.bed_bytes(rows), M, N)
             return e.run(*args, flags=flags), e.timings()["path"]
-    got, path = _env_run("NLDSC_BAND_MODE", mode, lambda: run(0))
+    got, path = _opt_run("band_mode", {"f32": 0, "i8": 1, "f4": 2}[mode], lambda: run(0))
     ref, ref_path = run(MODES[mode])
     assert path == ref_path == mode
     for k in got:
@@ -854,9 +845,10 @@ T2_CASES = {
 @pytest.mark.parametrize("t2", ["2", "1", "3"])
 @pytest.mark.parametrize("case", sorted(T2_CASES))
 def test_2x2_workgroups_bitwise_single_block(engine, case, t2):
-    """The 2 x 2 block-pair workgroups (LDS-shared strips) — for every super-item ($NLDSC_T2=2) or, the default,
-    for the missing-free ones with the rest routed to the single-block kernel ($NLDSC_T2=1) — give bitwise the
-    single-block kernel's results ($NLDSC_T2=0): each wave forms its block pair's partial sums exactly as the
+    """The 2 x 2 block-pair workgroups (LDS-shared strips) — for every super-item (option t2 = 2) or for the
+    missing-free ones with the rest routed to the single-block kernel (t2 = 1), and the 4 x 4 quad workgroups for the
+    missing-free 4 x 4 super-items (t2 = 3, the default) — give bitwise the single-block kernel's results (t2 = 0):
+    each wave forms its block pair's partial sums exactly as the
     single-block kernel does; both match the fp64 truth."""
     from conftest import rare_variant_set
     from nldsc_amd import synth
@@ -881,20 +873,21 @@ def test_2x2_workgroups_bitwise_single_block(engine, case, t2):
     flags = MODES["f4"] | (0 if dom else _lib_flag("FLAG_ADDITIVE_ONLY")) | (0 if rare else _lib_flag("FLAG_EXACT_RARE"))
     args = (wind, 1e-5, 1e-5, 1.0 / M, pos)
 
-    def fresh(kernel):  # engines read $NLDSC_* when created; these launches are small enough for the K-split
+    def fresh(kernel):  # (engine options apply to the engines made here); small enough launches for the K-split
         with Engine(0) as e:
             e.load_bed_bytes(synth.bed_bytes(rows), M, N)
             r = e.run(*args, flags=flags, own=own)
-            # (with routing, data without a missing-free block skips the super-item kernels: the single-block run)
+            # with routing (t2 1, 3) a run takes the super-item kernels only when one of its 32-SNP blocks is
+            # missing-free (the engine's free_blocks gate), else it is the single-block run (the gate
+            # checked against the data, not inferred from the case name)
             got_kernel = e.timings()["band_kernel"]
-            assert got_kernel == kernel or (t2 in ("1", "3") and got_kernel == "f4" and "missing_free" not in case
-                                            and "mixed" not in case), (got_kernel, kernel)
+            want = kernel if t2 == "2" or free > 0 else "f4"
+            assert got_kernel == want, (got_kernel, want, free)
             return r
-    # (additive-only with T2=3: the study mode that sends every super-item to the quad kernel, $NLDSC_QUAD_ADD=1)
-    got = _env_run("NLDSC_QUAD_ADD", "1" if not dom and t2 == "3" else "0", lambda: _env_run(
-        "NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", t2, lambda: fresh(
-            {"2": "f4_2x2", "1": "f4_routed", "3": "f4_quad"}[t2]))))
-    ref = _env_run("NLDSC_KSPLIT", "0", lambda: _env_run("NLDSC_T2", "0", lambda: fresh("f4")))
+    free = missing_free_blocks(rows, N)
+    got = _opt_run("ksplit", 0, lambda: _opt_run("t2", t2, lambda: fresh(
+        {"2": "f4_2x2", "1": "f4_routed", "3": "f4_quad"}[t2])))
+    ref = _opt_run("ksplit", 0, lambda: _opt_run("t2", 0, lambda: fresh("f4")))
     for k in got:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{case} {k}")
     if rare:
@@ -912,7 +905,7 @@ def test_2x2_workgroups_bitwise_single_block(engine, case, t2):
 
 
 NC2_CASES = {
-    # additive-only: (T2_CASES key, $NLDSC_T2); pairs with one column block routed to a super-item kernel, diagonal
+    # additive-only: (T2_CASES key, option t2); pairs with one column block routed to a super-item kernel, diagonal
     # pairs, odd last items of a row, owned ranges, the KC launch of replayed rare variants
     "additive_single": ("additive_only", "0"),
     "additive_routed": ("additive_only", "1"),
@@ -927,7 +920,7 @@ NC2_CASES = {
 
 @pytest.mark.parametrize("case", sorted(NC2_CASES))
 def test_f4_column_block_pairs_bitwise_single_blocks(engine, case):
-    """Additive-only fp4 items of two column blocks ($NLDSC_F4_NC2=1: 32 x 64 tiles, the row strip decoded once for
+    """Additive-only fp4 items of two column blocks (option f4_nc2 1: 32 x 64 tiles, the row strip decoded once for
     both; a block the super-item routing takes is dropped from its item) give bitwise the single-block items' results
     and the same issued-product count."""
     from conftest import rare_variant_set
@@ -958,9 +951,8 @@ def test_f4_column_block_pairs_bitwise_single_blocks(engine, case):
             e.load_bed_bytes(synth.bed_bytes(rows), M, N)
             r = e.run(*args, flags=flags, own=own)
             return r, e.timings()
-    # ($NLDSC_QUAD_ADD=0: the quad kernel keeps only the missing-free super-items, so the pairs run here)
-    run = lambda nc2: _env_run("NLDSC_QUAD_ADD", "0", lambda: _env_run("NLDSC_KSPLIT", "0", lambda: _env_run(  # noqa
-        "NLDSC_T2", t2, lambda: _env_run("NLDSC_F4_NC2", nc2, fresh))))
+    # (the quad kernel keeps only the missing-free super-items, so the pairs run here)
+    run = lambda nc2: _opt_run("ksplit", 0, lambda: _opt_run("t2", t2, lambda: _opt_run("f4_nc2", nc2, fresh)))  # noqa
     (got, tg), (ref, tr) = run("1"), run("0")
     assert tg["band_items"] < tr["band_items"], (tg["band_items"], tr["band_items"])  # the plan paired them
     assert tg["flop_issued"] == tr["flop_issued"], (tg["flop_issued"], tr["flop_issued"])
@@ -981,12 +973,12 @@ ROUND_CASES = {
 def test_band_round_launches_bitwise_one_launch(engine, case):
     """The single-block fp4 band in launches of one round of the wave slots each (the default for long rows,
     N >= 2^17, when the band has at least one round of items), with the partial last round K-split when the cost
-    model prefers it, gives bitwise the results of one launch of all items ($NLDSC_BAND_ROUNDS=0): the per-SNP sums
+    model prefers it, gives bitwise the results of one launch of all items (option band_rounds 0): the per-SNP sums
     are order-independent fixed point, the K-split partial Gram tiles are exact integers, and every item runs once.
     12 000 SNPs at 800 per cM, 1 % missing; a few SNPs against the exact truth.  The additive-only case runs
-    single-block items ($NLDSC_QUAD_ADD=0 and $NLDSC_F4_NC2=0: by default its super-items all go to the quad kernel)."""
+    single-block items (f4_nc2 0)."""
     if not ROUND_CASES[case][3]:
-        return _env_run("NLDSC_QUAD_ADD", "0", lambda: _env_run("NLDSC_F4_NC2", "0", lambda: _round_launch_case(case)))
+        return _opt_run("f4_nc2", 0, lambda: _round_launch_case(case))
     return _round_launch_case(case)
 
 
@@ -1009,7 +1001,7 @@ def _round_launch_case(case):
                 assert t["band_tail_ksplit"] > 1 or not tail, t
             return r
     got = fresh(True)
-    ref = _env_run("NLDSC_BAND_ROUNDS", "0", lambda: fresh(False))
+    ref = _opt_run("band_rounds", 0, lambda: fresh(False))
     for k in got:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
     assert (got["l2_ws"] > 100).all() and np.isfinite(got["l2"]).all()
@@ -1030,8 +1022,8 @@ def test_round_launches_with_replayed_rare_variants_in_the_tail(engine):
     FLAG_EXACT_RARE), the band in round launches, and the partial last round K-split — where the KC epilogue of
     the tail reads the partial Gram tiles the main launch wrote.  Rare SNPs (<= 16 calls in a genotype class) sit in
     the last row blocks (whose items end the tile-ordered plan: the K-split tail) and mid-chromosome.  Bitwise equal
-    to one launch ($NLDSC_BAND_ROUNDS=0) and to the replay run in line on the main stream
-    ($NLDSC_REPLAY_OVERLAP=0); the replayed SNPs' residual std equals the oracle's bit for bit and their scores
+    to one launch (option band_rounds 0) and to the KC launch of the deferred rare-variant items (defer_rep 0); the
+    replayed SNPs' residual std equals the oracle's bit for bit and their scores
     pass the bar against it."""
     import torch
     from nldsc_amd import synth
@@ -1064,8 +1056,8 @@ def test_round_launches_with_replayed_rare_variants_in_the_tail(engine):
                 assert t["band_tail_ksplit"] > 1, t
             return r
     got = fresh(True)
-    for var, value, rounds in (("NLDSC_BAND_ROUNDS", "0", False), ("NLDSC_REPLAY_OVERLAP", "0", True)):
-        ref = _env_run(var, value, lambda: fresh(rounds))
+    for var, value, rounds in (("band_rounds", 0, False), ("defer_rep", 0, True)):
+        ref = _opt_run(var, value, lambda: fresh(rounds))
         for k in got:
             np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{var}={value} {k}")
     bed = img.tobytes()
@@ -1080,8 +1072,8 @@ def test_round_launches_with_replayed_rare_variants_in_the_tail(engine):
 
 def test_quad_round_launches_bitwise_one_launch(engine):
     """Missing-free bands of many 4 x 4 super-items (a C5-shaped slice: 1000 kb windows, 288 bp per SNP) run the quad
-    kernel in launches of one workgroup per CU ($NLDSC_Q_ROUNDS, from 16 such rounds): bitwise the one-launch results
-    ($NLDSC_Q_ROUNDS=0) — the per-SNP sums are order-independent fixed point."""
+    kernel in launches of one workgroup per CU (option q_rounds, from 16 such rounds): bitwise the one-launch results
+    (option q_rounds 0) — the per-SNP sums are order-independent fixed point."""
     from nldsc_amd import synth
     from nldsc_amd.engine import Engine
     N, M = 2053, 150_000
@@ -1095,7 +1087,7 @@ def test_quad_round_launches_bitwise_one_launch(engine):
             assert e.timings()["band_kernel"] == "f4_quad"
             return r
     got = fresh()
-    ref = _env_run("NLDSC_Q_ROUNDS", "0", fresh)
+    ref = _opt_run("q_rounds", 0, fresh)
     for k in got:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
     assert (got["l2_ws"] > 3000).all()  # (a half window at the chromosome ends)
@@ -1104,10 +1096,10 @@ def test_quad_round_launches_bitwise_one_launch(engine):
 @pytest.mark.parametrize("dom", [False, True])
 def test_deferred_rare_variant_items_bitwise_kc_launch(engine, dom):
     """Items holding a replayed rare variant run their K loops in the main single-block launch and their epilogues
-    after the replay from stored Gram tiles ($NLDSC_DEFER_REP, the default): bitwise the separate KC launch
-    ($NLDSC_DEFER_REP=0).  Additive-only: a rare variant only in the second column block of a column-block pair item
+    after the replay from stored Gram tiles (option defer_rep, the default): bitwise the separate KC launch
+    (option defer_rep 0).  Additive-only: a rare variant only in the second column block of a column-block pair item
     (block 1 of item (0, 0, 2)) — that pair must take the ka terms too — and equal to single-block items
-    ($NLDSC_F4_NC2=0)."""
+    (option f4_nc2 0)."""
     from nldsc_amd import synth
     from nldsc_amd.engine import Engine
     N, M = 50_000, 320
@@ -1129,11 +1121,11 @@ def test_deferred_rare_variant_items_bitwise_kc_launch(engine, dom):
         with Engine(0) as e:
             e.load_bed_bytes(synth.bed_bytes(rows), M, N)
             return e.run(*args, flags=flags)
-    ksplit_off = lambda fn: _env_run("NLDSC_KSPLIT", "0", fn)  # noqa: E731  (small launch: no whole-band K-split)
+    ksplit_off = lambda fn: _opt_run("ksplit", 0, fn)  # noqa: E731  (small launch: no whole-band K-split)
     got = ksplit_off(fresh)
-    refs = {"kc_launch": ksplit_off(lambda: _env_run("NLDSC_DEFER_REP", "0", fresh))}
+    refs = {"kc_launch": ksplit_off(lambda: _opt_run("defer_rep", 0, fresh))}
     if not dom:
-        refs["single_blocks"] = ksplit_off(lambda: _env_run("NLDSC_F4_NC2", "0", fresh))
+        refs["single_blocks"] = ksplit_off(lambda: _opt_run("f4_nc2", 0, fresh))
     for name, ref in refs.items():
         for k in got:
             np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{name} {k}")
@@ -1147,7 +1139,7 @@ def test_deferred_rare_items_capped_on_wide_bands_with_missing_calls(engine):
     """A wide band (1000 kb windows at 288 bp per SNP: ~3 500 neighbours) of data with missing calls keeps nearly every
     item in the single-block kernel; the deferred rare-variant Gram tiles would need 32 KiB per item (~140
     GB at the C5 slice with 1 % missing).  Past 2^16 items the engine runs the rare-variant items in the KC launch
-    instead: bitwise the KC launch ($NLDSC_DEFER_REP=0), and the exact integer outputs of a few SNPs equal the oracle's."""
+    instead: bitwise the KC launch (option defer_rep 0), and the exact integer outputs of a few SNPs equal the oracle's."""
     from nldsc_amd import synth
     from nldsc_amd.engine import Engine
     N, M = 2053, 90_000
@@ -1162,7 +1154,7 @@ def test_deferred_rare_items_capped_on_wide_bands_with_missing_calls(engine):
             assert t["band_items"] > (1 << 16) and t["band_kernel"] in ("f4", "f4_quad"), t
             return r
     got = fresh()
-    ref = _env_run("NLDSC_DEFER_REP", "0", fresh)
+    ref = _opt_run("defer_rep", 0, fresh)
     for k in got:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
     t = np.array([0, 31, 32, 45_000, M - 1], np.int32)

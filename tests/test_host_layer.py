@@ -202,11 +202,13 @@ def test_progress_is_throttled_and_quiet():
 
 
 @pytest.mark.parametrize("text", ["a\tb\t0\t0\t1\t-9\n" * 5, "a\tb\t0\t0\t1\t-9\n" * 4 + "a\tb\t0\t0\t1\t-9",
-                                  "a\tb\t0\t0\t1\t-9\n\n\na\tb\t0\t0\t1\t-9\n", "a\tb\t0\t0\t1\t-9\r\n" * 3])
+                                  "a\tb\t0\t0\t1\t-9\n\n\na\tb\t0\t0\t1\t-9\n", "a\tb\t0\t0\t1\t-9\r\n" * 3,
+                                  "a\tb\t0\t0\t1\t-9\r" * 4, "a\tb\t0\t0\t1\t-9\r\ra\tb\t0\t0\t1\t-9\n",
+                                  "", "\n\n", " \r\n", "a\n  \nb\n", "\t\n", "\x0b\n"])
 def test_fam_count_equals_pandas_rows(tmp_path, text):
     """FAMFile counts its individuals from the lines (a whole-genome run reads a 315 599-line .fam per chromosome):
-    the same number as the rows the reference's pandas parse gives (blank lines skipped, CRLF, no final newline), and
-    the table itself is still available."""
+    the same number as the rows the reference's pandas parse gives (blank and space-only lines skipped, CRLF, lone CR,
+    no final newline, an empty file: 0 rows), and the table itself is still available."""
     import pandas as pd
     from nldsc_amd.ldscore.common import FAMFile
     p = tmp_path / "x.fam"
@@ -214,3 +216,4 @@ def test_fam_count_equals_pandas_rows(tmp_path, text):
     f = FAMFile(str(p))
     rows = pd.read_csv(p, sep="\t", names=FAMFile.COLUMNS)
     assert f.n_org == len(rows) and len(f.data) == len(rows) and repr(f) == f"FAMFile(n_org={len(rows)})"
+

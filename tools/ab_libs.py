@@ -27,7 +27,8 @@ WORKLOADS = {  # name: (N, M, length_cm, window, missing, additive_only)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--libs", nargs="+", required=True,
-                    help="name=path.so[,ENV=VALUE...] (engine knobs are read when an engine is created)")
+                    help="name=path.so[,option=value...] (engine options, nldsc_engine_set_option; builds before round 5 "
+                         "read NLDSC_<OPTION> environment variables when an engine is created, which is set for those)")
     ap.add_argument("--workload", nargs="+", default=["c3"], choices=sorted(WORKLOADS))
     ap.add_argument("--runs", type=int, default=8)
     ap.add_argument("--c5-snp", type=int, default=300_000)
@@ -57,11 +58,16 @@ def main():
         flags = _lib.FLAG_ADDITIVE_ONLY if add else 0
         engines = {}
         for name, spec in libs.items():
-            path, *envs = spec.split(",")
-            old = {k: os.environ.get(k) for k, _ in (x.split("=", 1) for x in envs)}
-            os.environ.update(dict(x.split("=", 1) for x in envs))
+            path, *kv = spec.split(",")
+            opts = dict(x.split("=", 1) for x in kv)
+            env = {"NLDSC_" + k.upper(): v for k, v in opts.items()}
+            old = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
             try:
                 e = Engine(0, lib_path=path)
+                if hasattr(e._L, "nldsc_engine_set_option"):
+                    for k, v in opts.items():
+                        e.set_option(k, int(v))
             finally:
                 for k, v in old.items():
                     if v is None:

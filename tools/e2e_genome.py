@@ -6,7 +6,9 @@
                 N = 315 599 (~47 GB of .bed), cM positions over the chromosome's length
   --chroms K    K equal chromosomes of --n-snp SNPs over 70 cM (the round-1 I/O study)
 
-Files are written once to --dir (kept when they exist with the right size).  Then, with every .bed's pages dropped
+Files are written to --dir (a .bed of the right size already there is reused).  Afterwards, unless --keep, the tool
+removes exactly the files it wrote (chrN.bed/.bim/.fam, its out/ TSVs) and --dir only if it created it and it is then
+empty — never anything else found there.  Then, with every .bed's pages dropped
 from the page cache (fsync + POSIX_FADV_DONTNEED) before each cold run:
   cli      - `python -m nldsc_amd ld --bfile <dir>/chr@ --ld-wind-cm 1 --out <out>/o@.L2 --extra --quiet` as a child
              process: the wall clock a user sees (interpreter start, imports, every file, every TSV)
@@ -45,22 +47,27 @@ def drop_pages(paths):
             os.close(fd)
 
 
-def write_set(stem, chrom, M, N, seed, length_cm, missing):
-    """stem.bed/.bim/.fam; the .bed generated on the GPU (synth.device_bed) and streamed to disk."""
+def write_set(stem, chrom, M, N, seed, length_cm, missing, created):
+    """stem.bed/.bim/.fam; the .bed generated on the GPU (synth.device_bed) and streamed to disk.  Every path this
+    call writes is appended to `created` (the cleanup removes those and nothing else)."""
     from nldsc_amd import synth
     nb = (N + 3) // 4
     want = 3 + M * nb
     buf, pos = synth.device_bed(M, N, seed=seed, length_cm=length_cm, missing=missing)
     if not (os.path.exists(stem + ".bed") and os.path.getsize(stem + ".bed") == want):
+        created.append(stem + ".bed")
         with open(stem + ".bed", "wb") as fh:
             step = 1 << 30
             for o in range(0, want, step):  # 1 GiB pieces: bounded host memory
                 fh.write(buf[o:o + step].cpu().numpy().tobytes())
     del buf
     bp = np.round(pos * 1e6).astype(np.int64)
+    if not os.path.exists(stem + ".bim"):
+        created.append(stem + ".bim")
     with open(stem + ".bim", "w") as fh:
         fh.writelines(f"{chrom}\trs{chrom}_{j}\t{pos[j]:.6f}\t{bp[j]}\tA\tG\n" for j in range(M))
     if not os.path.exists(stem + ".fam"):
+        created.append(stem + ".fam")
         with open(stem + ".fam", "w") as fh:
             fh.writelines(f"f{i}\ti{i}\t0\t0\t0\t-9\n" for i in range(N))
     return want
@@ -89,7 +96,9 @@ def main():
     import torch
     from nldsc_amd.engine import Engine
     from nldsc_amd.ldscore.genome import estimate_lds_genome
+    made_dir = not os.path.isdir(a.dir)
     os.makedirs(a.dir, exist_ok=True)
+    created = []  # files this run wrote (removed at the end unless --keep)
     N = a.n_org
     nb = (N + 3) // 4
     if a.autosomes:
@@ -114,13 +123,16 @@ def main():
         raise SystemExit(f"not enough disk in {a.dir}: need {need / 1e9:.1f} GB, free {du.free / 1e9:.1f} GB")
     t = time.perf_counter()
     for c, M, length in chroms:
-        write_set(os.path.join(a.dir, f"chr{c}"), c, M, N, 100 + c, length, a.missing)
+        write_set(os.path.join(a.dir, f"chr{c}"), c, M, N, 100 + c, length, a.missing, created)
         print(f"[write] chr{c} M={M} ({time.perf_counter() - t:.1f} s)", file=sys.stderr, flush=True)
     torch.cuda.empty_cache()
     doc["write_s"] = round(time.perf_counter() - t, 2)
     beds = [os.path.join(a.dir, f"chr{c}.bed") for c, _, _ in chroms]
     outdir = os.path.join(a.dir, "out")
+    made_out = not os.path.isdir(outdir)
     os.makedirs(outdir, exist_ok=True)
+    outs = [os.path.join(outdir, f"{s}{c}.L2") for s in ("o", "s") for c, _, _ in chroms]
+    outs += [o + ".M" for o in outs]
     cli = [sys.executable, "-m", "nldsc_amd", "ld", "--bfile", os.path.join(a.dir, "chr@"), "--ld-wind-cm", "1",
            "-maf", "0.0001", "--out", os.path.join(outdir, "o@.L2"), "--extra", "--quiet"]
 
@@ -191,7 +203,23 @@ def main():
     if a.out:
         json.dump(doc, open(a.out, "w"), indent=1)
     if not a.keep:
-        shutil.rmtree(a.dir, ignore_errors=True)
+        cleanup(created, outs, outdir if made_out else None, a.dir if made_dir else None)
+
+
+def cleanup(created, outputs, outdir, topdir):
+    """Remove the files this run wrote and the directories it created, if they are then empty (never
+    rmtree a directory the user passed, which may hold other data)."""
+    for p in list(created) + list(outputs):
+        try:
+            os.unlink(p)
+        except FileNotFoundError:
+            pass
+    for d in (outdir, topdir):
+        if d is not None:
+            try:
+                os.rmdir(d)  # only when empty
+            except OSError:
+                pass
 
 
 if __name__ == "__main__":
