@@ -322,7 +322,6 @@ struct nldsc_engine {
     bool f4_nc2 = true;
     // single-block fp4 band in launches of one round of wave slots (option "band_rounds" 0: one launch)
     bool band_rounds = true;
-    bool band_persist = false;  // (study) the round launches as one persistent launch walking the rounds
     DevBuf<uint8_t> blk_miss;
     // quad super-items in launches of one workgroup per CU when there are at least 16 such rounds (option "q_rounds" 0:
     // one launch): the workgroups on an XCD then stream their shared strips at nearby K offsets; C5 slice band
@@ -533,7 +532,6 @@ int nldsc_engine_set_option(nldsc_engine* e, const char* name, int64_t value, ch
         {"band_rounds", 0, 1, [&](int64_t v) { e->band_rounds = v != 0; }},
         {"f4_nc2", 0, 1, [&](int64_t v) { e->f4_nc2 = v != 0; }},
         {"q_rounds", 0, 1, [&](int64_t v) { e->q_rounds = v != 0; }},
-        {"band_persist", 0, 1, [&](int64_t v) { e->band_persist = v != 0; }},
         {"defer_rep", 0, 1, [&](int64_t v) { e->defer_rep = v != 0; }},
         {"debug_timing", 0, 1, [&](int64_t v) { e->debug_timing = v != 0; }},
     };
@@ -1213,7 +1211,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                                                  e->ws_acc.p, true, blk_rep, which, st, single_miss, round_items,
                                                  route_shift,
                                                  dfr ? e->rep_gram.p : nullptr, dfr ? e->rep_items.p : nullptr,
-                                                 dfr ? e->rep_count.p : nullptr, e->band_persist);
+                                                 dfr ? e->rep_count.p : nullptr);
             if (r == hipSuccess && dfr && (which & 2))  // after the replay: the deferred items' epilogues
                 r = nldsc::launch_band_f4_deferred_epi(dom, n_full * (nc2 ? 2 : 1), e->cst.p, e->rep_items.p,
                                                        e->rep_count.p, e->rep_gram.p, e->pos.p, e->Lw.p, e->Rw.p,

@@ -112,8 +112,7 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
                           int which, hipStream_t st, const uint8_t* blk_miss = nullptr, int round_items = 0,
-                          int route_shift = 1, float* rep_gram = nullptr, int4* rep_items = nullptr, int* rep_count = nullptr,
-                          bool persist = false);
+                          int route_shift = 1, float* rep_gram = nullptr, int4* rep_items = nullptr, int* rep_count = nullptr);
 // rep_gram (unsegmented rows): the items holding a replayed rare variant run their K loops in the main launch and store
 // each block pair's exact Gram tiles (rep_gram slot = atomicAdd(rep_count), 8192 floats; rep_items[slot] = the block
 // pair); after the replay, launch_band_f4_deferred_epi runs their epilogues (max_items >= the slots used) in place of

@@ -1858,7 +1858,7 @@ __device__ __forceinline__ bool routed_item(const uint8_t* blk_miss, int route_s
 // NCX 2 (additive-only, unsegmented): items (I, J, 2) pair column blocks J and J + 1 in one wave (a 32 x 64 tile: the
 // row strip decoded once for both), as the plan emits them with pairing; a column block the super-item routing sends
 // elsewhere (blk_miss) is dropped from its item here.
-template <bool DOM, int WPS, int SEG, bool KC, int NCX = 1, bool PERSIST = false>
+template <bool DOM, int WPS, int SEG, bool KC, int NCX = 1>
 __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __restrict__ geno, int pitch_words, int n_it,
                                                         const SnpConst* __restrict__ cst, const int4* __restrict__ items,
                                                         const double* __restrict__ pos, const int* __restrict__ Lw,
@@ -1869,7 +1869,7 @@ __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __rest
                                                         const uint8_t* __restrict__ blk_rep,
                                                         const uint8_t* __restrict__ blk_miss, int route_shift,
                                                         float* __restrict__ rep_gram, int4* __restrict__ rep_items,
-                                                        int* __restrict__ rep_count, int persist_items) {
+                                                        int* __restrict__ rep_count) {
     __shared__ BandI8Lds sh;
     __shared__ float tr[32 * 33];
     auto item = [&](const int4 it) __attribute__((always_inline)) {  // (not a call: the body's registers stay live)
@@ -1926,20 +1926,7 @@ __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __rest
     if (it.y == it.x) NLDSC_BODY(1, true, it); else NLDSC_BODY(1, false, it);
 #undef NLDSC_BODY
     };
-    if constexpr (!PERSIST) {
-        item(items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x]);
-    } else {
-        // persistent rounds (study: option band_persist): one workgroup per wave slot walks the rounds of `items`, round
-        // k = items [k S, k S + S) with S = gridDim.x in the same per-XCD order as a round launch, without the launch
-        // boundary between rounds (a wave starts its next item as soon as it finishes one)
-        const int S = gridDim.x;
-        for (int base = 0; base < persist_items; base += S) {
-            const int n = min(S, persist_items - base);
-            if ((int)blockIdx.x >= n) break;
-            __syncthreads();  // (the slot tables of the previous item were read)
-            item(items[base + (xcd ? xcd_slot(blockIdx.x, n) : blockIdx.x)]);
-        }
-    }
+    item(items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x]);
 }
 
 // ---- 2 x 2 block-pair workgroups: the operand feed ----
@@ -2986,7 +2973,7 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
                           const uint8_t* sflags, int n_snp, double ld_wind, double n_org, double rsq_thr, int own_lo,
                           int own_hi, double* l2_acc, double* l2d_acc, int* ws_acc, bool xcd, const uint8_t* blk_rep,
                           int which, hipStream_t st, const uint8_t* blk_miss, int round_items, int route_shift,
-                          float* rep_gram, int4* rep_items, int* rep_count, bool persist) {
+                          float* rep_gram, int4* rep_items, int* rep_count) {
     if (n_items <= 0) return hipSuccess;
     // single block-pair items, or (additive-only, unsegmented rows) column-block pairs
     if (max_nc != 1 && !(max_nc == 2 && !dom && n_it <= F4_SEG_CHUNKS)) return hipErrorInvalidValue;
@@ -2994,26 +2981,13 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
     // round_items > 0: the items go in launches of that many (one round of the wave slots each), see ld_engine.cpp;
     // not the KC launch (items holding a replayed rare variant: few, the others return at once)
     int chunk = round_items > 0 ? round_items : n_items;
-    // persist (round launches only): one launch of `chunk` workgroups walking every round (band_f4_kernel
-    // persist_items)
-    // (add+dom, unsegmented rows, single block pairs: the variant instantiated with PERSIST)
-    int persist_n = persist && dom && n_it <= F4_SEG_CHUNKS && max_nc == 1 && round_items > 0 && n_items > chunk
-                        ? n_items : 0;
-#define NLDSC_BAND_LAUNCH(DOM_, WPS_, SEG_, KC_, NCX_, P_)                                                          \
-    hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_, KC_, NCX_, P_>), dim3(std::min(chunk, n_items - o)), dim3(64), \
-                       0, st, geno, pitch_words,                                                                      \
+#define NLDSC_BAND_NC(DOM_, WPS_, SEG_, KC_, NCX_)                                                                  \
+    for (int o = 0; o < n_items; o += chunk)                                                                      \
+    hipLaunchKernelGGL((band_f4_kernel<DOM_, WPS_, SEG_, KC_, NCX_>), dim3(std::min(chunk, n_items - o)), dim3(64), 0, \
+                       st, geno, pitch_words,                                                                         \
                        n_it, cst, items + o, pos, Lw, Rw, sflags, n_snp, ld_wind, n_org, rsq_thr, own_lo, own_hi,       \
                        l2_acc, l2d_acc, ws_acc, xcd ? 1 : 0, blk_rep, blk_miss, route_shift, SEG_ ? nullptr : rep_gram, \
-                       rep_items, rep_count, persist_n)
-#define NLDSC_BAND_NC(DOM_, WPS_, SEG_, KC_, NCX_)                                                                  \
-    do {                                                                                                             \
-        for (int o = 0; o < n_items; o += (persist_n ? n_items : chunk)) {                                        \
-            if constexpr (DOM_ && SEG_ == 0 && !KC_ && NCX_ == 1) {                                                 \
-                if (persist_n) { NLDSC_BAND_LAUNCH(DOM_, WPS_, SEG_, KC_, NCX_, true); continue; }                   \
-            }                                                                                                        \
-            NLDSC_BAND_LAUNCH(DOM_, WPS_, SEG_, KC_, NCX_, false);                                                   \
-        }                                                                                                            \
-    } while (0)
+                       rep_items, rep_count)
 #define NLDSC_BAND(DOM_, WPS_, SEG_, KC_) NLDSC_BAND_NC(DOM_, WPS_, SEG_, KC_, 1)
 #define NLDSC_PICK(KC_)                                                                                              \
     if (n_it > F4_SEG_CHUNKS) { if (dom) NLDSC_BAND(true, 1, F4_SEG_CHUNKS, KC_); else NLDSC_BAND(false, 2, F4_SEG_CHUNKS, KC_); } \
@@ -3023,13 +2997,11 @@ hipError_t launch_band_f4(bool dom, int max_nc, int n_items, const uint32_t* gen
     // segmented kernel: the add+dom variant needs more than 256 registers (2 waves / SIMD would spill)
     if (which & 1) { NLDSC_PICK(false); }
     chunk = n_items;
-    persist_n = 0;
     // (with rep_gram the KC items ran their K loops in the main launch: launch_band_f4_deferred_epi after the replay)
     if (blk_rep && (which & 2) && (rep_gram == nullptr || n_it > F4_SEG_CHUNKS)) { NLDSC_PICK(true); }
 #undef NLDSC_PICK
 #undef NLDSC_BAND
 #undef NLDSC_BAND_NC
-#undef NLDSC_BAND_LAUNCH
     return hipGetLastError();
 }
 

@@ -81,6 +81,7 @@ def main():
         stages = ("count_ms", "stats_ms", "schedule_ms", "band_ms", "finalize_ms", "total_ms")
         res = {name: {"band": [], "total": [], "kernel": None, "stages": {k: [] for k in stages}} for name in libs}
         ref = None
+        dl2 = {name: 0.0 for name in libs}  # max |L2 - first build's L2| (and L2D), computed SNPs
         for r in range(a.runs + 1):
             for name, e in engines.items():
                 got = e.run(w, 1e-4, 1e-5, 1.0 / (M if own is None else 80_000), pos, flags=flags, own=own)
@@ -96,9 +97,16 @@ def main():
                 elif not a.no_check:  # every build must agree on the integer outputs
                     for k in ("l2_ws", "l2d_ws"):
                         assert np.array_equal(got[k], ref[k]), (wl, name, k)
+                if ref is not None and got is not ref:
+                    ok = ref["l2_ws"] > 0
+                    for k in ("l2", "l2d"):
+                        d = np.abs(np.asarray(got[k])[ok] - np.asarray(ref[k])[ok])
+                        d = d[np.isfinite(d)]
+                        if d.size:
+                            dl2[name] = max(dl2[name], float(d.max()))
         out[wl] = {name: {"band_ms_median": float(np.median(v["band"])), "band_ms_min": float(np.min(v["band"])),
                           "total_ms_median": float(np.median(v["total"])), "runs": len(v["band"]),
-                          "band_kernel": v["kernel"],
+                          "band_kernel": v["kernel"], "max_abs_dl2_vs_first": dl2[name],
                           "stages_ms_median": {k: round(float(np.median(x)), 4) for k, x in v["stages"].items()}}
                    for name, v in res.items()}
         print(json.dumps({wl: out[wl]}), file=sys.stderr, flush=True)
