@@ -272,6 +272,7 @@ struct nldsc_engine {
     DevBuf<uint8_t> flip;   // per SNP: resident row stores the swapped (00 <-> 11) coding
     DevBuf<uint8_t> row_miss;  // per SNP: bit 0 / 1 = a missing call among the reference's / PLINK's individual slots
     DevBuf<uint32_t> miss_flags;  // (the load kernels' per-row word of the same flags)
+    DevBuf<int> lcounts;          // per row: genotype counts of its stored bytes [0, nb - 1), load_parts parts
     bool orient = true;     // store rows minor-homozygote-as-00 at load (option "orient" 0: file coding)
     bool oriented = false;  // the resident image was oriented
     int32_t n_snp = 0, n_org = 0;
@@ -365,6 +366,7 @@ struct nldsc_engine {
     ~nldsc_engine() {
         (void)hipSetDevice(device);
         bed.release(); stage_dev.release(); lastb.release(); flip.release(); row_miss.release(); miss_flags.release();
+        lcounts.release();
         counts.release(); Lw.release(); Rw.release(); Aw.release(); ws_acc.release();
         res.release(); lut.release(); cst.release(); sflags.release(); pos.release();
         l2_acc.release(); l2d_acc.release(); items.release(); gram.release();
@@ -431,6 +433,8 @@ hipError_t alloc_image(nldsc_engine* e, int32_t n_snp, int32_t n_org) {
     if (he == hipSuccess) he = e->flip.ensure((size_t)n_snp);
     if (he == hipSuccess) he = e->row_miss.ensure((size_t)n_snp);
     if (he == hipSuccess) he = e->miss_flags.ensure((size_t)n_snp);
+    if (he == hipSuccess)
+        he = e->lcounts.ensure((size_t)nldsc::load_parts(n_snp, row_pitch(n_org)) * (size_t)n_snp * 3);
     return he;
 }
 
@@ -443,7 +447,7 @@ hipError_t load_slice(nldsc_engine* e, const uint8_t* src, int32_t row0, int32_t
     const uint32_t keep_compat = rem ? (0xFFu << (8 - 2 * rem)) & 0xFFu : 0xFFu;
     const uint32_t keep_strict = rem ? (1u << (2 * rem)) - 1u : 0xFFu;
     return nldsc::launch_load_slice(src, nb, row0, n_rows, n_snp, e->bed.p, row_pitch(n_org), e->oriented, e->flip.p,
-                                    e->lastb.p, keep_compat, keep_strict, e->miss_flags.p, st);
+                                    e->lastb.p, keep_compat, keep_strict, e->miss_flags.p, e->lcounts.p, st);
 }
 
 // after every slice is in: per-row missing flags, the missing-free block counts, and mark the image valid
@@ -870,8 +874,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // the band kernels read the resident rows (Mpad rows at row_bytes pitch) in place
     const uint32_t* geno = reinterpret_cast<const uint32_t*>(e->bed.p);
     HIPCHK(e->counts.ensure((size_t)M * 4));
-    const int count_parts = nldsc::count_parts(M, nb);
-    HIPCHK(e->cparts.ensure((size_t)count_parts * M * 3));
+    HIPCHK(e->cparts.ensure((size_t)M * 3));
     HIPCHK(e->rep_count.ensure(1));  // (zeroed by the statistics kernel)
     HIPCHK(e->lut.ensure((size_t)Mpad * 4));
     HIPCHK(e->cst.ensure((size_t)Mpad));
@@ -944,7 +947,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         if (t2_cand) {
             const size_t nblk2 = (size_t)(nblk + 1) / 2, n_t2 = (nblk2 + 15) / 16;
             HIPCHK(e->plan_rows2.ensure(nblk2));
-            HIPCHK(e->plan_counts2.ensure(n_t2 * n_t2));
+            HIPCHK(e->plan_counts2.ensure(std::max<size_t>(n_t2 * n_t2, (size_t)nldsc::plan_super_counts(M, route_shift))));
         }
     }
 
@@ -963,11 +966,12 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     }
     if (gpu_plan) HIPCHK(nldsc::launch_plan_edges(e->pos.p, M, p->ld_wind, e->Aw.p, e->Aw.p + M, e->plan_meta.p, st));
     HIPCHK(hipEventRecord(e->ev_pos, st));
-    // non-individual slots read as missing (0x55) for the int8 / fp32 kernels, as 00 (all fp4 planes zero) for fp4
+    // non-individual slots read as missing (0x55) for the int8 / fp32 kernels, as 00 (all fp4 planes zero) for fp4;
+    // the genotype counts: the load's (every byte before the last) plus this run's last byte
     const uint32_t pad = use_f4 ? 0x00u : 0x55u;
-    const int n_pad00 = use_f4 ? 4 * row_bytes - N : 0;
-    HIPCHK(hipEventRecord(e->ev[0], st));  // (count_ms: the count kernel alone; the host total covers the above)
-    HIPCHK(nldsc::launch_count_rows(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, pad, n_pad00, e->cparts.p, st));
+    HIPCHK(hipEventRecord(e->ev[0], st));  // (count_ms: the tail kernel alone; the host total covers the above)
+    HIPCHK(nldsc::launch_tail_counts(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, pad, e->lcounts.p,
+                                     nldsc::load_parts(M, row_bytes), e->cparts.p, st));
     HIPCHK(hipEventRecord(e->ev[1], st));
     if (gpu_plan) {
         HIPCHK(hipStreamWaitEvent(e->plan_stream, e->ev_pos, 0));
@@ -981,7 +985,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         HIPCHK(hipMemcpyAsync(e->h_meta.p, e->plan_meta.p, 8 * sizeof(int), hipMemcpyDeviceToHost, e->plan_stream));
         HIPCHK(hipEventRecord(e->ev_plan, e->plan_stream));
     }
-    HIPCHK(nldsc::launch_snp_stats(e->cparts.p, count_parts, e->counts.p, e->rep_count.p,
+    HIPCHK(nldsc::launch_snp_stats(e->cparts.p, 1, e->counts.p, e->rep_count.p,
                                    e->oriented ? e->flip.p : nullptr, e->pos.p, M, Mpad, N, p->maf, p->std_thr,
                                    e->lut.p, e->cst.p, e->sflags.p, e->maf.p, e->rstd.p, st, e->l2_acc.p, e->l2d_acc.p,
                                    e->ws_acc.p, e->blk_rep.p));

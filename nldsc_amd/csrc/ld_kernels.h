@@ -26,23 +26,24 @@ struct SnpConst {
 // rows [row0, row0 + n_rows) of a .bed image (row r of nb bytes at src + r * nb, any alignment) into the resident
 // layout (block-interleaved, ld_kernels.hip tile_off) — pitch padding 0x55, the last block's rows past n_snp all 0x55 —
 // each stored in the orientation flip[j] chosen from its head (orient: rows with more hom-A2 than hom-A1 calls there
-// stored 00 <-> 11 swapped; !orient: as in the file), its stored last byte saved to last[j], and its missing calls
+// stored 00 <-> 11 swapped; !orient: as in the file), its stored last byte saved to last[j], its missing calls
 // among the individual slots of the reference's (bit 0) / PLINK's (bit 1) sample order ORed into miss_flags[j]
-// (keep_*: the last byte's individual bit pairs per order).  After every slice: launch_load_flags -> row_miss.
+// (keep_*: the last byte's individual bit pairs per order), and the genotype counts of its stored bytes [0, nb - 1)
+// (hom A1, het, hom A2) per part p of load_parts(n_snp, row_bytes) to lcounts[(p n_snp + j) 3 + k].  After every
+// slice: launch_load_flags -> row_miss.
+int load_parts(int n_snp, int row_bytes);
 hipError_t launch_load_slice(const uint8_t* src, int nb, int row0, int n_rows, int n_snp, uint8_t* img, int row_bytes,
                              bool orient, uint8_t* flip, uint8_t* last, uint32_t keep_compat, uint32_t keep_strict,
-                             uint32_t* miss_flags, hipStream_t st);
+                             uint32_t* miss_flags, int* lcounts, hipStream_t st);
 hipError_t launch_load_flags(const uint32_t* miss_flags, int n_snp, uint8_t* row_miss, hipStream_t st);
-// per run: set each row's non-individual slots (last byte outside tail_keep, pitch padding) to `pad`
-// (0x55 missing, or 0x00 for the fp4 kernel) and count genotype codes; n_pad00 = 00-coded non-individual
-// slots per row (discounted from hom-A1).  Counts of part p (count_parts per 32-SNP block) of SNP j land in
-// parts[(p n_snp + j) 3 + k], k = hom A1, het, hom A2 (count_parts(n_snp, nb) * n_snp * 3 ints, no zeroing needed)
-int count_parts(int n_snp, int nb);
-hipError_t launch_count_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
-                             uint32_t pad, int n_pad00, int* parts, hipStream_t st);
-// parts / P: the count kernel's output, summed into counts[4 j + k] (n_snp * 4 ints; the rare-variant kernels read
-// them); zero: one int cleared on the way (nullptr: none).  flip: per-SNP stored-orientation flags (nullptr: none
-// flipped)
+// per run: set each row's non-individual slots (last byte outside tail_keep, pitch padding) to `pad` (0x55 missing,
+// or 0x00 for the fp4 kernel) and its genotype counts — the load's lcounts (P parts) plus the last byte's individual
+// pairs — to counts3[3 j + k] (one thread per row; no pass over the rows)
+hipError_t launch_tail_counts(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
+                              uint32_t pad, const int* lcounts, int P, int* counts3, hipStream_t st);
+// parts / P: genotype counts in P parts ([P][n_snp][3]: launch_tail_counts gives one), summed into counts[4 j + k]
+// (n_snp * 4 ints; the rare-variant kernels read them); zero: one int cleared on the way (nullptr: none).  flip:
+// per-SNP stored-orientation flags (nullptr: none flipped)
 hipError_t launch_snp_stats(const int* parts, int P, int* counts, int* zero, const uint8_t* flip, const double* pos,
                             int n_snp, int n_snp_pad, int n_org, double maf_thr, double std_thr, float2* lut,
                             SnpConst* cst, uint8_t* sflags, double* maf_out, double* rstd_out, hipStream_t st,
@@ -135,7 +136,10 @@ hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* ge
 // as meta; counts2 capacity ceil(nblk2/16)^2) and launch_plan_emit_super; the kernel reads `rows` (nblk) to skip the
 // block pairs the single-block plan does not hold
 constexpr int T2_STAGES = 4;  // LDS ring stages (2 chunks each) of band_f4_t2_kernel
-// shift 1: 2 x 2 super-items; shift 2: the quad kernel's 4 x 4 super-items
+// shift 1: 2 x 2 super-items (16 x 16 tiles); shift 2: the quad kernel's 4 x 4 super-items in 32-item groups of 4
+// super-rows x 8 offsets, padded with null items (I, J, 0, -1) to exactly 32 (one XCD's share of a round launch);
+// counts2 capacity: plan_super_counts(n, shift)
+int plan_super_counts(int n, int shift);
 hipError_t launch_plan_super(int n, const int2* rows, int2* rows2, int* counts2, int* meta2, int shift, hipStream_t st);
 hipError_t launch_plan_emit_super(int n, const int2* rows2, const int* meta2, const int* offsets2, int4* items2,
                                   int shift, hipStream_t st);

@@ -61,6 +61,31 @@ __device__ __forceinline__ int count_missing(uint32_t word) {
     return __popc(~(word >> 1) & word & 0x55555555u);  // pairs 01
 }
 
+// Block sweeps of the resident layout: a workgroup of 4 waves takes 32-SNP block b; per chunk t a wave reads the
+// chunk's 1 KiB with one 16-byte load per lane — lane l always lands on row l / 2 (half l % 2 of its 32 bytes), so
+// per-row sums stay in the lane and meet its partner's (l ^ 1) and the other waves' at the end.  Wave w takes chunks
+// t = w, w + 4, ... of [t_lo, t_hi).
+struct BlockRed {
+    int v[4][32][3];
+};
+// sums c[0..2] of lanes l and l ^ 1 (one row), then over the 4 waves: row i's totals on thread i (< 32) in out[]
+__device__ __forceinline__ void block_row_sums(BlockRed& sh, const int (&c)[3], int (&out)[3]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int t[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t[k] = c[k] + __shfl_xor(c[k], 1, 64);
+    if ((lane & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sh.v[w][lane >> 1][k] = t[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) out[k] = sh.v[0][threadIdx.x][k] + sh.v[1][threadIdx.x][k] + sh.v[2][threadIdx.x][k] +
+                                             sh.v[3][threadIdx.x][k];
+    }
+}
+
 // ---- loads: .bed rows -> the resident layout, oriented, with per-row missing flags (one pass over the rows) ----
 // A load takes slices of whole 32-SNP blocks (row0 a multiple of 32; the last slice may end mid-block) of a .bed image
 // (src: the slice's row r at r * nb bytes, any alignment: the file's rows follow a 3-byte magic number).  Per slice:
@@ -147,8 +172,10 @@ __global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restri
                                                          int n_rows, int n_snp, uint8_t* __restrict__ img,
                                                          int row_bytes, int P, const uint8_t* __restrict__ flip,
                                                          uint8_t* __restrict__ last, uint32_t keep_compat,
-                                                         uint32_t keep_strict, uint32_t* __restrict__ miss_flags) {
+                                                         uint32_t keep_strict, uint32_t* __restrict__ miss_flags,
+                                                         int* __restrict__ lcounts) {
     __shared__ uint32_t rowflags[4][32];
+    __shared__ BlockRed red;
     const int bl = blockIdx.x / P, part = blockIdx.x % P, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int i = lane >> 1, h = lane & 1;
     const int r = 32 * bl + i, j = row0 + r;  // the lane's row: in the slice, in the image
@@ -161,6 +188,7 @@ __global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restri
     // units [0, n_fast) of 16 bytes take the aligned-dword path (one dword past the unit stays inside the row)
     const int n_fast = nb >= 20 ? (nb - 20) / 16 + 1 : 0;
     uint32_t mflags = 0;  // bit 0 / 1: a missing call among the reference's / PLINK's individual slots
+    int cnt[3] = {0, 0, 0};  // genotype codes of the stored row in bytes [0, nb - 1) (hom A1, het, hom A2)
     auto one = [&](int t, const uint4 v_in) {
         const int u = 2 * t + h, p0 = 16 * u;
         uint4 v = v_in;
@@ -169,6 +197,10 @@ __global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restri
         if (!real) return;
         if (p0 + 16 <= nb - 1) {
             if (count_missing(v.x) + count_missing(v.y) + count_missing(v.z) + count_missing(v.w)) mflags |= 3u;
+            count_codes(v.x, cnt[0], cnt[1], cnt[2]);
+            count_codes(v.y, cnt[0], cnt[1], cnt[2]);
+            count_codes(v.z, cnt[0], cnt[1], cnt[2]);
+            count_codes(v.w, cnt[0], cnt[1], cnt[2]);
         } else if (p0 <= nb - 1) {  // the unit holding the last byte: the bytes before it, then the byte per order
             const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -177,7 +209,11 @@ __global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restri
                 for (int k = 0; k < 4; ++k) {
                     const int p = p0 + 4 * q + k;
                     const uint32_t byte = (wd[q] >> (8 * k)) & 0xFFu;
-                    if (p < nb - 1 && count_missing(byte)) mflags |= 3u;
+                    if (p < nb - 1) {
+                        if (count_missing(byte)) mflags |= 3u;
+                        // (a byte's four pairs, counted as a word whose upper bytes are 01 pairs: missing, no class)
+                        count_codes(byte | 0x55555500u, cnt[0], cnt[1], cnt[2]);
+                    }
                     if (p == nb - 1) {
                         last[j] = (uint8_t)byte;
                         if (count_missing(byte & keep_compat)) mflags |= 1u;
@@ -201,6 +237,18 @@ __global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restri
         for (int k = 0; k < LOAD_U; ++k) one(t + 4 * k, v[k]);
     }
     for (; t < t_hi; t += 4) one(t, fetch(t));
+    // rows' counts of this part (block_row_sums: the lane pair, then the four waves) to lcounts[(part n_snp + j) 3 + k]
+    {
+        int tot[3];
+        block_row_sums(red, cnt, tot);
+        const int jj = row0 + 32 * bl + threadIdx.x;
+        if (threadIdx.x < 32 && 32 * bl + (int)threadIdx.x < n_rows && jj < n_snp) {
+            int* o = lcounts + ((size_t)part * n_snp + jj) * 3;
+            o[0] = tot[0];
+            o[1] = tot[1];
+            o[2] = tot[2];
+        }
+    }
     // rows' flags: the lane pair, then the four waves, then one atomic per row and workgroup
     mflags |= __shfl_xor(mflags, 1, 64);
     if (h == 0) rowflags[w][i] = mflags;
@@ -218,30 +266,6 @@ __global__ void load_flags_kernel(const uint32_t* __restrict__ miss_flags, int n
     if (j < n_snp) row_miss[j] = (uint8_t)miss_flags[j];
 }
 
-// Block sweeps of the resident layout: a workgroup of 4 waves takes 32-SNP block b; per chunk t a wave reads the
-// chunk's 1 KiB with one 16-byte load per lane — lane l always lands on row l / 2 (half l % 2 of its 32 bytes), so
-// per-row sums stay in the lane and meet its partner's (l ^ 1) and the other waves' at the end.  Wave w takes chunks
-// t = w, w + 4, ... of [t_lo, t_hi).
-struct BlockRed {
-    int v[4][32][3];
-};
-// sums c[0..2] of lanes l and l ^ 1 (one row), then over the 4 waves: row i's totals on thread i (< 32) in out[]
-__device__ __forceinline__ void block_row_sums(BlockRed& sh, const int (&c)[3], int (&out)[3]) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int t[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) t[k] = c[k] + __shfl_xor(c[k], 1, 64);
-    if ((lane & 1) == 0) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) sh.v[w][lane >> 1][k] = t[k];
-    }
-    __syncthreads();
-    if (threadIdx.x < 32) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) out[k] = sh.v[0][threadIdx.x][k] + sh.v[1][threadIdx.x][k] + sh.v[2][threadIdx.x][k] +
-                                             sh.v[3][threadIdx.x][k];
-    }
-}
 
 // Halo pairs computed once across ranks (nldsc_engine_run_device_split): only pairs whose lower SNP lies in
 // [pair_lo, pair_hi) — the rank's owned range — keep flag bit 3 (snp_stats_kernel sets it on every SNP); the pairs of
@@ -280,48 +304,41 @@ __global__ void block_missing_rows_kernel(const uint8_t* __restrict__ row_miss, 
     blk_miss[b] = m;
 }
 
-// Per run: genotype-code counts of every row after setting the row's non-individual slots — the last byte's bit
-// pairs that are not individuals for this run's sample order, (saved byte & keep) | (pad & ~keep), and the pitch
-// padding — to this run's pad code: 0x55 ("missing": x = h = o = 0 for the int8 / fp32 kernels) or 0x00 for the
-// fp4 kernel, whose missing-indicator plane m must be 0 there so that SNPs without missing calls have an all-zero m
-// plane (their m products are skipped); its epilogue counts o = 1 - m over the n_org individual slots.
-// Grid: (block, part): part p of P sweeps chunks [p n_tail / P, (p + 1) n_tail / P) of the chunks before the last
-// byte's (16-byte non-temporal loads, 8 in flight per lane); part P - 1's wave 0 also rebuilds, writes and counts the
-// tail chunks (the last byte's and the padding after it), discounting 00-coded padding (n_pad00 slots).  Part p's
-// counts of SNP j go to parts[(p n_snp + j) 3 + k] (plain stores: no memset before the kernel, no atomics);
-// snp_stats_kernel adds the P parts.
-typedef uint32_t u32x4nt __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void count_chunk(const u32x4nt o, int (&c)[3]) {
-    count_codes(o.x, c[0], c[1], c[2]);
-    count_codes(o.y, c[0], c[1], c[2]);
-    count_codes(o.z, c[0], c[1], c[2]);
-    count_codes(o.w, c[0], c[1], c[2]);
-}
-
-__global__ void __launch_bounds__(256) count_rows_kernel(uint8_t* __restrict__ img, const uint8_t* __restrict__ last,
-                                                         int n_snp, int nb, int row_bytes, uint32_t tail_keep,
-                                                         uint32_t pad, int n_pad00, int P, int* __restrict__ parts) {
-    __shared__ BlockRed red;
-    const int b = blockIdx.x / P, part = blockIdx.x % P, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int h = lane & 1, j = 32 * b + (lane >> 1);
-    uint8_t* bbase = img + (size_t)b * 32 * (size_t)row_bytes;
-    const u32x4nt* blk = reinterpret_cast<const u32x4nt*>(bbase);
-    const int n_ch = row_bytes >> 5, tc0 = (nb - 1) >> 5;  // chunks [tc0, n_ch) hold the last byte and padding
-    const int t_lo = (int)((long long)tc0 * part / P), t_hi = (int)((long long)tc0 * (part + 1) / P);
+// Per run, one thread per row: the row's non-individual slots — the last byte's bit pairs that are not individuals
+// for this run's sample order, (saved byte & keep) | (pad & ~keep), and the pitch padding after it — set to this run's
+// pad code: 0x55 ("missing": x = h = o = 0 for the int8 / fp32 kernels) or 0x00 for the fp4 kernel, whose
+// missing-indicator plane m must be 0 there so that SNPs without missing calls have an all-zero m plane (their m
+// products are skipped; its epilogue counts o = 1 - m over the n_org individual slots); and the row's genotype counts:
+// the load's counts of bytes [0, nb - 1) (lcounts, P parts: load_tiled_kernel — the run's count pass over every row
+// until round 4, 6.3 GB at C3, now read where the load writes the rows) plus the last byte's individual pairs, to
+// counts3[3 j + k] (k = hom A1, het, hom A2; the statistics kernel's input as one part).
+__global__ void __launch_bounds__(256) tail_counts_kernel(uint8_t* __restrict__ img, const uint8_t* __restrict__ last,
+                                                          int n_snp, int nb, int row_bytes, uint32_t tail_keep,
+                                                          uint32_t pad, const int* __restrict__ lcounts, int P,
+                                                          int* __restrict__ counts3) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_snp) return;
     int c[3] = {0, 0, 0};
-    int t = t_lo + w;
-    for (; t + 28 < t_hi; t += 32) {
-        u32x4nt v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(blk + (size_t)(t + 4 * u) * 64 + lane);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) count_chunk(v[u], c);
+    for (int p = 0; p < P; ++p) {
+        const int* o = lcounts + ((size_t)p * n_snp + j) * 3;
+        c[0] += o[0];
+        c[1] += o[1];
+        c[2] += o[2];
     }
-    for (; t < t_hi; t += 4) count_chunk(__builtin_nontemporal_load(blk + (size_t)t * 64 + lane), c);
-    if (part == P - 1 && w == 0 && j < n_snp) {
-        const uint32_t lb = ((uint32_t)last[j] & tail_keep) | (pad & ~tail_keep & 0xFFu);
-        for (int tt = tc0; tt < n_ch; ++tt) {
-            uint4* unit = reinterpret_cast<uint4*>(bbase + (size_t)tt * 1024 + (size_t)(lane >> 1) * 32 + 16 * h);
+    const uint32_t lb = ((uint32_t)last[j] & tail_keep) | (pad & ~tail_keep & 0xFFu);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // the last byte's individual pairs
+        if (((tail_keep >> (2 * k)) & 3u) == 0) continue;
+        const uint32_t code = (lb >> (2 * k)) & 3u;
+        c[0] += code == 0;
+        c[1] += code == 2;
+        c[2] += code == 3;
+    }
+    uint8_t* rbase = img + (size_t)(j >> 5) * 32 * (size_t)row_bytes + (size_t)(j & 31) * 32;
+    const int n_ch = row_bytes >> 5, tc0 = (nb - 1) >> 5;  // chunks [tc0, n_ch) hold the last byte and padding
+    for (int t = tc0; t < n_ch; ++t)
+        for (int h = 0; h < 2; ++h) {
+            uint4* unit = reinterpret_cast<uint4*>(rbase + (size_t)t * 1024 + 16 * h);
             const uint4 v = *unit;
             uint32_t wd[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -329,26 +346,17 @@ __global__ void __launch_bounds__(256) count_rows_kernel(uint8_t* __restrict__ i
                 uint32_t o = 0;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const int p = 32 * tt + 16 * h + 4 * q + k;
+                    const int p = 32 * t + 16 * h + 4 * q + k;
                     const uint32_t byte = p < nb - 1 ? (wd[q] >> (8 * k)) & 0xFFu : p == nb - 1 ? lb : (pad & 0xFFu);
                     o |= byte << (8 * k);
                 }
                 wd[q] = o;
-                count_codes(o, c[0], c[1], c[2]);
             }
             *unit = make_uint4(wd[0], wd[1], wd[2], wd[3]);
         }
-        if (h == 0) c[0] -= n_pad00;
-    }
-    int tot[3];
-    block_row_sums(red, c, tot);
-    const int jj = 32 * b + threadIdx.x;
-    if (threadIdx.x < 32 && jj < n_snp) {
-        int* o = parts + ((size_t)part * n_snp + jj) * 3;
-        o[0] = tot[0];
-        o[1] = tot[1];
-        o[2] = tot[2];
-    }
+    counts3[3 * (size_t)j] = c[0];
+    counts3[3 * (size_t)j + 1] = c[1];
+    counts3[3 * (size_t)j + 2] = c[2];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2154,6 +2162,7 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
     static_assert(S >= 2, "ring of at least two stages");
     __shared__ QLds<S> sh;
     const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
+    if (it.w < 0) return;  // a null item of its 32-item group (plan_qemit_kernel)
     const int I4 = it.x, J4 = it.y;
     const bool dsup = I4 == J4;  // diagonal super-item: the column strips are the row strips
     auto strip_blk = [&](int s) { return s < 4 ? 4 * I4 + s : 4 * J4 + s - 4; };  // (may be >= nblk: no SNPs)
@@ -2365,7 +2374,7 @@ __global__ void issued_products_kernel(const int4* __restrict__ items, int n_ite
     } else if (items2 != nullptr && t < n_items + n_items2 && route_shift == 2) {
         // quad super-items (missing-free): a wave with any needed block pair issues all four pairs' products
         const int4 it = items2[t - n_items];
-        if (!(routed & 2) || q_routed(blk_miss, it.x, it.y, nblk)) {
+        if (it.w >= 0 && (!(routed & 2) || q_routed(blk_miss, it.x, it.y, nblk))) {
             for (int w = 0; w < 4; ++w) {
                 bool any = false;
                 for (int p = 0; p < 4; ++p) {
@@ -2410,6 +2419,47 @@ __global__ void plan_rows2_kernel(const int2* __restrict__ rows, int nblk, int s
     if (r2.x <= r2.y) {
         atomicMax(&meta[0], r2.y + 1);
         if (r2.x == 0) atomicAdd(&meta[2], 1);
+    }
+}
+
+// The quad kernel's super-items in groups of QG_R super-rows x QG_C diagonal offsets, QG_R QG_C = 32 items each —
+// one XCD's share of a round launch of 256 workgroups (xcd_slot gives XCD x the run [32 x, 32 x + 32)), so the 32
+// workgroups an XCD holds at once share 4 row and 11 column strips (4 x 4 super-strips) through its L2, where runs of
+// 32 items of the 16 x 16-tile order straddled tile rows (2 x 16: 19 strips, and tiles cut by the band edge broke the
+// alignment of every later run).  Items a group lacks (band edges) are null ((0, 0, 0, -1): the kernels return at
+// once), so every group is exactly 32 long.  Empty groups are skipped.
+constexpr int QG_R = 4, QG_C = 8;
+__device__ __forceinline__ int qg_n_c(const int* meta2) { return (meta2[0] + QG_C - 1) / QG_C; }
+__global__ void plan_qcount_kernel(const int2* __restrict__ rows2, int nblk2, const int* __restrict__ meta2,
+                                   int* __restrict__ counts) {
+    const int n_r = (nblk2 + QG_R - 1) / QG_R, n_c = qg_n_c(meta2);
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n_r * n_c; k += gridDim.x * blockDim.x) {
+        const int R = k / n_c, C = k % n_c;
+        bool any = false;
+        for (int I = R * QG_R; I < min(nblk2, R * QG_R + QG_R); ++I)
+            any |= max(rows2[I].x, C * QG_C) <= min(rows2[I].y, C * QG_C + QG_C - 1);
+        counts[k] = any ? QG_R * QG_C : 0;
+    }
+}
+// one workgroup: exclusive scan of the group counts in place; meta2[1] = total items (nulls included)
+__global__ void __launch_bounds__(PLAN_WG) plan_qscan_kernel(int* __restrict__ counts, int nblk2, int* __restrict__ meta2) {
+    __shared__ int part[PLAN_WG];
+    const int total = chunked_scan_excl<false>(counts, (nblk2 + QG_R - 1) / QG_R * qg_n_c(meta2), 0, part);
+    if (threadIdx.x == 0) meta2[1] = total;
+}
+__global__ void plan_qemit_kernel(const int2* __restrict__ rows2, int nblk2, const int* __restrict__ meta2,
+                                  const int* __restrict__ offsets, int4* __restrict__ items) {
+    const int n_r = (nblk2 + QG_R - 1) / QG_R, n_c = qg_n_c(meta2);
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n_r * n_c; k += gridDim.x * blockDim.x) {
+        const int R = k / n_c, C = k % n_c;
+        const int o0 = offsets[k], o1 = k + 1 < n_r * n_c ? offsets[k + 1] : meta2[1];
+        if (o1 == o0) continue;
+        int o = o0;
+        for (int I = R * QG_R; I < min(nblk2, R * QG_R + QG_R); ++I) {
+            const int a = max(rows2[I].x, C * QG_C), b = min(rows2[I].y, C * QG_C + QG_C - 1);
+            for (int d = a; d <= b; ++d) items[o++] = make_int4(I, I + d, 1, 0);
+        }
+        for (; o < o1; ++o) items[o] = make_int4(0, 0, 0, -1);
     }
 }
 
@@ -2696,18 +2746,22 @@ __global__ void __launch_bounds__(256) synth_bed_kernel(uint8_t* __restrict__ ro
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
+int load_parts(int n_snp, int row_bytes) {
+    // parts per block: about 16 k workgroups over the whole image, at least 8 chunks each
+    const int n_ch = row_bytes >> 5, nblk_img = (n_snp + 31) / 32;
+    return std::max(1, std::min(std::max(n_ch / 8, 1), (16384 + nblk_img - 1) / nblk_img));
+}
+
 hipError_t launch_load_slice(const uint8_t* src, int nb, int row0, int n_rows, int n_snp, uint8_t* img, int row_bytes,
                              bool orient, uint8_t* flip, uint8_t* last, uint32_t keep_compat, uint32_t keep_strict,
-                             uint32_t* miss_flags, hipStream_t st) {
+                             uint32_t* miss_flags, int* lcounts, hipStream_t st) {
     if (n_rows <= 0) return hipSuccess;
     if (row0 % 32 != 0 || row0 + n_rows > n_snp) return hipErrorInvalidValue;
     hipLaunchKernelGGL(load_orient_kernel, dim3((n_rows + 3) / 4), dim3(256), 0, st, src, nb, row0, n_rows,
                        orient ? 1 : 0, flip, miss_flags);
-    // parts per block: about 16 k workgroups over the whole image (as the count kernel), at least 8 chunks each
-    const int n_ch = row_bytes >> 5, nblk_img = (n_snp + 31) / 32, nblk = (n_rows + 31) / 32;
-    const int P = std::max(1, std::min(std::max(n_ch / 8, 1), (16384 + nblk_img - 1) / nblk_img));
+    const int nblk = (n_rows + 31) / 32, P = load_parts(n_snp, row_bytes);
     hipLaunchKernelGGL(load_tiled_kernel, dim3(nblk * P), dim3(256), 0, st, src, nb, row0, n_rows, n_snp, img,
-                       row_bytes, P, flip, last, keep_compat, keep_strict, miss_flags);
+                       row_bytes, P, flip, last, keep_compat, keep_strict, miss_flags, lcounts);
     return hipGetLastError();
 }
 
@@ -2717,19 +2771,11 @@ hipError_t launch_load_flags(const uint32_t* miss_flags, int n_snp, uint8_t* row
     return hipGetLastError();
 }
 
-int count_parts(int n_snp, int nb) {
-    // parts per block: about 16 k workgroups in all (8 resident per CU: several rounds, small tails), at least 8
-    // chunks each
-    const int nblk = (n_snp + 31) / 32, tc0 = (nb - 1) >> 5;
-    return std::max(1, std::min(std::max(tc0 / 8, 1), (16384 + nblk - 1) / nblk));
-}
-
-hipError_t launch_count_rows(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
-                             uint32_t pad, int n_pad00, int* parts, hipStream_t st) {
+hipError_t launch_tail_counts(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
+                              uint32_t pad, const int* lcounts, int P, int* counts3, hipStream_t st) {
     if (n_snp <= 0) return hipSuccess;
-    const int nblk = (n_snp + 31) / 32, P = count_parts(n_snp, nb);
-    hipLaunchKernelGGL(count_rows_kernel, dim3(nblk * P), dim3(256), 0, st, img, last, n_snp, nb, row_bytes, tail_keep,
-                       pad, n_pad00, P, parts);
+    hipLaunchKernelGGL(tail_counts_kernel, dim3((n_snp + 255) / 256), dim3(256), 0, st, img, last, n_snp, nb, row_bytes,
+                       tail_keep, pad, lcounts, P, counts3);
     return hipGetLastError();
 }
 
@@ -2860,13 +2906,25 @@ hipError_t launch_band_i8(bool dom, int max_nc, int n_items, const uint32_t* gen
     return hipGetLastError();
 }
 
+int plan_super_counts(int n, int shift) {
+    const int nblk2 = ((n + 31) / 32 + (1 << shift) - 1) >> shift;
+    if (shift == 2) return ((nblk2 + QG_R - 1) / QG_R) * ((nblk2 + QG_C - 1) / QG_C + 1);
+    const int n_t2 = (nblk2 + PLAN_R - 1) / PLAN_R;
+    return n_t2 * n_t2;
+}
+
 hipError_t launch_plan_super(int n, const int2* rows, int2* rows2, int* counts2, int* meta2, int shift, hipStream_t st) {
     const int nblk = (n + 31) / 32, nblk2 = (nblk + (1 << shift) - 1) >> shift;
     hipError_t e = hipMemsetAsync(meta2, 0, 4 * sizeof(int), st);
     if (e != hipSuccess || n <= 0) return e;
     hipLaunchKernelGGL(plan_rows2_kernel, dim3((nblk2 + 255) / 256), dim3(256), 0, st, rows, nblk, shift, rows2, meta2);
-    hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, counts2, 0);
-    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(PLAN_WG), 0, st, counts2, nblk2, meta2);
+    if (shift == 2) {  // the quad kernel's 32-item groups
+        hipLaunchKernelGGL(plan_qcount_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, counts2);
+        hipLaunchKernelGGL(plan_qscan_kernel, dim3(1), dim3(PLAN_WG), 0, st, counts2, nblk2, meta2);
+    } else {
+        hipLaunchKernelGGL(plan_count_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, counts2, 0);
+        hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(PLAN_WG), 0, st, counts2, nblk2, meta2);
+    }
     return hipGetLastError();
 }
 
@@ -2875,7 +2933,10 @@ hipError_t launch_plan_emit_super(int n, const int2* rows2, const int* meta2, co
                                   int shift, hipStream_t st) {
     const int nblk2 = ((n + 31) / 32 + (1 << shift) - 1) >> shift;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, offsets2, items2, 0);
+    if (shift == 2)
+        hipLaunchKernelGGL(plan_qemit_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, offsets2, items2);
+    else
+        hipLaunchKernelGGL(plan_emit_kernel, dim3(256), dim3(256), 0, st, rows2, nblk2, meta2, offsets2, items2, 0);
     return hipGetLastError();
 }
 

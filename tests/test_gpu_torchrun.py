@@ -115,21 +115,28 @@ def test_rccl_device_gather_one_rank(tmp_path):
 
 def test_bench_force_dist_rccl_one_rank():
     """`bench.py --force-dist`: the strong-scaling bench's N-GPU code (process group, owned range + halo, device
-    table, RCCL gather every step, max-over-ranks timing) run as a group of one on the one GPU."""
+    table, RCCL gather every step, max-over-ranks timing) run as a group of one on the one GPU.  The line records the
+    RCCL group it saw (rccl_world) and, in the overlapped mode, each step's gather timed with HIP events on its side
+    stream (gather_ms: the all-gather, assembly and D2H on the GPU), the host's wait for an earlier gather and the
+    enqueue time apart (verdict r04: gather_ms used to time the enqueue only)."""
     import json
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     def bench(*extra):
         p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--no-cpu", "--no-file", "--steps", "3",
-                            "--warmup", "1", "--n-snp", "6000", "--n-org", "20000", "--length-cm", "21", *extra],
+                            "--warmup", "1", "--n-snp", "6000", "--n-org", "20000", "--length-cm", "21", "--no-extra",
+                            *extra],
                            cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
         assert p.returncode == 0, p.stderr[-3000:]
         return json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     d = bench("--force-dist")
     assert d["n_gpus"] == 1 and d["value"] > 0 and "RCCL" in d["config"]["parallelism"], d
     assert "side stream" in d["config"]["parallelism"], d  # each step's gather beside the next step's compute
-    assert d["stages_ms"]["gather_ms"] >= 0 and d["per_rank"][0]["owned_snps"] == 6000
+    assert d["stages_ms"]["gather_ms"] > 0 and d["per_rank"][0]["owned_snps"] == 6000
+    r0 = d["per_rank"][0]
+    assert d["rccl_world"] == 1 and d["collectives_backend"] == "nccl", d
+    assert r0["gather_ms"] > 0 and r0["gather_enqueue_ms"] > 0 and r0["gather_wait_ms"] >= 0 and "gather_note" in d, r0
     # the overlapped gather, the sequential one and the one-process run: the same table
     seq, one = bench("--force-dist", "--no-gather-overlap"), bench()
     assert "side stream" not in seq["config"]["parallelism"], seq
