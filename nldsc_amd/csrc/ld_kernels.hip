@@ -2162,7 +2162,6 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
     static_assert(S >= 2, "ring of at least two stages");
     __shared__ QLds<S> sh;
     const int4 it = items[xcd ? xcd_slot(blockIdx.x, gridDim.x) : blockIdx.x];
-    if (it.w < 0) return;  // a null item of its 32-item group (plan_qemit_kernel)
     const int I4 = it.x, J4 = it.y;
     const bool dsup = I4 == J4;  // diagonal super-item: the column strips are the row strips
     auto strip_blk = [&](int s) { return s < 4 ? 4 * I4 + s : 4 * J4 + s - 4; };  // (may be >= nblk: no SNPs)
@@ -2374,7 +2373,7 @@ __global__ void issued_products_kernel(const int4* __restrict__ items, int n_ite
     } else if (items2 != nullptr && t < n_items + n_items2 && route_shift == 2) {
         // quad super-items (missing-free): a wave with any needed block pair issues all four pairs' products
         const int4 it = items2[t - n_items];
-        if (it.w >= 0 && (!(routed & 2) || q_routed(blk_miss, it.x, it.y, nblk))) {
+        if (!(routed & 2) || q_routed(blk_miss, it.x, it.y, nblk)) {
             for (int w = 0; w < 4; ++w) {
                 bool any = false;
                 for (int p = 0; p < 4; ++p) {
@@ -2422,12 +2421,13 @@ __global__ void plan_rows2_kernel(const int2* __restrict__ rows, int nblk, int s
     }
 }
 
-// The quad kernel's super-items in groups of QG_R super-rows x QG_C diagonal offsets, QG_R QG_C = 32 items each —
-// one XCD's share of a round launch of 256 workgroups (xcd_slot gives XCD x the run [32 x, 32 x + 32)), so the 32
-// workgroups an XCD holds at once share 4 row and 11 column strips (4 x 4 super-strips) through its L2, where runs of
-// 32 items of the 16 x 16-tile order straddled tile rows (2 x 16: 19 strips, and tiles cut by the band edge broke the
-// alignment of every later run).  Items a group lacks (band edges) are null ((0, 0, 0, -1): the kernels return at
-// once), so every group is exactly 32 long.  Empty groups are skipped.
+// The quad kernel's super-items in tile order: row groups of QG_R super-rows, and within one the items by diagonal
+// offset d, then super-row — so a run of 32 consecutive items (one XCD's share of a round launch of 256 workgroups:
+// xcd_slot gives XCD x the run [32 x, 32 x + 32)) is 8 offsets of the same 4 super-rows where the band is full, and the
+// 32 workgroups an XCD holds at once share 4 row and 11 column strips (4 x 4 super-strips) through its L2; in the
+// 16 x 16-tile order a run straddled tile rows (2 x 16: 19 strips).  No padding: a null item would hold a wave slot of
+// its round (32-item groups padded at the band edge: C5 -7.5 %).  Counted and emitted per (row group, block of QG_C
+// offsets), in that order.
 constexpr int QG_R = 4, QG_C = 8;
 __device__ __forceinline__ int qg_n_c(const int* meta2) { return (meta2[0] + QG_C - 1) / QG_C; }
 __global__ void plan_qcount_kernel(const int2* __restrict__ rows2, int nblk2, const int* __restrict__ meta2,
@@ -2435,13 +2435,13 @@ __global__ void plan_qcount_kernel(const int2* __restrict__ rows2, int nblk2, co
     const int n_r = (nblk2 + QG_R - 1) / QG_R, n_c = qg_n_c(meta2);
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n_r * n_c; k += gridDim.x * blockDim.x) {
         const int R = k / n_c, C = k % n_c;
-        bool any = false;
+        int n = 0;
         for (int I = R * QG_R; I < min(nblk2, R * QG_R + QG_R); ++I)
-            any |= max(rows2[I].x, C * QG_C) <= min(rows2[I].y, C * QG_C + QG_C - 1);
-        counts[k] = any ? QG_R * QG_C : 0;
+            n += max(0, min(rows2[I].y, C * QG_C + QG_C - 1) - max(rows2[I].x, C * QG_C) + 1);
+        counts[k] = n;
     }
 }
-// one workgroup: exclusive scan of the group counts in place; meta2[1] = total items (nulls included)
+// one workgroup: exclusive scan of the group counts in place; meta2[1] = total items
 __global__ void __launch_bounds__(PLAN_WG) plan_qscan_kernel(int* __restrict__ counts, int nblk2, int* __restrict__ meta2) {
     __shared__ int part[PLAN_WG];
     const int total = chunked_scan_excl<false>(counts, (nblk2 + QG_R - 1) / QG_R * qg_n_c(meta2), 0, part);
@@ -2452,14 +2452,11 @@ __global__ void plan_qemit_kernel(const int2* __restrict__ rows2, int nblk2, con
     const int n_r = (nblk2 + QG_R - 1) / QG_R, n_c = qg_n_c(meta2);
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n_r * n_c; k += gridDim.x * blockDim.x) {
         const int R = k / n_c, C = k % n_c;
-        const int o0 = offsets[k], o1 = k + 1 < n_r * n_c ? offsets[k + 1] : meta2[1];
-        if (o1 == o0) continue;
-        int o = o0;
-        for (int I = R * QG_R; I < min(nblk2, R * QG_R + QG_R); ++I) {
-            const int a = max(rows2[I].x, C * QG_C), b = min(rows2[I].y, C * QG_C + QG_C - 1);
-            for (int d = a; d <= b; ++d) items[o++] = make_int4(I, I + d, 1, 0);
-        }
-        for (; o < o1; ++o) items[o] = make_int4(0, 0, 0, -1);
+        int o = offsets[k];
+        const int i_hi = min(nblk2, R * QG_R + QG_R);
+        for (int d = C * QG_C; d < C * QG_C + QG_C; ++d)
+            for (int I = R * QG_R; I < i_hi; ++I)
+                if (rows2[I].x <= d && d <= rows2[I].y) items[o++] = make_int4(I, I + d, 1, 0);
     }
 }
 
