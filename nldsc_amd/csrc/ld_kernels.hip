@@ -102,16 +102,15 @@ __device__ __forceinline__ void block_row_sums(BlockRed& sh, const int (&c)[3], 
 // nearly all).
 constexpr int LOAD_ORIENT_BYTES = 1024;
 
-// 16 source bytes at any alignment: aligned dword loads + byte shifts (src + o .. + 16 must lie within the buffer and
-// so must the dword after it when o is not a multiple of 4: the caller keeps the last units of a row on the byte path)
+// 16 source bytes at any alignment (src + o .. + 16 within the buffer): one global_load_dwordx4 — the HSA memory model
+// runs in unaligned access mode, and the compiler emits the vector load for this 1-byte-aligned type (five dword loads
+// and byte shifts before: the load kernel's source reads took 5x the vector-memory instructions)
+struct __attribute__((packed, aligned(1))) Bytes16 {
+    uint32_t x, y, z, w;
+};
 __device__ __forceinline__ uint4 load16_unaligned(const uint8_t* __restrict__ src, size_t o) {
-    const size_t a = o & ~(size_t)3;
-    const uint32_t sh = (uint32_t)(o & 3);
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(src + a);
-    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3];
-    const uint32_t d4 = sh ? p[4] : 0u;
-    return make_uint4(__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
-                      __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh));
+    const Bytes16 q = *reinterpret_cast<const Bytes16*>(src + o);
+    return make_uint4(q.x, q.y, q.z, q.w);
 }
 // bytes [p0, p0 + 16) of a row of nb bytes (bytes past it read as `fill`), one byte at a time
 __device__ __forceinline__ uint4 load16_bytes(const uint8_t* __restrict__ row, int p0, int nb, uint32_t fill) {
@@ -146,7 +145,7 @@ __global__ void __launch_bounds__(256) load_orient_kernel(const uint8_t* __restr
         const int p0 = 16 * lane;
         if (p0 < head) {
             // (bytes past the head, or past the row, read as 0x55: missing, counted in neither class)
-            const uint4 v = p0 + 20 <= nb && p0 + 16 <= head ? load16_unaligned(src, (size_t)r * nb + p0)
+            const uint4 v = p0 + 16 <= head ? load16_unaligned(src, (size_t)r * nb + p0)
                                                                : load16_bytes(row, p0, head, 0x55u);
             count_codes(v.x, c0, c1, c2);
             count_codes(v.y, c0, c1, c2);
@@ -164,10 +163,14 @@ __global__ void __launch_bounds__(256) load_orient_kernel(const uint8_t* __restr
     }
 }
 
-// grid (block of the slice, part): part p of P sweeps the block's chunks [p n_ch / P, (p + 1) n_ch / P); wave w
-// chunks t = lo + w, lo + w + 4, ...  n_snp: the image's SNPs (rows past it, in its last block: 0x55).  keep_compat /
-// keep_strict: the last byte's bit pairs that are individuals in the reference's / PLINK's sample order.
-constexpr int LOAD_U = 4;  // chunks in flight per lane
+// grid (block of the slice, part): part p of P sweeps the block's chunks [p n_ch / P, (p + 1) n_ch / P) in stages of
+// LOAD_SC chunks: the workgroup reads the stage's 32 row segments (LOAD_SC x 32 bytes each) row by row — 8 threads per
+// row, 128 contiguous bytes per 8 lanes, whole lines — into LDS, then wave w writes chunks t = t0 + w, t0 + w + 4, ...
+// of the stage (lane l: row l / 2, half l % 2) as whole 1 KiB chunks.  Reading the source 32 bytes per row and chunk
+// straight into the chunk layout touched 32 rows' lines at once per wave: 4.0 TB/s of read + write at C3 (3.16 ms).
+// n_snp: the image's SNPs (rows past it, in its last block: 0x55).  keep_compat / keep_strict: the last byte's bit
+// pairs that are individuals in the reference's / PLINK's sample order.
+constexpr int LOAD_SC = 16;  // chunks per stage (LDS: 32 rows x LOAD_SC x 32 bytes)
 __global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restrict__ src, int nb, int row0,
                                                          int n_rows, int n_snp, uint8_t* __restrict__ img,
                                                          int row_bytes, int P, const uint8_t* __restrict__ flip,
@@ -176,6 +179,7 @@ __global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restri
                                                          int* __restrict__ lcounts) {
     __shared__ uint32_t rowflags[4][32];
     __shared__ BlockRed red;
+    __shared__ uint4 tile[32][2 * LOAD_SC + 1];  // (+1 unit: rows 528 bytes apart in LDS)
     const int bl = blockIdx.x / P, part = blockIdx.x % P, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int i = lane >> 1, h = lane & 1;
     const int r = 32 * bl + i, j = row0 + r;  // the lane's row: in the slice, in the image
@@ -184,9 +188,8 @@ __global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restri
     const int n_ch = row_bytes >> 5;
     const int t_lo = (int)((long long)n_ch * part / P), t_hi = (int)((long long)n_ch * (part + 1) / P);
     uint8_t* blk = img + (size_t)(row0 / 32 + bl) * 32 * (size_t)row_bytes;
-    const size_t rbase = (size_t)r * nb;
-    // units [0, n_fast) of 16 bytes take the aligned-dword path (one dword past the unit stays inside the row)
-    const int n_fast = nb >= 20 ? (nb - 20) / 16 + 1 : 0;
+    // units [0, n_fast) of 16 bytes lie inside the row: one vector load each
+    const int n_fast = nb / 16;
     uint32_t mflags = 0;  // bit 0 / 1: a missing call among the reference's / PLINK's individual slots
     int cnt[3] = {0, 0, 0};  // genotype codes of the stored row in bytes [0, nb - 1) (hom A1, het, hom A2)
     auto one = [&](int t, const uint4 v_in) {
@@ -222,21 +225,24 @@ __global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restri
                 }
         }
     };
-    auto fetch = [&](int t) -> uint4 {
-        const int u = 2 * t + h;
-        // (rows past the slice end the image: the last block's padding rows)
-        if (r >= n_rows) return make_uint4(0x55555555u, 0x55555555u, 0x55555555u, 0x55555555u);
-        return u < n_fast ? load16_unaligned(src, rbase + 16 * (size_t)u) : load16_bytes(src + rbase, 16 * u, nb, 0x55u);
-    };
-    int t = t_lo + w;
-    for (; t + 4 * (LOAD_U - 1) < t_hi; t += 4 * LOAD_U) {
-        uint4 v[LOAD_U];
+    // the stage reader: thread tid takes row tid / 8 of the block and its units (tid % 8) + 8 k of the stage
+    const int rr = threadIdx.x >> 3, c8 = threadIdx.x & 7;
+    const int gr = 32 * bl + rr;  // (in the slice; rows past it end the image: the last block's padding rows)
+    const size_t gbase = (size_t)gr * nb;
+    for (int t0 = t_lo; t0 < t_hi; t0 += LOAD_SC) {
+        const int nu = 2 * min(LOAD_SC, t_hi - t0);  // units per row this stage
 #pragma unroll
-        for (int k = 0; k < LOAD_U; ++k) v[k] = fetch(t + 4 * k);
-#pragma unroll
-        for (int k = 0; k < LOAD_U; ++k) one(t + 4 * k, v[k]);
+        for (int k = 0; k < 2 * LOAD_SC / 8; ++k) {
+            const int uu = c8 + 8 * k, u = 2 * t0 + uu;
+            if (uu < nu)
+                tile[rr][uu] = gr >= n_rows ? make_uint4(0x55555555u, 0x55555555u, 0x55555555u, 0x55555555u)
+                               : u < n_fast ? load16_unaligned(src, gbase + 16 * (size_t)u)
+                                            : load16_bytes(src + gbase, 16 * u, nb, 0x55u);
+        }
+        __syncthreads();
+        for (int t = t0 + w; t < t0 + nu / 2; t += 4) one(t, tile[i][2 * (t - t0) + h]);
+        __syncthreads();
     }
-    for (; t < t_hi; t += 4) one(t, fetch(t));
     // rows' counts of this part (block_row_sums: the lane pair, then the four waves) to lcounts[(part n_snp + j) 3 + k]
     {
         int tot[3];

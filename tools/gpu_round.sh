@@ -34,7 +34,7 @@ find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats_c3.csv \;
 fi
 pmc() {  # <label> <workload string> <alg-bytes spec> <bench args>
   local label=$1 wl=$2 alg=$3; shift 3
-  local B="python3 bench.py --no-cpu --no-file --steps 1 --warmup 0 $*" P=$O/pmc_$label
+  local B="python3 bench.py --no-cpu --no-file --no-extra --steps 1 --warmup 0 $*" P=$O/pmc_$label
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $P/fetch -o f --output-format csv -- $B > /dev/null 2> $P.f.err && \
   timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $P/write -o w --output-format csv -- $B > /dev/null 2> $P.w.err && \
   timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU --kernel-trace -d $P/sq -o s --output-format csv -- $B > /dev/null 2> $P.s.err && \
