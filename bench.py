@@ -45,7 +45,7 @@ PATHS = {
 def band_kernel_name(variant: str, dom: bool, default: str) -> str:
     """The band kernel that ran (Engine.timings()['band_kernel']) as rocprof names it, with what it issues."""
     d = "true" if dom else "false"
-    # the single-block kernel: additive-only runs pair neighbouring column blocks per wave ($NLDSC_F4_NC2, default)
+    # the single-block kernel: additive-only runs pair neighbouring column blocks per wave (engine option f4_nc2, default)
     single = ("band_f4_kernel<true, 2, 0, false> (one wave per 32x32 block pair)" if dom else
               "band_f4_kernel<false, 2, 0, false, 2> (one wave per 32x64 pair of column blocks)")
     names = {
