@@ -192,6 +192,17 @@ __global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restri
     const int n_fast = nb / 16;
     uint32_t mflags = 0;  // bit 0 / 1: a missing call among the reference's / PLINK's individual slots
     int cnt[3] = {0, 0, 0};  // genotype codes of the stored row in bytes [0, nb - 1) (hom A1, het, hom A2)
+    // whole units before the last byte, per 16-code word with hi / lo the pairs' high / low bits: popcounts of hi,
+    // hi & lo (hom A2) and hi | lo (not hom A1), and lo & ~hi (missing) ORed — the classes follow at the end
+    int n_hi = 0, n_and = 0, n_or = 0, n_words = 0;
+    uint32_t miss_or = 0;
+    auto tally = [&](uint32_t word) {
+        const uint32_t hi = (word >> 1) & 0x55555555u, lo = word & 0x55555555u;
+        n_hi += __popc(hi);
+        n_and += __popc(hi & lo);
+        n_or += __popc(hi | lo);
+        miss_or |= lo & ~hi;
+    };
     auto one = [&](int t, const uint4 v_in) {
         const int u = 2 * t + h, p0 = 16 * u;
         uint4 v = v_in;
@@ -199,11 +210,11 @@ __global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restri
         *reinterpret_cast<uint4*>(blk + (size_t)t * 1024 + (size_t)i * 32 + 16 * h) = v;
         if (!real) return;
         if (p0 + 16 <= nb - 1) {
-            if (count_missing(v.x) + count_missing(v.y) + count_missing(v.z) + count_missing(v.w)) mflags |= 3u;
-            count_codes(v.x, cnt[0], cnt[1], cnt[2]);
-            count_codes(v.y, cnt[0], cnt[1], cnt[2]);
-            count_codes(v.z, cnt[0], cnt[1], cnt[2]);
-            count_codes(v.w, cnt[0], cnt[1], cnt[2]);
+            tally(v.x);
+            tally(v.y);
+            tally(v.z);
+            tally(v.w);
+            n_words += 4;
         } else if (p0 <= nb - 1) {  // the unit holding the last byte: the bytes before it, then the byte per order
             const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -243,6 +254,10 @@ __global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restri
         for (int t = t0 + w; t < t0 + nu / 2; t += 4) one(t, tile[i][2 * (t - t0) + h]);
         __syncthreads();
     }
+    cnt[0] += 16 * n_words - n_or;
+    cnt[1] += n_hi - n_and;
+    cnt[2] += n_and;
+    if (miss_or) mflags |= 3u;
     // rows' counts of this part (block_row_sums: the lane pair, then the four waves) to lcounts[(part n_snp + j) 3 + k]
     {
         int tot[3];

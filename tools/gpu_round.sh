@@ -7,6 +7,7 @@
 #   gpurun --timeout 1200 -- bash tools/gpu_tests.sh <tag>                       (the GPU suite + smoke)
 #   gpurun --timeout 1200 -- bash tools/gpu_round.sh <tag> skip-tests bench      (bench, rocprof stats)
 #   gpurun --timeout 1200 -- bash tools/gpu_round.sh <tag> skip-tests pmc        (PMC passes, C2 / C5, scaling)
+#   (phase pmc-only: the PMC passes alone)
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 T=${1:-run}
 O=gpurun_out/$T
@@ -52,6 +53,7 @@ step pmc c2
 pmc c2 "C2 bench: N=50000 M=80000 missing=0.01 additive-only 1 cM" band_f4_kernel=1003520000 --n-org 50000 --additive-only || exit 1
 step pmc c5
 LDS_PASS=1 pmc c5 "C5 slice bench: N=315599 M=1250000 missing=0 add+dom 1000 kb" band_f4_q_kernel=98640000000 --workload c5 || exit 1
+[ "$PH" = pmc-only ] && { step done; exit 0; }
 step bench c2 c5
 timeout -k 10 300 python bench.py --no-cpu --no-file --steps 10 --n-org 50000 --additive-only > $O/bench_c2.json 2> $O/bench_c2.err || { tail $O/bench_c2.err; exit 1; }
 timeout -k 10 400 python bench.py --no-cpu --no-file --steps 2 --workload c5 > $O/bench_c5.json 2> $O/bench_c5.err || { tail $O/bench_c5.err; exit 1; }
