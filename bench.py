@@ -433,7 +433,8 @@ def main():
     if rank == 0 and not use_dist and (not args.no_cpu or want_file):
         bed_host = buf.cpu().numpy().tobytes()
     # (N = 1: the device image stays for the one-shot measurement after the timed region)
-    want_extra = rank == 0 and not use_dist and not args.no_extra and args.workload == "c3" and args.path == "f4"
+    want_extra = (rank == 0 and not use_dist and not split and not args.no_extra and args.workload == "c3"
+                  and args.path == "f4")
     img_dev = buf if want_extra else None
     del buf
     torch.cuda.empty_cache()

@@ -144,6 +144,30 @@ def test_bench_force_dist_rccl_one_rank():
                                                                               one["table_digest"])
 
 
+def test_bench_default_line_records_and_rehearsal():
+    """The default one-GPU bench line carries its extra records after the timed region (fp32_path: the fp32 MFMA
+    path on the same rows, its window counts equal to the default path's; oneshot_gpu_ms: load + run), and a
+    rehearsal of one rank of 8 (`--rehearse 0/8`, a split run whose host result is the owned slice alone) skips them."""
+    import json
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    def bench(*extra):
+        p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--no-cpu", "--no-file", "--steps", "2",
+                            "--warmup", "1", "--n-snp", "6000", "--n-org", "20000", "--length-cm", "21", *extra],
+                           cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-3000:]
+        return json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    d = bench()
+    f = d["fp32_path"]
+    assert f["band_ms"] > 0 and 0 < f["frac"] < 1 and f["vs_default_path"]["l2_ws_equal"], f
+    assert f["vs_default_path"]["l2d_ws_equal"] and f["vs_default_path"]["l2_max_abs_diff"] < 1e-3, f
+    o = d["oneshot_gpu_ms"]
+    assert o["load"] > 0 and o["run"] > 0 and abs(o["total"] - o["load"] - o["run"]) < 0.01, o
+    r = bench("--rehearse", "0/8")
+    assert "fp32_path" not in r and "oneshot_gpu_ms" not in r and r["value"] > 0, r
+
+
 SPLIT_SCRIPT = r'''
 import json, os, sys
 sys.path.insert(0, {repo!r})
