@@ -64,8 +64,10 @@ def main():
     alg = dict((k, float(v)) for k, v in (a.split("=") for a in args.alg_bytes))
     fetch, write, sq, l2, lds = (read_counters(os.path.join(args.dir, p))
                                  for p in ("fetch", "write", "sq", "l2", "lds"))
-    # engine runs in the profiled command: finalize_kernel runs once per run (the band may take several launches)
-    runs = len(fetch.get("finalize_kernel", {}).get("FETCH_SIZE", [])) or None
+    # engine runs in the profiled command: tail_counts_kernel runs once per run (the band may take several launches;
+    # round 4's per-run finalize_kernel is finalize_out_kernel for host results since round 5)
+    runs = next((len(fetch[k]["FETCH_SIZE"]) for k in ("tail_counts_kernel", "finalize_out_kernel", "finalize_kernel")
+                 if fetch.get(k, {}).get("FETCH_SIZE")), None)
     kernels = {}
     for name in sorted(set(fetch) | set(write) | set(sq)):
         if name.startswith("__amd"):
