@@ -1655,6 +1655,13 @@ __device__ __forceinline__ f32x16v mfma_f4(const i32x4& a, const i32x4& b, const
 // of 2^16 move to packed 16-bit counters (additive-only), exact while every entry is <= 16N < 2^31.
 // PART: K-split partial mode (small launches, see band_f4_part_kernel): run chunks [t_lo, t_hi) only and store
 // the 8 fp32 Gram tiles to `part` (exact integers) instead of running the epilogue.
+// the chunk loads of the K loop stay where they are written (issued two K steps before their data is decoded): left to
+// itself the scheduler sank them to within ~10 MFMAs of their use, behind an s_waitcnt vmcnt(0)
+#ifdef NLDSC_STUDY_NO_LOAD_FENCE
+#define NLDSC_LOAD_FENCE() ((void)0)
+#else
+#define NLDSC_LOAD_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
 template <bool DOM, int NC, bool DIAG0, int SEG, bool KC, bool PART = false>
 __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const uint32_t* __restrict__ geno,
                                              int pitch_words, int n_it, const SnpConst* __restrict__ cst,
@@ -1747,6 +1754,7 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
             pr = rowp[CHUNK_U4 * min(t + 2, last)];
 #pragma unroll
             for (int c = 0; c < NC; ++c) pc[c] = colp[c][CHUNK_U4 * min(t + 2, last)];
+            NLDSC_LOAD_FENCE();
             a0 = decode_f4<RM>(qr.x, qr.y);
 #pragma unroll
             for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(qc[c].x, qc[c].y);
@@ -1758,6 +1766,7 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
             qr = rowp[CHUNK_U4 * min(t + 3, last)];
 #pragma unroll
             for (int c = 0; c < NC; ++c) qc[c] = colp[c][CHUNK_U4 * min(t + 3, last)];
+            NLDSC_LOAD_FENCE();
             a0 = decode_f4<RM>(pr.x, pr.y);
 #pragma unroll
             for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(pc[c].x, pc[c].y);
