@@ -1590,7 +1590,7 @@ constexpr int E8M0_ONE = 127;  // block scale 2^0
 constexpr int E8M0_HALF = 126;  // 2^-1
 // VALU instructions interleaved after each MFMA of a full 8-product K step (3, 5, 6 and alternating 4/5
 // measured slower in round 1)
-constexpr int F4_VPM = 4;
+constexpr int F4_VPM = 4;  // (with the fenced loads, 3 / 5 measured slower / equal: profiles/r05_ab_load_fence.json)
 
 struct F4Frag {
     i32x4 x, h, o;
@@ -1657,11 +1657,7 @@ __device__ __forceinline__ f32x16v mfma_f4(const i32x4& a, const i32x4& b, const
 // the 8 fp32 Gram tiles to `part` (exact integers) instead of running the epilogue.
 // the chunk loads of the K loop stay where they are written (issued two K steps before their data is decoded): left to
 // itself the scheduler sank them to within ~10 MFMAs of their use, behind an s_waitcnt vmcnt(0)
-#ifdef NLDSC_STUDY_NO_LOAD_FENCE
-#define NLDSC_LOAD_FENCE() ((void)0)
-#else
 #define NLDSC_LOAD_FENCE() __builtin_amdgcn_sched_barrier(0)
-#endif
 template <bool DOM, int NC, bool DIAG0, int SEG, bool KC, bool PART = false>
 __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const uint32_t* __restrict__ geno,
                                              int pitch_words, int n_it, const SnpConst* __restrict__ cst,
