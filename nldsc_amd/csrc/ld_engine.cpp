@@ -434,7 +434,7 @@ hipError_t alloc_image(nldsc_engine* e, int32_t n_snp, int32_t n_org) {
     if (he == hipSuccess) he = e->row_miss.ensure((size_t)n_snp);
     if (he == hipSuccess) he = e->miss_flags.ensure((size_t)n_snp);
     if (he == hipSuccess)
-        he = e->lcounts.ensure((size_t)nldsc::load_parts(n_snp, row_pitch(n_org)) * (size_t)n_snp * 3);
+        he = e->lcounts.ensure((size_t)n_snp * 3);
     return he;
 }
 
@@ -971,7 +971,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     const uint32_t pad = use_f4 ? 0x00u : 0x55u;
     HIPCHK(hipEventRecord(e->ev[0], st));  // (count_ms: the tail kernel alone; the host total covers the above)
     HIPCHK(nldsc::launch_tail_counts(e->bed.p, e->lastb.p, M, nb, row_bytes, tail_keep, pad, e->lcounts.p,
-                                     nldsc::load_parts(M, row_bytes), e->cparts.p, st));
+                                     1, e->cparts.p, st));  // (the load's parts add into one: load_tiled_kernel)
     HIPCHK(hipEventRecord(e->ev[1], st));
     if (gpu_plan) {
         HIPCHK(hipStreamWaitEvent(e->plan_stream, e->ev_pos, 0));

@@ -29,15 +29,15 @@ struct SnpConst {
 // stored 00 <-> 11 swapped; !orient: as in the file), its stored last byte saved to last[j], its missing calls
 // among the individual slots of the reference's (bit 0) / PLINK's (bit 1) sample order ORed into miss_flags[j]
 // (keep_*: the last byte's individual bit pairs per order), and the genotype counts of its stored bytes [0, nb - 1)
-// (hom A1, het, hom A2) per part p of load_parts(n_snp, row_bytes) to lcounts[(p n_snp + j) 3 + k].  After every
-// slice: launch_load_flags -> row_miss.
+// (hom A1, het, hom A2) added over the load_parts(n_snp, row_bytes) parts of the row into lcounts[3 j + k] (cleared by
+// the slice's orientation pass; integer atomics).  After every slice: launch_load_flags -> row_miss.
 int load_parts(int n_snp, int row_bytes);
 hipError_t launch_load_slice(const uint8_t* src, int nb, int row0, int n_rows, int n_snp, uint8_t* img, int row_bytes,
                              bool orient, uint8_t* flip, uint8_t* last, uint32_t keep_compat, uint32_t keep_strict,
                              uint32_t* miss_flags, int* lcounts, hipStream_t st);
 hipError_t launch_load_flags(const uint32_t* miss_flags, int n_snp, uint8_t* row_miss, hipStream_t st);
 // per run: set each row's non-individual slots (last byte outside tail_keep, pitch padding) to `pad` (0x55 missing,
-// or 0x00 for the fp4 kernel) and its genotype counts — the load's lcounts (P parts) plus the last byte's individual
+// or 0x00 for the fp4 kernel) and its genotype counts — the load's lcounts (P parts; the loaders keep 1) plus the last byte's individual
 // pairs — to counts3[3 j + k] (one thread per row; no pass over the rows)
 hipError_t launch_tail_counts(uint8_t* img, const uint8_t* last, int n_snp, int nb, int row_bytes, uint32_t tail_keep,
                               uint32_t pad, const int* lcounts, int P, int* counts3, hipStream_t st);

@@ -135,7 +135,7 @@ __device__ __forceinline__ uint32_t swap_hom(uint32_t v) {  // 00 <-> 11 in ever
 // one wave per row (4 per workgroup): flip[row0 + r] and the row's missing-flag word cleared
 __global__ void __launch_bounds__(256) load_orient_kernel(const uint8_t* __restrict__ src, int nb, int row0, int n_rows,
                                                           int orient, uint8_t* __restrict__ flip,
-                                                          uint32_t* __restrict__ miss_flags) {
+                                                          uint32_t* __restrict__ miss_flags, int* __restrict__ lcounts) {
     const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (r >= n_rows) return;
     int c0 = 0, c1 = 0, c2 = 0;
@@ -157,6 +157,7 @@ __global__ void __launch_bounds__(256) load_orient_kernel(const uint8_t* __restr
             c2 += __shfl_xor(c2, o, 64);
         }
     }
+    if (lane < 3) lcounts[3 * (size_t)(row0 + r) + lane] = 0;  // (the tiled kernel's parts add into them)
     if (lane == 0) {
         flip[row0 + r] = (uint8_t)(c2 > c0);
         miss_flags[row0 + r] = 0u;
@@ -258,16 +259,17 @@ __global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restri
     cnt[1] += n_hi - n_and;
     cnt[2] += n_and;
     if (miss_or) mflags |= 3u;
-    // rows' counts of this part (block_row_sums: the lane pair, then the four waves) to lcounts[(part n_snp + j) 3 + k]
+    // rows' counts of this part (block_row_sums: the lane pair, then the four waves) added into lcounts[3 j + k]
+    // (integer atomics: exact in any order; a separate pass folding P per-part copies cost 0.15 ms at C3)
     {
         int tot[3];
         block_row_sums(red, cnt, tot);
         const int jj = row0 + 32 * bl + threadIdx.x;
         if (threadIdx.x < 32 && 32 * bl + (int)threadIdx.x < n_rows && jj < n_snp) {
-            int* o = lcounts + ((size_t)part * n_snp + jj) * 3;
-            o[0] = tot[0];
-            o[1] = tot[1];
-            o[2] = tot[2];
+            int* o = lcounts + (size_t)jj * 3;
+            atomicAdd(o, tot[0]);
+            atomicAdd(o + 1, tot[1]);
+            atomicAdd(o + 2, tot[2]);
         }
     }
     // rows' flags: the lane pair, then the four waves, then one atomic per row and workgroup
@@ -2770,9 +2772,13 @@ __global__ void __launch_bounds__(256) synth_bed_kernel(uint8_t* __restrict__ ro
 // launchers
 // ------------------------------------------------------------------------------------------
 int load_parts(int n_snp, int row_bytes) {
-    // parts per block: about 16 k workgroups over the whole image, at least 8 chunks each
+    // parts per block: about 64 k workgroups over the whole image, at least 8 chunks each
     const int n_ch = row_bytes >> 5, nblk_img = (n_snp + 31) / 32;
-    return std::max(1, std::min(std::max(n_ch / 8, 1), (16384 + nblk_img - 1) / nblk_img));
+    // (~64 k workgroups: the load of a C3 image 2.72 ms at 16 k, 2.53-2.57 ms from 48 k to 96 k, 2.65 ms at 128 k —
+    // short uniform workgroups, so the count sets how much of the last wave of them idles:
+    // profiles/r05_ab_load_parts.json)
+    constexpr int target = 65536;
+    return std::max(1, std::min(std::max(n_ch / 8, 1), (target + nblk_img - 1) / nblk_img));
 }
 
 hipError_t launch_load_slice(const uint8_t* src, int nb, int row0, int n_rows, int n_snp, uint8_t* img, int row_bytes,
@@ -2781,7 +2787,7 @@ hipError_t launch_load_slice(const uint8_t* src, int nb, int row0, int n_rows, i
     if (n_rows <= 0) return hipSuccess;
     if (row0 % 32 != 0 || row0 + n_rows > n_snp) return hipErrorInvalidValue;
     hipLaunchKernelGGL(load_orient_kernel, dim3((n_rows + 3) / 4), dim3(256), 0, st, src, nb, row0, n_rows,
-                       orient ? 1 : 0, flip, miss_flags);
+                       orient ? 1 : 0, flip, miss_flags, lcounts);
     const int nblk = (n_rows + 31) / 32, P = load_parts(n_snp, row_bytes);
     hipLaunchKernelGGL(load_tiled_kernel, dim3(nblk * P), dim3(256), 0, st, src, nb, row0, n_rows, n_snp, img,
                        row_bytes, P, flip, last, keep_compat, keep_strict, miss_flags, lcounts);
