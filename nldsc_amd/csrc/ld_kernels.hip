@@ -2268,13 +2268,29 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
                 rb[k][c] = sh.stage[t % S][cs + k][c][lane];
             }
     };
+    // Two named fragment sets (F, G): the next K step's four strips are decoded while the current step's MFMAs issue —
+    // across the stage boundary too: the next stage's first step is decoded from its registers (read from LDS a stage
+    // ahead) during the current stage's last step, so after the barrier the MFMAs start at once
     auto kloop = [&](auto ACTc) {
         constexpr bool ACT = decltype(ACTc)::value;
         uint4 ra[2][2], rb[2][2];
         wait_vmcnt<4 * (S - 1)>();  // stage 0 landed (this wave's loads)
         __builtin_amdgcn_s_barrier();  // every wave's
         asm volatile("" ::: "memory");
-        if constexpr (ACT) read_stage(0, ra, rb);
+        F4Frag FA[2], FB[2], GA[2], GB[2];
+        auto dec = [&](F4Frag (&A)[2], F4Frag (&B)[2], const uint4 (&xa)[2][2], const uint4 (&xb)[2][2], int c,
+                       bool hi) __attribute__((always_inline)) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                A[k] = hi ? decode_f4<false>(xa[k][c].z, xa[k][c].w) : decode_f4<false>(xa[k][c].x, xa[k][c].y);
+                B[k] = hi ? decode_f4<false>(xb[k][c].z, xb[k][c].w) : decode_f4<false>(xb[k][c].x, xb[k][c].y);
+            }
+        };
+        if constexpr (ACT) {
+            read_stage(0, ra, rb);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            dec(FA, FB, ra, rb, 0, false);
+        }
         for (int t = 0; t < n_st; ++t) {
             wait_vmcnt<4 * (S - 2)>();  // this wave's loads of stage t + 1 have landed
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // its reads of stage t are in registers
@@ -2285,22 +2301,15 @@ __global__ void __launch_bounds__(256, 1) band_f4_q_kernel(
                 uint4 na[2][2], nb[2][2];
                 read_stage(t + 1, na, nb);  // past the last stage: a buffer of surplus bytes, never used
                 __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    F4Frag A[2], B[2];
-#pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        A[k] = decode_f4<false>(ra[k][c].x, ra[k][c].y);
-                        B[k] = decode_f4<false>(rb[k][c].x, rb[k][c].y);
-                    }
-                    q_step<DOM>(A, B, g0, g1, g2);
-#pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        A[k] = decode_f4<false>(ra[k][c].z, ra[k][c].w);
-                        B[k] = decode_f4<false>(rb[k][c].z, rb[k][c].w);
-                    }
-                    q_step<DOM>(A, B, g0, g1, g2);
-                }
+                dec(GA, GB, ra, rb, 0, true);
+                q_step<DOM>(FA, FB, g0, g1, g2);  // chunk 0, words 0-1
+                dec(FA, FB, ra, rb, 1, false);
+                q_step<DOM>(GA, GB, g0, g1, g2);  // chunk 0, words 2-3
+                dec(GA, GB, ra, rb, 1, true);
+                q_step<DOM>(FA, FB, g0, g1, g2);  // chunk 1, words 0-1
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the next stage's registers
+                dec(FA, FB, na, nb, 0, false);  // (the next stage's first step)
+                q_step<DOM>(GA, GB, g0, g1, g2);  // chunk 1, words 2-3
 #pragma unroll
                 for (int k = 0; k < 2; ++k)
 #pragma unroll

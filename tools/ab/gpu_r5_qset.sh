@@ -1,5 +1,5 @@
 #!/bin/bash
-# Quad kernel stages alternating two register sets (no per-stage copies): quad / routing GPU tests, then a same-box C5
+# Quad kernel variant (see the tag): quad / routing GPU tests, then a same-box C5
 # A/B against the fenced build (r5_fence), two orders
 # (gpurun --timeout 1200 -- bash tools/ab/gpu_r5_qset.sh <tag>)
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
