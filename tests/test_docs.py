@@ -21,3 +21,31 @@ def test_cited_tools_exist():
     refs = set(re.findall(r"\btools/[A-Za-z0-9_/.\-]+\.(?:py|sh|hip)", _text()))
     missing = sorted(r for r in refs if not os.path.exists(os.path.join(REPO, r)))
     assert refs and not missing, missing
+
+
+def _latest_bench_c3():
+    files = sorted(f for f in os.listdir(os.path.join(REPO, "profiles")) if re.fullmatch(r"r0\d_bench_c3\.json", f))
+    assert files, "no profiles/r0N_bench_c3.json"
+    with open(os.path.join(REPO, "profiles", files[-1])) as fh:
+        lines = [ln for ln in fh.read().splitlines() if ln.startswith("{")]
+    import json
+    return files[-1], json.loads(lines[-1])
+
+
+def test_readme_headline_matches_latest_bench_line():
+    """The README's headline sentence quotes the newest committed C3 bench line (verdict r04: the README's figures
+    drifted from the measured ones): the file it cites is the latest profiles/r0N_bench_c3.json, and the ms per run,
+    the SNP-pairs/s and the fraction of the fp4 MFMA peak it quotes are that line's, to the digits printed."""
+    name, d = _latest_bench_c3()
+    text = open(os.path.join(REPO, "README.md")).read()
+    m = re.search(r"Headline \(profiles/(r0\d_bench_c3\.json)\): ([0-9.]+) ms per run, ([0-9.]+) G SNP-pairs/s, "
+                  r"([0-9.]+) of the dense fp4 MFMA peak", text)
+    assert m, "README headline sentence missing"
+    assert m.group(1) == name, (m.group(1), name)
+    ms, gps, frac = m.group(2), m.group(3), m.group(4)
+    def same(quoted, value):
+        digits = len(quoted.split(".")[1]) if "." in quoted else 0
+        return abs(float(quoted) - value) <= 0.5 * 10 ** -digits + 1e-12
+    assert same(ms, d["ms_per_step"]), (ms, d["ms_per_step"])
+    assert same(gps, d["value"] / 1e9), (gps, d["value"] / 1e9)
+    assert same(frac, d["roofline"]["frac"]), (frac, d["roofline"]["frac"])
