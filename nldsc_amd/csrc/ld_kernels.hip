@@ -165,9 +165,10 @@ __global__ void __launch_bounds__(256) load_orient_kernel(const uint8_t* __restr
 }
 
 // grid (block of the slice, part): part p of P sweeps the block's chunks [p n_ch / P, (p + 1) n_ch / P) in stages of
-// LOAD_SC chunks: the workgroup reads the stage's 32 row segments (LOAD_SC x 32 bytes each) row by row — 8 threads per
-// row, 128 contiguous bytes per 8 lanes, whole lines — into LDS, then wave w writes chunks t = t0 + w, t0 + w + 4, ...
-// of the stage (lane l: row l / 2, half l % 2) as whole 1 KiB chunks.  Reading the source 32 bytes per row and chunk
+// LOAD_SC chunks: the workgroup reads the stage's 32 row segments (LOAD_SC x 32 bytes each) row by row — 32 threads per
+// row, 512 contiguous bytes per half wave (8 threads x 128 bytes before: load_tiled 2.64 -> 2.55 ms at C3) — into
+// registers one stage ahead, then through LDS, and wave w writes chunks t = t0 + w, t0 + w + 4, ... of the stage
+// (lane l: row l / 2, half l % 2) as whole 1 KiB chunks (profiles/r05_ab_load_reader.json).  Reading the source 32 bytes per row and chunk
 // straight into the chunk layout touched 32 rows' lines at once per wave: 4.0 TB/s of read + write at C3 (3.16 ms).
 // n_snp: the image's SNPs (rows past it, in its last block: 0x55).  keep_compat / keep_strict: the last byte's bit
 // pairs that are individuals in the reference's / PLINK's sample order.
@@ -208,7 +209,11 @@ __global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restri
         const int u = 2 * t + h, p0 = 16 * u;
         uint4 v = v_in;
         if (fl) v = make_uint4(swap_hom(v.x), swap_hom(v.y), swap_hom(v.z), swap_hom(v.w));
-        *reinterpret_cast<uint4*>(blk + (size_t)t * 1024 + (size_t)i * 32 + 16 * h) = v;
+        // (nontemporal: the image is written once and read by the runs, far past the caches; load_tiled 2.55 ->
+        // 2.46 ms at C3, profiles/r05_ab_load_reader.json)
+        typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w},
+                                    reinterpret_cast<u32x4_t*>(blk + (size_t)t * 1024 + (size_t)i * 32 + 16 * h));
         if (!real) return;
         if (p0 + 16 <= nb - 1) {
             tally(v.x);
@@ -237,21 +242,33 @@ __global__ void __launch_bounds__(256) load_tiled_kernel(const uint8_t* __restri
                 }
         }
     };
-    // the stage reader: thread tid takes row tid / 8 of the block and its units (tid % 8) + 8 k of the stage
-    const int rr = threadIdx.x >> 3, c8 = threadIdx.x & 7;
-    const int gr = 32 * bl + rr;  // (in the slice; rows past it end the image: the last block's padding rows)
-    const size_t gbase = (size_t)gr * nb;
-    for (int t0 = t_lo; t0 < t_hi; t0 += LOAD_SC) {
-        const int nu = 2 * min(LOAD_SC, t_hi - t0);  // units per row this stage
+    // the stage reader: thread tid takes unit tid % TPR of the stage in rows tid / TPR + RPP k of the block (a wave
+    // reads 64 / TPR row segments of 16 TPR contiguous bytes per instruction)
+    constexpr int TPR = 2 * LOAD_SC, RPP = 256 / TPR;
+    const int uu = threadIdx.x % TPR, rr0 = threadIdx.x / TPR;
+    uint4 pre[32 / RPP];  // the next stage's units, read while this stage is written (2.46 -> 2.42 ms at C3)
+    auto fetch = [&](int t0) {
+        const int nu = 2 * min(LOAD_SC, t_hi - t0), u = 2 * t0 + uu;
+        if (uu < nu) {
 #pragma unroll
-        for (int k = 0; k < 2 * LOAD_SC / 8; ++k) {
-            const int uu = c8 + 8 * k, u = 2 * t0 + uu;
-            if (uu < nu)
-                tile[rr][uu] = gr >= n_rows ? make_uint4(0x55555555u, 0x55555555u, 0x55555555u, 0x55555555u)
-                               : u < n_fast ? load16_unaligned(src, gbase + 16 * (size_t)u)
-                                            : load16_bytes(src + gbase, 16 * u, nb, 0x55u);
+            for (int k = 0; k < 32 / RPP; ++k) {
+                const int rr = rr0 + RPP * k, gr = 32 * bl + rr;
+                const size_t gbase = (size_t)gr * nb;
+                pre[k] = gr >= n_rows ? make_uint4(0x55555555u, 0x55555555u, 0x55555555u, 0x55555555u)
+                         : u < n_fast ? load16_unaligned(src, gbase + 16 * (size_t)u)
+                                      : load16_bytes(src + gbase, 16 * u, nb, 0x55u);
+            }
+        }
+    };
+    if (t_lo < t_hi) fetch(t_lo);
+    for (int t0 = t_lo; t0 < t_hi; t0 += LOAD_SC) {
+        const int nu = 2 * min(LOAD_SC, t_hi - t0);
+        if (uu < nu) {
+#pragma unroll
+            for (int k = 0; k < 32 / RPP; ++k) tile[rr0 + RPP * k][uu] = pre[k];
         }
         __syncthreads();
+        if (t0 + LOAD_SC < t_hi) fetch(t0 + LOAD_SC);
         for (int t = t0 + w; t < t0 + nu / 2; t += 4) one(t, tile[i][2 * (t - t0) + h]);
         __syncthreads();
     }

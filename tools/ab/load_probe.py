@@ -14,6 +14,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--loads", type=int, default=5)
     ap.add_argument("--libs", nargs="*", default=[], help="name=path.so builds to alternate (default: the tree's)")
+    ap.add_argument("--shift", type=int, default=0,
+                    help="place the image this many bytes into a fresh buffer (13: its rows start 16-byte aligned)")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
@@ -21,6 +23,12 @@ def main():
     from nldsc_amd.engine import Engine
     M, N = 80_000, 315_599
     buf, pos = synth.device_bed(M, N, seed=7, length_cm=280.0)
+    if a.shift:
+        big = torch.empty(buf.numel() + 64, dtype=torch.uint8, device=buf.device)
+        big[a.shift:a.shift + buf.numel()].copy_(buf)
+        del buf
+        buf = big[a.shift:a.shift + big.numel() - 64]
+        print(f"image at base + {a.shift}: rows at {(buf.data_ptr() + 3) % 16} mod 16", file=sys.stderr)
     libs = dict(x.split("=", 1) for x in a.libs) or {"tree": None}
     engines = {name: Engine(0, lib_path=path) for name, path in libs.items()}
     times = {name: [] for name in libs}
