@@ -140,31 +140,48 @@ def log(*a):
 
 
 def cpu_baseline(bed_host: bytes, n_snp, n_org, w, maf, std_thr, rsq, pos, target_s=15.0):
-    """Time the C port of the reference CPU path on the first K SNPs (K sized for ~target_s)."""
+    """Time the C port of the reference CPU path on the first K SNPs (K sized for ~target_s), on the threads the box
+    gives this job, then on one thread (~target_s / 4).  The host's load average and affinity set are recorded with
+    it: the cores are shared with other jobs, which is what moves this figure between boxes of one CPU model."""
     from oracle import oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    # the cost per SNP grows while the first window fills, so K is sized from the marginal cost
-    # between two prefixes grown geometrically until they take a quarter of the target
-    def timed(k):
-        t = time.perf_counter()
-        r = O.run_c(bed_host, n_snp, n_org, w, maf, std_thr, rsq, pos, end=k, threads=threads)
-        return r, time.perf_counter() - t
-    k_prev, t_prev = 0, 0.0
-    k = min(n_snp, 16)
-    r0, t0 = timed(k)
-    while t0 < target_s / 4 and k < n_snp:
-        k_prev, t_prev = k, t0
-        k = min(n_snp, 3 * k)
+
+    def rate(nth, target):
+        # the cost per SNP grows while the first window fills, so K is sized from the marginal cost
+        # between two prefixes grown geometrically until they take a quarter of the target
+        def timed(k):
+            t = time.perf_counter()
+            r = O.run_c(bed_host, n_snp, n_org, w, maf, std_thr, rsq, pos, end=k, threads=nth)
+            return r, time.perf_counter() - t
+        k_prev, t_prev = 0, 0.0
+        k = min(n_snp, 16)
         r0, t0 = timed(k)
-    if t0 < 0.6 * target_s and k < n_snp:
-        marginal = max((t0 - t_prev) / max(k - k_prev, 1), 1e-6)
-        k = int(min(n_snp, k + (target_s - t0) / marginal))
-        r0, t0 = timed(k)
-    ws = r0["l2_ws"][:k]
-    pairs = float(ws[ws > 0].sum())
+        while t0 < target / 4 and k < n_snp:
+            k_prev, t_prev = k, t0
+            k = min(n_snp, 3 * k)
+            r0, t0 = timed(k)
+        if t0 < 0.6 * target and k < n_snp:
+            marginal = max((t0 - t_prev) / max(k - k_prev, 1), 1e-6)
+            k = int(min(n_snp, k + (target - t0) / marginal))
+            r0, t0 = timed(k)
+        ws = r0["l2_ws"][:k]
+        return k, float(ws[ws > 0].sum()), t0
+
+    load0 = os.getloadavg()
+    k, pairs, t0 = rate(threads, target_s)
+    k1, pairs1, t1 = rate(1, target_s / 4)
+    load1 = os.getloadavg()
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     return dict(value=pairs / t0, unit="SNP-pairs/s", cores=threads, kind="port", cpu_model=cpu_model(),
+                one_thread_value=pairs1 / t1, scaling_over_one_thread=(pairs / t0) / (pairs1 / t1),
+                host_loadavg_1m_before_after=[round(load0[0], 2), round(load1[0], 2)], affinity_cpus=affinity,
+                host_cpus=os.cpu_count(),
                 sample=f"first {k} SNPs of the same chromosome (full sliding window from SNP 0), "
-                       f"{pairs:.0f} pairs in {t0:.2f} s, C port of the reference path (oracle/ldscore_oracle.c: "
+                       f"{pairs:.0f} pairs in {t0:.2f} s on {threads} threads; one thread: first {k1} SNPs, "
+                       f"{pairs1:.0f} pairs in {t1:.2f} s; C port of the reference path (oracle/ldscore_oracle.c: "
                        f"fp32 sdot + per-pair vector copies, OpenMP over neighbours)")
 
 
@@ -321,7 +338,11 @@ def main():
                          "(fp32_path) and the one-shot load + run GPU time (oneshot_gpu_ms)")
     ap.add_argument("--concurrent", type=int, default=3,
                     help="c4: chromosomes computed at once per GPU (host threads, one engine stream each)")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="engine option (nldsc_engine_set_option, include/nldsc_ld.h), repeatable: a study of a "
+                         "non-default schedule, e.g. --option debug_timing=1")
     args = ap.parse_args()
+    args.engine_options = {k: int(v) for k, v in (o.split("=", 1) for o in args.option)}
 
     # --gpus N without a launcher: start the N ranks here (torch.distributed.run in a child process, before
     # anything touches the GPU) and exit with their status; under a launcher, WORLD_SIZE must equal --gpus
@@ -378,7 +399,7 @@ def main():
     overlap = False  # (strong scaling over RCCL: the gather beside the next step, below)
     buf, pos = synth.device_bed(M, N, seed=7 if split else 7 + rank, length_cm=args.length_cm,
                                 missing=args.missing, device=local)
-    eng = Engine(local)
+    eng = Engine(local, options=args.engine_options)
     own = (0, M)
     if split:
         # --split: ONE chromosome position-sharded over the ranks (strong scaling): rank g keeps only its
@@ -610,6 +631,7 @@ def main():
                               "%s, window %g bp, maf %g, std-thr %g, rsq 1/M" %
                               (N, M, args.length_cm / 1e6, "additive only" if args.additive_only else
                                "additive+dominance", w, args.maf, args.std_thr))),
+                **({"engine_options": args.engine_options} if args.engine_options else {}),
                 "n_org": N, "n_snp": M, "mean_window": float(ws[ws > 0].mean()),
                 "pairs_per_step_per_gpu": tims[-1]["pairs"],
                 "parallelism": (f"one chromosome position-sharded over {world} GPUs (owned SNP ranges balanced by "
@@ -677,7 +699,7 @@ def whole_genome(args, world, rank, local, coll):
     t = time.perf_counter()
     for u in mine:
         buf, pos = synth.device_bed(int(Mc[u]), N, seed=100 + u, length_cm=float(L[u]), device=local)
-        e = Engine(local)
+        e = Engine(local, options=args.engine_options)
         e.load_bed_device(buf.data_ptr(), buf.numel(), int(Mc[u]), N)
         del buf
         units.append((u, e, pos))

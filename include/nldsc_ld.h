@@ -194,6 +194,10 @@ int nldsc_engine_band_tail_ksplit(const nldsc_engine* e);
 #define NLDSC_BAND_F4_QUAD 7 /* option t2 = 3: missing-free 4x4 super-items in the quad workgroups (64x64 tiles per
                                 wave), the rest in the single-block kernel */
 int nldsc_engine_band_kernel(const nldsc_engine* e);
+/* Where the last host-result run (nldsc_engine_run) wrote its owned slice: 1 straight into the caller's arrays (all
+ * seven in nldsc_host_alloc buffers, zero copy), 0 through the engine's landing buffer and host copies, -1 no host
+ * result written (device-table runs, empty owned ranges). */
+int nldsc_engine_result_direct(const nldsc_engine* e);
 
 /* Load SNP rows [snp_begin, snp_end) of a .bed file of n_snp_file SNPs as the engine's image
  * (snp_end - snp_begin SNPs; the run then takes the positions of that slice).  Position sharding

@@ -33,6 +33,7 @@ EXPORTED = (
     "nldsc_format_scores", "nldsc_engine_ksplit", "nldsc_engine_band_kernel", "nldsc_engine_band_round_items",
     "nldsc_engine_band_tail_ksplit", "nldsc_engine_run_device", "nldsc_engine_run_device_split",
     "nldsc_engine_run_device_finish", "nldsc_engine_set_option", "nldsc_host_alloc", "nldsc_host_free",
+    "nldsc_engine_result_direct",
 )
 
 
@@ -104,6 +105,8 @@ def lib(path: str | None = None) -> ctypes.CDLL:
             L.nldsc_engine_band_round_items.argtypes = [vp]
         if hasattr(L, "nldsc_engine_band_tail_ksplit"):
             L.nldsc_engine_band_tail_ksplit.argtypes = [vp]
+        if hasattr(L, "nldsc_engine_result_direct"):
+            L.nldsc_engine_result_direct.argtypes = [vp]
         if hasattr(L, "nldsc_engine_run_device"):
             L.nldsc_engine_run_device.argtypes = [vp, ctypes.POINTER(Params), ctypes.c_int32, ctypes.c_int32, vp,
                                                   ctypes.c_int32] + c_err

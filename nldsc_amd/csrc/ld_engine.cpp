@@ -257,7 +257,7 @@ struct nldsc_engine {
     hipStream_t plan_stream = nullptr;  // the GPU schedule runs here, beside the count kernel
     hipEvent_t ev_pos = nullptr;        // positions uploaded and their window edges searched (the schedule's input)
     hipEvent_t ev[6] = {};
-    hipEvent_t ev_dbg[2] = {};  // $NLDSC_DEBUG_TIMING: after the super-item launch, before the single-block launches
+    hipEvent_t ev_dbg[2] = {};  // option debug_timing: after the super-item launch, before the single-block launches
     bool debug_timing = false;
     hipEvent_t ev_plan = nullptr;  // GPU plan counters landed in h_meta
     hipEvent_t ev_stats = nullptr;   // SNP constants and replay flags written (the replay's inputs)
@@ -312,6 +312,7 @@ struct nldsc_engine {
     size_t rep_gram_max_slots = (size_t)1 << 16;
     int last_ksplit = 1;
     int last_round_items = 0;
+    int last_direct = -1;  // nldsc_engine_result_direct
     int last_tail_ksplit = 1;
     // fp4 band kernels on the GPU plan (option "t2"): 3 (default) missing-free 4 x 4 super-items in the quad
     // workgroups (64 x 64 tiles per wave), the rest in the single-block kernel (C5 slice band -25 % against 1, the
@@ -483,7 +484,27 @@ int nldsc_device_count(void) {
     return n;
 }
 
+// The environment knobs of rounds 1-4 ($NLDSC_T2, $NLDSC_BAND_MODE, ...) became engine options
+// (nldsc_engine_set_option) in round 5; a process that still sets one is told once, on stderr, which option replaces
+// it instead of silently running the defaults.
+static void warn_legacy_env_once() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        static const char* const legacy[][2] = {
+            {"NLDSC_BAND_MODE", "band_mode"}, {"NLDSC_GPU_PLAN", "gpu_plan"},   {"NLDSC_ORIENT", "orient"},
+            {"NLDSC_KSPLIT", "ksplit"},       {"NLDSC_T2", "t2"},               {"NLDSC_BAND_ROUNDS", "band_rounds"},
+            {"NLDSC_F4_NC2", "f4_nc2"},       {"NLDSC_Q_ROUNDS", "q_rounds"},   {"NLDSC_DEFER_REP", "defer_rep"},
+            {"NLDSC_DEBUG_TIMING", "debug_timing"}, {"NLDSC_QUAD_ADD", nullptr}, {"NLDSC_REPLAY_OVERLAP", nullptr}};
+        for (const auto& kv : legacy)
+            if (std::getenv(kv[0]))
+                std::fprintf(stderr, "nldsc_amd: $%s is no longer read; %s%s%s\n", kv[0],
+                             kv[1] ? "use the engine option \"" : "the study mode it selected was removed",
+                             kv[1] ? kv[1] : "", kv[1] ? "\" (nldsc_engine_set_option / Engine(options=...))" : "");
+    });
+}
+
 int nldsc_engine_create(int32_t device, nldsc_engine** out, char* err, size_t errlen) {
+    warn_legacy_env_once();
     if (!out) return set_err(err, errlen, NLDSC_E_ARG, "out is NULL");
     *out = nullptr;
     int d = 0;
@@ -656,8 +677,8 @@ int nldsc_engine_load_bed_file_range(nldsc_engine* e, const char* path, int32_t 
     // Rows stream through T reader threads, each with its own pinned slot (~32 MiB of whole rows), device staging slot
     // and stream: thread t reads slices t, t + T, ... with pread (several reads in flight: the page cache copies and
     // the device's queue run in parallel, where one fread loop held the load to one core's memcpy rate), then queues
-    // the slice's H2D copy and the kernel that places its rows (load_rows_kernel), and waits for both before it reuses
-    // the slot.  Slices are independent (each names its rows), so their order does not matter.
+    // the slice's H2D copy and the kernels that place its rows (load_slice), and waits for both before it reuses the
+    // slot.  Slices are independent (each names its rows), so their order does not matter.
     const int fd = fileno(f);
     // (slices of whole 32-SNP blocks: load_slice)
     const size_t rows_per = std::max<size_t>(32, (size_t(32) << 20) / nb / 32 * 32), CH = rows_per * nb;
@@ -785,6 +806,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         e->last_ksplit = 1;
         e->last_tail_ksplit = 1;
         e->last_round_items = 0;
+        e->last_direct = -1;
         e->last_band_kernel = NLDSC_BAND_F4;
         if (table_dev) {
             HIPCHK(hipSetDevice(e->device));
@@ -812,6 +834,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     unsigned long long* wsum_h = nullptr;
     unsigned long long* wsum_d = nullptr;
     const int n_wsum = nldsc::finalize_out_blocks(n_own);
+    e->last_direct = -1;
     if (host_out) {
         const size_t o = (size_t)own_begin, wsum_off = (4 * b8 + 3 * b4 + 7) / 8 * 8;
         HIPCHK(e->h_res.ensure(wsum_off + 2 * sizeof(unsigned long long) * (size_t)n_wsum));
@@ -830,6 +853,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         reg.wsd = static_cast<int32_t*>(registered_device_ptr(callers.wsd, b4));
         reg.wsde = static_cast<int32_t*>(registered_device_ptr(callers.wsde, b4));
         direct = reg.l2 && reg.l2d && reg.maf && reg.rstd && reg.wsa && reg.wsd && reg.wsde;
+        e->last_direct = direct ? 1 : 0;
         if (direct) {
             out_h = callers;
             out_d = reg;
@@ -1232,7 +1256,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                                      e->Lw.p, e->Rw.p, e->sflags.p, M, p->ld_wind, (double)N, p->rsq_thr, own_begin,
                                      flush_hi, e->l2_acc.p, e->l2d_acc.p, e->ws_acc.p, true, blk_rep, which, st);
     };
-    const bool run_single = !use_t2 || routed;  // ($NLDSC_T2=2: every block pair in the 2 x 2 workgroups)
+    const bool run_single = !use_t2 || routed;  // (option t2 = 2: every block pair in the 2 x 2 workgroups)
     if (n_items > 0 && (use_f4 || use_i8)) {
         if (use_t2) HIPCHK(launch_super(1));
         if (e->debug_timing) HIPCHK(hipEventRecord(e->ev_dbg[0], st));
@@ -1482,6 +1506,8 @@ int nldsc_engine_ksplit(const nldsc_engine* e) { return e ? e->last_ksplit : NLD
 int nldsc_engine_band_round_items(const nldsc_engine* e) { return e ? e->last_round_items : NLDSC_E_ARG; }
 int nldsc_engine_band_tail_ksplit(const nldsc_engine* e) { return e ? e->last_tail_ksplit : NLDSC_E_ARG; }
 int nldsc_engine_band_kernel(const nldsc_engine* e) { return e ? e->last_band_kernel : NLDSC_E_ARG; }
+
+int nldsc_engine_result_direct(const nldsc_engine* e) { return e ? e->last_direct : NLDSC_E_ARG; }
 
 int nldsc_ld_calculate(const nldsc_ld_params* p, nldsc_ld_result* r, char* err, size_t errlen) {
     if (!p || !r || !p->bedfile) return set_err(err, errlen, NLDSC_E_ARG, "NULL argument");

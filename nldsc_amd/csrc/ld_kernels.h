@@ -136,9 +136,10 @@ hipError_t launch_band_f4_split(bool dom, int P, int n_items, const uint32_t* ge
 // as meta; counts2 capacity ceil(nblk2/16)^2) and launch_plan_emit_super; the kernel reads `rows` (nblk) to skip the
 // block pairs the single-block plan does not hold
 constexpr int T2_STAGES = 4;  // LDS ring stages (2 chunks each) of band_f4_t2_kernel
-// shift 1: 2 x 2 super-items (16 x 16 tiles); shift 2: the quad kernel's 4 x 4 super-items in 32-item groups of 4
-// super-rows x 8 offsets, padded with null items (I, J, 0, -1) to exactly 32 (one XCD's share of a round launch);
-// counts2 capacity: plan_super_counts(n, shift)
+// shift 1: 2 x 2 super-items (16 x 16 tiles); shift 2: the quad kernel's 4 x 4 super-items in row groups of 4
+// super-rows, each group's items by diagonal offset then super-row (plan_qemit_kernel), NOT padded: a group's item
+// count varies and the list is dense (null padding to 32-item groups held wave slots: r05_ab_quad_groups.json), so
+// nothing may assume 32-aligned groups; counts2 capacity: plan_super_counts(n, shift)
 int plan_super_counts(int n, int shift);
 hipError_t launch_plan_super(int n, const int2* rows, int2* rows2, int* counts2, int* meta2, int shift, hipStream_t st);
 hipError_t launch_plan_emit_super(int n, const int2* rows2, const int* meta2, const int* offsets2, int4* items2,

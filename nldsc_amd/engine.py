@@ -178,7 +178,9 @@ class Engine:
                  band_round_items=(self._L.nldsc_engine_band_round_items(self._h)
                                    if hasattr(self._L, "nldsc_engine_band_round_items") else 0),
                  band_tail_ksplit=(self._L.nldsc_engine_band_tail_ksplit(self._h)
-                                   if hasattr(self._L, "nldsc_engine_band_tail_ksplit") else 1))
+                                   if hasattr(self._L, "nldsc_engine_band_tail_ksplit") else 1),
+                 result_direct=(self._L.nldsc_engine_result_direct(self._h)
+                                if hasattr(self._L, "nldsc_engine_result_direct") else -1))
         return d
 
 

@@ -81,3 +81,17 @@ def test_product_never_imports_the_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h")):
                 text = open(os.path.join(root, f), errors="replace").read()
                 assert "oracle" not in re.sub(r"(#|//).*", "", text).lower().replace("oracle-free", ""), f
+
+
+def test_legacy_environment_knobs_are_reported():
+    """The round 1-4 environment knobs are engine options now (nldsc_engine_set_option); setting one warns once on
+    stderr when an engine is created (with or without a GPU) instead of being ignored silently."""
+    import sys
+    code = ("from nldsc_amd import engine\n"
+            "for _ in range(2):\n"
+            "    try:\n        engine.Engine(0).close()\n    except RuntimeError:\n        pass\n")
+    env = dict(os.environ, NLDSC_T2="1", NLDSC_BAND_MODE="0")
+    p = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert p.stderr.count('$NLDSC_T2 is no longer read; use the engine option "t2"') == 1, p.stderr
+    assert p.stderr.count('"band_mode"') == 1, p.stderr
