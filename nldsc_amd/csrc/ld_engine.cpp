@@ -940,28 +940,16 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     // Model: a round of items takes ~0.67 us per K chunk (C3: 2 466 chunks, 1.65 ms per round, 12.7 rounds in
     // 20.9 ms); the split adds ~64 KiB of partial-tile traffic per piece at ~3 TB/s effective (measured: a 1/8
     // shard of C3, 3 300 items, band 3.35 -> 3.01 ms; a 1/2 shard, 13 000 items, P = 5 made it 7.5 % slower).
-#ifndef NLDSC_ROUND_MIN_IT  // (A/B study: round launches for shorter rows, several rounds per launch)
-#define NLDSC_ROUND_MIN_IT 1024
-#endif
-#ifndef NLDSC_ROUND_MULT
-#define NLDSC_ROUND_MULT 1
-#endif
-#ifndef NLDSC_KSPLIT_PMAX
-#define NLDSC_KSPLIT_PMAX 8
-#endif
-#ifndef NLDSC_KSPLIT_TRAFFIC
-#define NLDSC_KSPLIT_TRAFFIC 1.0
-#endif
     auto choose_ksplit = [&](int n_items) {
         int ksplit = 1;
         if (use_f4 && !nc2 && n_items > 0 && n_it <= nldsc::F4_SEG_CHUNKS && e->ksplit_ok) {
             const double slots = 8.0 * (double)e->n_cu, t_round = 0.67e-6 * n_it;
             auto cost = [&](int P) {
                 return std::ceil((double)n_items * P / slots) / P * t_round +
-                       (P > 1 ? NLDSC_KSPLIT_TRAFFIC * n_items * P * 65536.0 / 3e12 : 0.0);
+                       (P > 1 ? n_items * P * 65536.0 / 3e12 : 0.0);
             };
             double best = cost(1);
-            for (int P = 2; P <= NLDSC_KSPLIT_PMAX && 2 * P <= n_it; ++P)
+            for (int P = 2; P <= 8 && 2 * P <= n_it; ++P)
                 if (cost(P) < 0.97 * best && (size_t)n_items * P * 32768 <= ((size_t)3 << 30)) {
                     best = cost(P);
                     ksplit = P;
@@ -1200,7 +1188,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     bool defer = replay && e->defer_rep && use_f4 && ksplit == 1 && n_it <= nldsc::F4_SEG_CHUNKS;
     auto size_single = [&]() -> hipError_t {
         round_items = use_f4 && ksplit == 1 && e->band_rounds && n_it <= nldsc::F4_SEG_CHUNKS &&
-                      n_it >= NLDSC_ROUND_MIN_IT && n_single >= e->round_min * slots ? NLDSC_ROUND_MULT * slots : 0;
+                      n_it >= 1024 && n_single >= e->round_min * slots ? slots : 0;
         const int tail = round_items > 0 ? n_single % round_items : 0;
         tail_p = tail > 0 ? choose_ksplit(tail) : 1;
         n_full = tail_p > 1 ? n_single - tail : n_single;

@@ -730,9 +730,6 @@ __global__ void __launch_bounds__(64) reference_residual_kernel(const uint8_t* _
 #pragma clang fp contract(off)
     const int j = blockIdx.x;
     if (j >= n_snp || !replayed_snp(counts, flip, sflags, j)) return;
-#ifdef NLDSC_REPLAY_PRIO  // (A/B study: the replay's dependent sums ahead of the band waves sharing its SIMD)
-    __builtin_amdgcn_s_setprio(NLDSC_REPLAY_PRIO);
-#endif
     const int s0 = counts[4 * (size_t)j], c1 = counts[4 * (size_t)j + 1], s2 = counts[4 * (size_t)j + 2];
     const bool fj = flip != nullptr && flip[j];
     const int c0 = fj ? s2 : s0, c2 = fj ? s0 : s2;
@@ -1926,9 +1923,6 @@ __global__ void __launch_bounds__(64, WPS) band_f4_kernel(const uint32_t* __rest
                                                         const uint8_t* __restrict__ blk_miss, int route_shift,
                                                         float* __restrict__ rep_gram, int4* __restrict__ rep_items,
                                                         int* __restrict__ rep_count) {
-#ifdef NLDSC_BAND_PRIO_PARITY  // (A/B study: static VALU priority for half of the waves)
-    if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
-#endif
     __shared__ BandI8Lds sh;
     __shared__ float tr[32 * 33];
     auto item = [&](const int4 it) __attribute__((always_inline)) {  // (not a call: the body's registers stay live)
