@@ -94,6 +94,7 @@ void nldsc_engine_destroy(nldsc_engine* e);
  * name or a value out of range.  Defaults in brackets.
  *   band_mode    default correlation path when a run's flags name none: 0 fp32, 1 exact int8, [2] exact fp4
  *   gpu_plan     [1] band schedule on the GPU for sorted non-negative positions; 0 the host replay always
+ *   plan_fused   [1] that schedule in one launch (items included) for slices of <= 32768 SNPs; 0 the kernel chain
  *   orient       [1] store rows minor-homozygote-as-00 at load (the exact kernels' operands mostly zero)
  *   ksplit       [1] K-split small launches (a rank's shard of one chromosome)
  *   t2           super-item kernels for missing-free blocks: 0 none, 1 2x2 routed, 2 2x2 for all, [3] 4x4 quad

@@ -355,6 +355,9 @@ struct nldsc_engine {
     HostPinned h_route;    // their count
     hipEvent_t ev_route = nullptr;
     bool gpu_plan = true;  // band schedule on the GPU for non-negative sorted positions (option "gpu_plan" 0: host)
+    // slices of at most PLAN_SMALL_N SNPs (a rank's shard): the GPU schedule in one fused launch, items included
+    // (option "plan_fused" 0: the kernel chain of long slices)
+    bool plan_fused = true;
     // timings of the last run
     double ms[6] = {0, 0, 0, 0, 0, 0};
     double flop_alg = 0, flop_issued = 0, pairs = 0, ops_alg_i8 = 0;
@@ -551,6 +554,7 @@ int nldsc_engine_set_option(nldsc_engine* e, const char* name, int64_t value, ch
     const Opt opts[] = {
         {"band_mode", 0, 2, [&](int64_t v) { e->band_mode = (int)v; }},
         {"gpu_plan", 0, 1, [&](int64_t v) { e->gpu_plan = v != 0; }},
+        {"plan_fused", 0, 1, [&](int64_t v) { e->plan_fused = v != 0; }},
         {"orient", 0, 1, [&](int64_t v) { e->orient = v != 0; }},
         {"ksplit", 0, 1, [&](int64_t v) { e->ksplit_ok = v != 0; }},
         {"t2", 0, 3, [&](int64_t v) { e->t2_mode = (int)v; }},
@@ -960,6 +964,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     int ksplit = 1;
     bool use_t2 = false;
     int n_items2 = 0;
+    const bool fused_plan = gpu_plan && e->plan_fused && M <= nldsc::PLAN_SMALL_N;
     if (gpu_plan) {
         const size_t n_t = (size_t)(nblk + 15) / 16;
         // window edges A | E, then the right-pointer scan's tile maxima
@@ -968,6 +973,7 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
         HIPCHK(e->plan_counts.ensure(n_t * n_t));
         HIPCHK(e->plan_meta.ensure(8));  // [0, 4) single-block plan, [4, 8) super-item plan
         HIPCHK(e->h_meta.ensure(8 * sizeof(int)));
+        if (fused_plan) HIPCHK(e->items.ensure(nldsc::plan_small_items(M)));  // (emitted with the plan)
         if (t2_cand) {
             const size_t nblk2 = (size_t)(nblk + 1) / 2, n_t2 = (nblk2 + 15) / 16;
             HIPCHK(e->plan_rows2.ensure(nblk2));
@@ -1000,7 +1006,8 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
     if (gpu_plan) {
         HIPCHK(hipStreamWaitEvent(e->plan_stream, e->ev_pos, 0));
         HIPCHK(nldsc::launch_plan(M, own_begin, own_end, e->Aw.p, e->Aw.p + M, e->Rw.p, e->plan_rows.p,
-                                  e->plan_counts.p, e->plan_meta.p, e->plan_stream, nc2));
+                                  e->plan_counts.p, e->plan_meta.p, e->plan_stream, nc2,
+                                  fused_plan ? e->items.p : nullptr));
         if (t2_cand)
             HIPCHK(nldsc::launch_plan_super(M, e->plan_rows.p, e->plan_rows2.p, e->plan_counts2.p, e->plan_meta.p + 4,
                                             route_shift,
@@ -1086,8 +1093,8 @@ int run_impl(nldsc_engine* e, const nldsc_ld_params* p, int32_t own_begin, int32
                                                  e->items2.p, route_shift, ps));
         }
         if (!use_t2 || routed) {
-            HIPCHK(e->items.ensure(std::max<size_t>((size_t)n_items, 1)));
-            if (n_items > 0)
+            HIPCHK(e->items.ensure(std::max<size_t>((size_t)n_items, 1)));  // (fused: already holds them)
+            if (n_items > 0 && !fused_plan)
                 HIPCHK(nldsc::launch_plan_emit(M, e->plan_rows.p, e->plan_meta.p, e->plan_counts.p, e->items.p, ps,
                                                nc2));
         }

@@ -88,8 +88,15 @@ hipError_t launch_plan_edges(const double* pos, int n, double w, int* A, int* E,
 // ceil(nblk/16) * ceil(nblk/16)); meta[1] = items, meta[2] = diagonal items (read after the stream
 // reaches it), then plan_emit writes the items (16 row blocks x 16 offsets tile order).  pair: items of two
 // neighbouring column blocks (I, J, 2) (the additive-only fp4 kernel's 32 x 64 tiles; a row's odd last one (I, J, 1))
+// small_items (n <= PLAN_SMALL_N): the whole plan in one workgroup, the items emitted too (capacity: every block pair
+// I <= J, plan_small_items); launch_plan_emit is then not called
+constexpr int PLAN_SMALL_N = 32768;
+inline size_t plan_small_items(int n) {
+    const size_t nblk = (size_t)(n + 31) / 32;
+    return nblk * (nblk + 1) / 2;
+}
 hipError_t launch_plan(int n, int own_lo, int own_hi, const int* A, int* E, int* R, int2* rows, int* counts, int* meta,
-                       hipStream_t st, bool pair = false);
+                       hipStream_t st, bool pair = false, int4* small_items = nullptr);
 hipError_t launch_plan_emit(int n, const int2* rows, const int* meta, const int* offsets, int4* items, hipStream_t st,
                             bool pair = false);
 hipError_t launch_band(bool dom, int wps, int n_items, const uint32_t* geno, int pitch_words, int n_it,

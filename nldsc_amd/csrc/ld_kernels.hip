@@ -1000,6 +1000,108 @@ __global__ void plan_emit_kernel(const int2* __restrict__ rows, int nblk, const 
     }
 }
 
+// The whole schedule of a short slice in one workgroup (n <= PLAN_SMALL_N: a rank's shard of a chromosome): the right
+// pointers (plan_tile_max / tile_scan / right), the row ranges (plan_rows), the tile counts and their scan (plan_count /
+// plan_scan) and the items (plan_emit) — the same values, in one launch instead of seven on the critical path of a
+// ~2.5 ms run (each a few us of work behind ~5-20 us of launch latency).  Row ranges and tile counts stay in LDS between
+// the phases; `items` must hold every block pair I <= J (the count is known only here).
+constexpr int PLAN_SMALL_WG = 1024;
+template <bool MAX>
+__device__ __forceinline__ int small_scan_excl(int v, int id, int* part, int& total) {
+    const int t = threadIdx.x;
+    part[t] = v;
+    __syncthreads();
+    for (int o = 1; o < PLAN_SMALL_WG; o <<= 1) {
+        const int u = t >= o ? part[t - o] : id;
+        __syncthreads();
+        part[t] = MAX ? max(part[t], u) : part[t] + u;
+        __syncthreads();
+    }
+    total = part[PLAN_SMALL_WG - 1];
+    const int ex = t > 0 ? part[t - 1] : id;
+    __syncthreads();
+    return ex;
+}
+__global__ void __launch_bounds__(PLAN_SMALL_WG) plan_small_kernel(const int* __restrict__ A, const int* __restrict__ E,
+                                                                   int n, int own_lo, int own_hi, int* __restrict__ R,
+                                                                   int2* __restrict__ rows, int* __restrict__ counts,
+                                                                   int* __restrict__ meta, int4* __restrict__ items,
+                                                                   int pair) {
+    constexpr int MAX_BLK = PLAN_SMALL_N / 32, MAX_TILES = ((MAX_BLK + 15) / 16) * ((MAX_BLK + 15) / 16);
+    __shared__ int part[PLAN_SMALL_WG];
+    __shared__ int2 srows[MAX_BLK];
+    __shared__ int scnt[MAX_TILES];
+    __shared__ int s_maxd, s_diag;
+    const int t = threadIdx.x, nblk = (n + 31) / 32;
+    if (t == 0) { s_maxd = 0; s_diag = 0; }
+    {  // R_k = min(n - 1, k + max_{j <= k} (E_j - j)): a chunked max-scan
+        const int per = (n + PLAN_SMALL_WG - 1) / PLAN_SMALL_WG, b = min(n, t * per), e = min(n, b + per);
+        int acc = INT_MIN;
+        for (int k = b; k < e; ++k) acc = max(acc, E[k] - k);
+        int total;
+        int run = small_scan_excl<true>(acc, INT_MIN, part, total);
+        for (int k = b; k < e; ++k) {
+            run = max(run, E[k] - k);
+            R[k] = min(n - 1, k + run);
+        }
+    }
+    for (int I = t; I < nblk; I += PLAN_SMALL_WG) {  // as plan_rows_kernel
+        int2 r = make_int2(1, 0);
+        if (I >= A[own_lo] / 32 && I * 32 < own_hi) {
+            const int i_end = min(n, 32 * I + 32) - 1;
+            const int Jmax = min(nblk - 1, (E[i_end] - 1) / 32);
+            const int ob0 = own_lo / 32, ob1 = (own_hi - 1) / 32;
+            const bool own_row = I >= ob0 && I <= ob1;
+            const int J0 = own_row ? I : max(I, ob0), J1 = own_row ? Jmax : min(Jmax, ob1);
+            r = make_int2(J0 - I, J1 - I);
+        }
+        srows[I] = r;
+        rows[I] = r;
+        if (r.x <= r.y) {
+            atomicMax(&s_maxd, r.y + 1);
+            if (r.x == 0) atomicAdd(&s_diag, 1);
+        }
+    }
+    __syncthreads();
+    const int n_t = (nblk + PLAN_R - 1) / PLAN_R, n_c = (s_maxd + PLAN_C - 1) / PLAN_C, nk = n_t * n_c;
+    auto tile = [&](int k, auto&& emit) {  // the items of tile (T, c), row by row (plan_count / plan_emit)
+        const int T = k / n_c, c = k % n_c;
+        for (int I = T * PLAN_R; I < min(nblk, T * PLAN_R + PLAN_R); ++I) {
+            const int a = max(srows[I].x, c * PLAN_C), b = min(srows[I].y, c * PLAN_C + PLAN_C - 1);
+            for (int d = a; d <= b; d += 1 + pair) emit(make_int4(I, I + d, pair ? min(2, b - d + 1) : 1, 0));
+        }
+    };
+    for (int k = t; k < nk; k += PLAN_SMALL_WG) {
+        int cnt = 0;
+        tile(k, [&](int4) { ++cnt; });
+        scnt[k] = cnt;
+    }
+    __syncthreads();
+    int total;
+    {  // exclusive scan of the tile counts in place (LDS)
+        const int per = (nk + PLAN_SMALL_WG - 1) / PLAN_SMALL_WG, b = min(nk, t * per), e = min(nk, b + per);
+        int acc = 0;
+        for (int k = b; k < e; ++k) acc += scnt[k];
+        int run = small_scan_excl<false>(acc, 0, part, total);
+        for (int k = b; k < e; ++k) {
+            const int c = scnt[k];
+            scnt[k] = run;
+            counts[k] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        meta[0] = s_maxd;
+        meta[1] = total;
+        meta[2] = s_diag;
+    }
+    for (int k = t; k < nk; k += PLAN_SMALL_WG) {
+        int o = scnt[k];
+        tile(k, [&](int4 it) { items[o++] = it; });
+    }
+}
+
 // Per-SNP sums across work items: every item adds its partial sums (fp64, per 32-SNP block) as fixed-point
 // integers (2^-44 units; |partial| <= 32, a SNP's total < 2^19) with 64-bit integer atomics, so the total does not
 // depend on the order in which items finish and L2 / L2D are bit-reproducible run to run (fp64 atomics are not).
@@ -2908,9 +3010,15 @@ hipError_t launch_plan_edges(const double* pos, int n, double w, int* A, int* E,
 }
 
 hipError_t launch_plan(int n, int own_lo, int own_hi, const int* A, int* E, int* R, int2* rows, int* counts, int* meta,
-                       hipStream_t st, bool pair) {
+                       hipStream_t st, bool pair, int4* small_items) {
     const int nblk = (n + 31) / 32;
     if (n <= 0 || own_hi <= own_lo) return hipSuccess;  // (meta zeroed by launch_plan_edges)
+    if (small_items != nullptr) {
+        if (n > PLAN_SMALL_N) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(plan_small_kernel, dim3(1), dim3(PLAN_SMALL_WG), 0, st, A, E, n, own_lo, own_hi, R, rows,
+                           counts, meta, small_items, pair ? 1 : 0);
+        return hipGetLastError();
+    }
     const int ntile = (n + PLAN_WG - 1) / PLAN_WG;  // (E holds n + ntile ints: the tiles' maxima after the n edges)
     hipLaunchKernelGGL(plan_tile_max_kernel, dim3(ntile), dim3(PLAN_WG), 0, st, E, n, E + n);
     hipLaunchKernelGGL(plan_tile_scan_kernel, dim3(1), dim3(PLAN_WG), 0, st, E + n, ntile);

@@ -49,3 +49,27 @@ def test_readme_headline_matches_latest_bench_line():
     assert same(ms, d["ms_per_step"]), (ms, d["ms_per_step"])
     assert same(gps, d["value"] / 1e9), (gps, d["value"] / 1e9)
     assert same(frac, d["roofline"]["frac"]), (frac, d["roofline"]["frac"])
+
+
+def _same(quoted: str, value: float) -> bool:
+    digits = len(quoted.split(".")[1]) if "." in quoted else 0
+    return abs(float(quoted) - value) <= 0.5 * 10 ** -digits + 1e-12
+
+
+def test_readme_fp32_and_cpu_figures_match_latest_bench_line():
+    """The README's fp32-path fraction and its CPU-baseline rates (16 threads and one thread) are the newest C3 bench
+    line's, cited by file (verdict r05: the README quoted 74.0 % where the driver measured 73.6 %, and 25-52 k pairs/s
+    where it measured 18.8 k)."""
+    name, d = _latest_bench_c3()
+    text = open(os.path.join(REPO, "README.md")).read()
+    m = re.search(r"\(([0-9.]+) % of the fp32 MFMA peak in\s+profiles/(r0\d_bench_c3\.json)'s `fp32_path` record\)",
+                  text)
+    assert m, "README fp32-path sentence missing"
+    assert m.group(2) == name and _same(m.group(1), 100 * d["fp32_path"]["frac"]), (m.groups(), d["fp32_path"]["frac"])
+    m = re.search(r"ran ([0-9.]+) k pairs/s on (\d+) host threads\s+and ([0-9.]+) k on one thread \(profiles/"
+                  r"(r0\d_bench_c3\.json)", text)
+    assert m, "README CPU-baseline sentence missing"
+    cb = d["cpu_baseline"]
+    assert m.group(4) == name, (m.group(4), name)
+    assert _same(m.group(1), cb["value"] / 1e3) and int(m.group(2)) == cb["cores"], (m.groups(), cb)
+    assert _same(m.group(3), cb["one_thread_value"] / 1e3), (m.group(3), cb["one_thread_value"])
