@@ -1744,6 +1744,34 @@ __device__ __forceinline__ void decode_f4_word(uint32_t w, int& x0, int& x1, int
     }
 }
 
+// decode_f4 with the two words' shifts as 64-bit shifts of (wb:wa): the bits crossing between the words land outside
+// every mask (K6 and M keep nibble bits 1-2 / 1; the crossing bits are 0 of the high word and 30-31 of the low one), so
+// the planes are bitwise decode_f4's, from 3 shifts per word pair instead of 6 (15 VALU instead of 18 with m planes).
+// Used by the additive-only column-pair loop, where it measured C2 band -3 % (profiles/r06_ab_decode64.json); the
+// add+dom single-block loop did not move and the quad kernel (register pairs moved into aligned places) slowed 6 %.
+template <bool WM>
+__device__ __forceinline__ F4Frag decode_f4_64(uint32_t wa, uint32_t wb) {
+    constexpr uint32_t M = 0x22222222u, K6 = 0x66666666u, M4 = 0x44444444u;
+    const uint64_t w = ((uint64_t)wb << 32) | wa;
+    uint64_t s1, s2;  // (the compiler splits a 64-bit shift into v_alignbit + a 32-bit shift: asm keeps one instruction)
+    asm("v_lshlrev_b64 %0, 1, %1" : "=v"(s1) : "v"(w));
+    asm("v_lshrrev_b64 %0, 1, %1" : "=v"(s2) : "v"(w));
+    const uint32_t s1a = (uint32_t)s1, s1b = (uint32_t)(s1 >> 32), s2a = (uint32_t)s2, s2b = (uint32_t)(s2 >> 32);
+    F4Frag f;
+    f.x = i32x4{(int)(s1a & K6), (int)(s2a & K6), (int)(s1b & K6), (int)(s2b & K6)};
+    if constexpr (WM) {
+        uint64_t w2;
+        asm("v_lshrrev_b64 %0, 2, %1" : "=v"(w2) : "v"(w));
+        const uint32_t w2a = (uint32_t)w2, w2b = (uint32_t)(w2 >> 32);
+        f.h = i32x4{(int)(wa & M), (int)(w2a & M), (int)(wb & M), (int)(w2b & M)};
+        f.o = i32x4{(int)(s1a & ~wa & M), (int)(s2a & ~w2a & M), (int)(s1b & ~wb & M), (int)(s2b & ~w2b & M)};
+    } else {
+        f.h = i32x4{(int)(s1a & M4), (int)(s2a & M4), (int)(s1b & M4), (int)(s2b & M4)};
+        f.o = i32x4{0, 0, 0, 0};
+    }
+    return f;
+}
+
 template <bool WM>
 __device__ __forceinline__ F4Frag decode_f4(uint32_t wa, uint32_t wb) {
     int x0, x1, x2, x3, h0, h1, h2, h3, o0, o1, o2, o3;
@@ -1852,41 +1880,46 @@ __device__ __forceinline__ void band_f4_body(BandI8Lds& sh, const int4 it, const
     // chunks [t_lo, t_hi), t_lo and t_hi even (rows are padded to 64 bytes).  Two chunk buffers: P holds
     // even chunks, Q odd ones; each is reloaded right after its last word is decoded and read again two K
     // steps later, with no register copies of loads in flight (those would force vmcnt(0)).
+    // the strips' decode: with 64-bit shifts in the additive-only column-pair loop (decode_f4_64)
+    auto dec = [](auto WMc, uint32_t wa, uint32_t wb) __attribute__((always_inline)) {
+        constexpr bool WM = decltype(WMc)::value;
+        if constexpr (NC == 2) return decode_f4_64<WM>(wa, wb);
+        else return decode_f4<WM>(wa, wb);
+    };
     auto kloop = [&](auto RMc, auto CMc, const int t_lo, const int t_hi) {
-        constexpr bool RM = decltype(RMc)::value, CM = decltype(CMc)::value;
         const int last = t_hi - 1;
         uint4 pr = rowp[CHUNK_U4 * t_lo], qr = rowp[CHUNK_U4 * (t_lo + 1)], pc[NC], qc[NC];
 #pragma unroll
         for (int c = 0; c < NC; ++c) { pc[c] = colp[c][CHUNK_U4 * t_lo]; qc[c] = colp[c][CHUNK_U4 * (t_lo + 1)]; }
         // two named fragment sets: set 1 is decoded while set 0 feeds the MFMAs and vice versa, so no
         // fragment is copied (a single rotating set costs ~12 v_mov per K step)
-        F4Frag a0 = decode_f4<RM>(pr.x, pr.y), a1, b0[NC], b1[NC];
+        F4Frag a0 = dec(RMc, pr.x, pr.y), a1, b0[NC], b1[NC];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(pc[c].x, pc[c].y);
+        for (int c = 0; c < NC; ++c) b0[c] = dec(CMc, pc[c].x, pc[c].y);
         for (int t = t_lo; t < t_hi; t += 2) {
-            a1 = decode_f4<RM>(pr.z, pr.w);
+            a1 = dec(RMc, pr.z, pr.w);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b1[c] = decode_f4<CM>(pc[c].z, pc[c].w);
+            for (int c = 0; c < NC; ++c) b1[c] = dec(CMc, pc[c].z, pc[c].w);
             mfmas_v(a0, b0, RMc, CMc);  // K step 2t   (chunk t, words 0-1)
             pr = rowp[CHUNK_U4 * min(t + 2, last)];
 #pragma unroll
             for (int c = 0; c < NC; ++c) pc[c] = colp[c][CHUNK_U4 * min(t + 2, last)];
             NLDSC_LOAD_FENCE();
-            a0 = decode_f4<RM>(qr.x, qr.y);
+            a0 = dec(RMc, qr.x, qr.y);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(qc[c].x, qc[c].y);
+            for (int c = 0; c < NC; ++c) b0[c] = dec(CMc, qc[c].x, qc[c].y);
             mfmas_v(a1, b1, RMc, CMc);  // K step 2t+1 (chunk t, words 2-3)
-            a1 = decode_f4<RM>(qr.z, qr.w);
+            a1 = dec(RMc, qr.z, qr.w);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b1[c] = decode_f4<CM>(qc[c].z, qc[c].w);
+            for (int c = 0; c < NC; ++c) b1[c] = dec(CMc, qc[c].z, qc[c].w);
             mfmas_v(a0, b0, RMc, CMc);  // K step 2t+2 (chunk t+1, words 0-1)
             qr = rowp[CHUNK_U4 * min(t + 3, last)];
 #pragma unroll
             for (int c = 0; c < NC; ++c) qc[c] = colp[c][CHUNK_U4 * min(t + 3, last)];
             NLDSC_LOAD_FENCE();
-            a0 = decode_f4<RM>(pr.x, pr.y);
+            a0 = dec(RMc, pr.x, pr.y);
 #pragma unroll
-            for (int c = 0; c < NC; ++c) b0[c] = decode_f4<CM>(pc[c].x, pc[c].y);
+            for (int c = 0; c < NC; ++c) b0[c] = dec(CMc, pc[c].x, pc[c].y);
             mfmas_v(a1, b1, RMc, CMc);  // K step 2t+3 (chunk t+1, words 2-3)
         }
     };
