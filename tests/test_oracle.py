@@ -169,3 +169,42 @@ def test_rare_variant_residual_noise(n_org):
     # SNPs with <= 2 genotypes of any other kind: the reference's fp32 residual is exactly 0 as well
     two = ((cnt[:, [0, 2, 3]] > 0).sum(1) <= 2) & ~flagged & ~np.isnan(orc["residuals_std"])
     assert two.sum() > 20 and (orc["residuals_std"][two] == 0).all()
+
+
+@pytest.mark.parametrize("name", ["n1000", "n1003"])
+def test_pair_r2_f64_sums_to_the_truth(name):
+    """oracle.pair_r2_f64 (the WSDE tie audit's per-pair exact r2adj) agrees with the fp64 truth it is cut from: its
+    pairs sum to L2 - 1 and L2D, count WSA / WSD, and its pairs above rsq_thr count WSDE, on every SNP."""
+    bed, pos, meta, _, f64 = load_set(name)
+    M, N = meta["n_snp"], meta["n_org"]
+    rows = np.frombuffer(bed, np.uint8, offset=3).reshape(M, -1)
+    js = np.arange(M)
+    pairs = O.pair_r2_f64(rows, N, meta["ld_wind"], meta["maf"], meta["std_thr"], pos, js, bed=bed)
+    for j, p in zip(js, pairs):
+        if p is None:
+            assert f64["l2_ws"][j] == -1
+            continue
+        ks, r2a, kds, r2d = p
+        assert len(ks) == f64["l2_ws"][j] and len(kds) == f64["l2d_ws"][j]
+        assert int((r2d > meta["rsq_thr"]).sum()) == f64["l2d_wse"][j]
+        np.testing.assert_allclose(1.0 + r2a.sum(), f64["l2"][j], rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(r2d.sum(), f64["l2d"][j], rtol=1e-10, atol=1e-10)
+
+
+def test_wsde_tie_audit_rules():
+    """conftest.wsde_tie_audit: a difference is accepted only on a SNP holding a pair within 1e-6 of rsq_thr, by at most
+    1, and the side named exact must equal the exact count there."""
+    from conftest import wsde_tie_audit
+    thr = 1e-3
+    exact_pairs = {0: (None, None, None, np.array([thr + 5e-7, 0.5])),   # a tie: 2 pairs above
+                   1: (None, None, None, np.array([thr + 1e-3, 0.5]))}   # no tie
+    pairs = lambda js: [exact_pairs[int(j)] for j in js]  # noqa: E731
+    rec = wsde_tie_audit(np.array([1, 5]), np.array([2, 5]), pairs, thr, exact="b")
+    assert rec["flips"] == 1 and rec["snps"] == [0] and rec["ties_1e6"] == [1]
+    with pytest.raises(AssertionError, match="no pair within"):
+        wsde_tie_audit(np.array([3, 4]), np.array([3, 5]), pairs, thr)
+    with pytest.raises(AssertionError, match="more than 1"):
+        wsde_tie_audit(np.array([0, 5]), np.array([2, 5]), pairs, thr)
+    with pytest.raises(AssertionError, match="exact WSDE"):
+        wsde_tie_audit(np.array([1, 5]), np.array([2, 5]), pairs, thr, exact="a")
+    assert wsde_tie_audit(np.array([1, 5]), np.array([1, 5]), pairs, thr)["flips"] == 0
